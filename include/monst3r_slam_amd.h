@@ -1,0 +1,164 @@
+/*
+ * monst3r_slam_amd.h — C ABI of the MI355X-native MonST3R/MASt3R-SLAM hot path.
+ *
+ * Plain pointers, sizes and scalars only (no torch types). Every pointer named
+ * `d_*` is a DEVICE pointer (HBM, hipMalloc'd or a torch CUDA tensor's data_ptr);
+ * `stream` is a hipStream_t passed as void* (NULL = legacy default stream, which is
+ * what the reference launches on: matching_kernels.cu:104,303; gn_kernels.cu:767,...).
+ * All tensors are dense, C-contiguous, in the reference's layouts (cited per call).
+ * Calls are asynchronous on `stream` unless the comment says otherwise.
+ *
+ * Return value: M3S_OK (0) or a negative M3S_ERR_* code; m3s_status_string() names it.
+ * The Python drop-in (monst3r-slam_amd/mast3r_slam_backends) maps non-zero to
+ * RuntimeError, like the reference's TORCH_CHECK (gn.h:5, gn.cpp:14-21,92-94,108-110).
+ *
+ * Numerical model (shared with oracle/):
+ *   - iter_proj: the reference source taken literally — f32 ops, no FMA contraction,
+ *     double-promoted sub-expressions (`1.0/x`, `(1.0-du)*dv`, `lambda*=0.1`) in f64.
+ *   - refine_matches: c10::Half arithmetic (Half-inl.h operator*, operator+=):
+ *     each product and each partial sum rounded to f16 (RNE), k = 0..F-1 in order;
+ *     initial best score = value-initialised half (+0.0) — see DESIGN.md.
+ */
+#ifndef MONST3R_SLAM_AMD_H
+#define MONST3R_SLAM_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  M3S_OK = 0,
+  M3S_ERR_INVALID_ARG = -1,   /* null pointer / bad size (reference: TORCH_CHECK) */
+  M3S_ERR_HIP = -2,           /* a HIP runtime call or kernel launch failed        */
+  M3S_ERR_TOO_LARGE = -3,     /* a size exceeds a kernel's static capacity          */
+  M3S_ERR_NOT_PD = -4,        /* Cholesky failed; reference semantics kept (zero step) */
+  M3S_ERR_NO_DEVICE = -5
+};
+
+const char* m3s_status_string(int status);
+int m3s_version(void);                 /* (major<<16)|(minor<<8)|patch */
+int m3s_device_count(void);
+
+/* ------------------------------------------------------------------------- *
+ * Projective matching.
+ * ------------------------------------------------------------------------- */
+
+/* Replaces mast3r_slam_backends.iter_proj  (gn.cpp:84-99 → matching_kernels.cu:279-316,
+ * kernel :119-275).  rays_img_with_grad f32[b,h,w,c] (c = 9: ray xyz, d/dx xyz, d/dy xyz),
+ * pts_3d_norm f32[b,n,3], p_init f32[b,n,2]  →  p_new f32[b,n,2], converged u8[b,n].
+ * Any n ≥ 0 (the reference needs n % 16 == 0 — it has no tail guard). */
+int m3s_iter_proj(const float* d_rays_img_with_grad, const float* d_pts_3d_norm,
+                  const float* d_p_init, float* d_p_new, uint8_t* d_converged,
+                  int64_t b, int64_t h, int64_t w, int64_t n,
+                  int max_iter, float lambda_init, float cost_thresh, void* stream);
+
+/* Replaces mast3r_slam_backends.refine_matches (gn.cpp:101-114 → matching_kernels.cu:84-116,
+ * kernel :25-81).  D11 f16[b,h,w,fdim], D21 f16[b,n,fdim] (raw IEEE half bits),
+ * p1 i64[b,n,2] (u,v)  →  p1_new i64[b,n,2].  fdim ≤ 64. */
+int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21, const int64_t* d_p1,
+                       int64_t* d_p1_new, int64_t b, int64_t h, int64_t w, int64_t n,
+                       int64_t fdim, int radius, int dilation_max, void* stream);
+
+/* Fused replacement for matching.prep_for_iter_proj (matching.py:25-49) and
+ * image.img_gradient (image.py:5-38): rays = X11/max(|X11|,1e-12);
+ * g{x,y} = 3×3 Scharr/32 on reflect-padded rays;  pts = X21/max(|X21|,1e-12);
+ * p_init = (idx % w, idx / w) (identity when d_idx_init == NULL).
+ * X11,X21 f32[b,h,w,3] → rays_with_grad f32[b,h,w,9], pts f32[b,h*w,3], p_init f32[b,h*w,2]. */
+int m3s_match_prep(const float* d_X11, const float* d_X21, const int64_t* d_idx_init,
+                   float* d_rays_with_grad, float* d_pts_norm, float* d_p_init,
+                   int64_t b, int64_t h, int64_t w, void* stream);
+
+/* Occlusion test + truncation of matching.match_iterative_proj (matching.py:67-76):
+ * p1 = trunc(p) (int64); valid = converged & (|X11[b,p1v,p1u] - X21[b,n]| < dist_thresh).
+ * p f32[b,n,2], converged u8[b,n] → p1 i64[b,n,2], valid u8[b,n]. */
+int m3s_match_occlusion(const float* d_X11, const float* d_X21, const float* d_p,
+                        const uint8_t* d_converged, int64_t* d_p1, uint8_t* d_valid,
+                        int64_t b, int64_t h, int64_t w, float dist_thresh, void* stream);
+
+/* pixel_to_lin (matching.py:13-15,88): idx = u + w*v.  p1 i64[b,n,2] → idx i64[b,n]. */
+int m3s_pixel_to_lin(const int64_t* d_p1, int64_t* d_idx, int64_t b, int64_t n, int64_t w,
+                     void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Backend Gauss-Newton over the keyframe graph (gn_kernels.cu).
+ * Twc f32[P,8] (t xyz, q xyzw, s — lietorch Sim3 layout) is UPDATED IN PLACE, exactly
+ * like the reference (gn_kernels.cu:1212 pose_retr_kernel writes Twc).  ii,jj i64[E]
+ * are global keyframe ids; Twc/Xs/Cs are indexed by rank in sorted unique(ii ∪ jj)
+ * (gn_kernels.cu:161-170); the rank-0 pose is fixed (num_fix = 1, :1157).
+ * Xs f32[P,N,3], Cs f32[P,N,1], idx_ii2jj i64[E,N], valid_match u8[E,N,1], Q f32[E,N,1].
+ * dx_out f32[P-1,7] receives the last step (the reference's return value).
+ * The solve (Eigen SimplicialLLT on the host in the reference, :57-159) runs on the
+ * GPU in fp64; no host round trip and no per-iteration sync.  If the Cholesky fails
+ * the step is zero (reference :142-150) and M3S_ERR_NOT_PD is reported through
+ * *h_status_out after the call completes (it is written by a final D2H copy; the call
+ * synchronises `stream` only when h_status_out != NULL).
+ * workspace: d_workspace of m3s_gn_workspace_bytes(P, E) bytes (device).
+ * ------------------------------------------------------------------------- */
+size_t m3s_gn_workspace_bytes(int64_t num_poses, int64_t num_edges);
+
+/* Replaces mast3r_slam_backends.gauss_newton_rays (gn.cpp:28-50 → gn_kernels.cu:1140-1228). */
+int m3s_gauss_newton_rays(float* d_Twc, const float* d_Xs, const float* d_Cs,
+                          const int64_t* d_ii, const int64_t* d_jj, const int64_t* d_idx_ii2jj,
+                          const uint8_t* d_valid_match, const float* d_Q,
+                          int64_t num_poses, int64_t num_points, int64_t num_edges,
+                          float sigma_ray, float sigma_dist, float C_thresh, float Q_thresh,
+                          int max_iter, float delta_thresh, float* d_dx_out,
+                          void* d_workspace, int* h_status_out, void* stream);
+
+/* Replaces mast3r_slam_backends.gauss_newton_calib (gn.cpp:52-82 → gn_kernels.cu:1546-1638).
+ * K f32[3,3] (device). */
+int m3s_gauss_newton_calib(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
+                           const int64_t* d_ii, const int64_t* d_jj, const int64_t* d_idx_ii2jj,
+                           const uint8_t* d_valid_match, const float* d_Q,
+                           int64_t num_poses, int64_t num_points, int64_t num_edges,
+                           int height, int width, int pixel_border, float z_eps,
+                           float sigma_pixel, float sigma_depth, float C_thresh, float Q_thresh,
+                           int max_iter, float delta_thresh, float* d_dx_out,
+                           void* d_workspace, int* h_status_out, void* stream);
+
+/* Replaces mast3r_slam_backends.gauss_newton_points (gn.cpp:3-26 → gn_kernels.cu:725-811). */
+int m3s_gauss_newton_points(float* d_Twc, const float* d_Xs, const float* d_Cs,
+                            const int64_t* d_ii, const int64_t* d_jj, const int64_t* d_idx_ii2jj,
+                            const uint8_t* d_valid_match, const float* d_Q,
+                            int64_t num_poses, int64_t num_points, int64_t num_edges,
+                            float sigma_point, float C_thresh, float Q_thresh,
+                            int max_iter, float delta_thresh, float* d_dx_out,
+                            void* d_workspace, int* h_status_out, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Frontend tracker: 7-dof Sim3 Gauss-Newton of FrameTracker2.opt_pose_ray_dist_sim3
+ * (tracker2.py:316-357, solve :299-314, check_convergence nonlinear_optimizer.py:5-25)
+ * and opt_pose_calib_sim3 (tracker2.py:359-409), fused: residual + Jacobian + Huber
+ * weights + 7×7 normal equations per point, reduced on device; 7×7 Cholesky, lietorch
+ * left retraction and the convergence test on device (no .item() per iteration).
+ * Twc_k, Twc_f f32[8] (lietorch Sim3 data).  Xf, Xk f32[N,3]; Qk f32[N]; valid u8[N].
+ * Out: T_WCf f32[8] and T_CkCf f32[8] (device), info i32[4] (device):
+ *   info[0] iterations run, info[1] 1 if Cholesky failed (frame lost, tracker2.py:234),
+ *   info[2] 1 if converged.
+ * workspace: m3s_track_workspace_bytes(N) bytes.
+ * ------------------------------------------------------------------------- */
+size_t m3s_track_workspace_bytes(int64_t n);
+
+int m3s_track_rays(const float* d_Twc_k, const float* d_Twc_f, const float* d_Xf,
+                   const float* d_Xk, const float* d_Qk, const uint8_t* d_valid, int64_t n,
+                   float sigma_ray, float sigma_dist, float huber_k, int max_iters,
+                   float rel_error, float delta_norm, float* d_T_WCf_out, float* d_T_CkCf_out,
+                   int* d_info, void* d_workspace, void* stream);
+
+/* Calibrated variant.  K f32[3,3] device; n points; img h,w; meas_k f32[n,3];
+ * valid_meas_k u8[n]. */
+int m3s_track_calib(const float* d_Twc_k, const float* d_Twc_f, const float* d_Xf,
+                    const float* d_Qk, const uint8_t* d_valid, const float* d_meas_k,
+                    const uint8_t* d_valid_meas_k, const float* d_K, int64_t n, int64_t h, int64_t w,
+                    float sigma_pixel, float sigma_depth, float huber_k, float pixel_border,
+                    float depth_eps, int max_iters, float rel_error, float delta_norm,
+                    float* d_T_WCf_out, float* d_T_CkCf_out, int* d_info, void* d_workspace,
+                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MONST3R_SLAM_AMD_H */

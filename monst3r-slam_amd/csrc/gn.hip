@@ -1,0 +1,572 @@
+// Backend Gauss-Newton over the keyframe graph, gfx950.
+//
+// Reference: gn_kernels.cu (ray_align_kernel :813-1138, calib_proj_kernel :1231-1543,
+// point_align_kernel :455-723, drivers :725-811/:1140-1228/:1546-1638, Eigen host solve
+// :57-159).  MI355X design:
+//  * Algebra: every residual row has Ji = -Jj and Jj = M_i J' (M_i the reference's
+//    apply_Sim3_adj_inv of pose i, linear in J').  So the 14x14 edge Hessian is
+//    [[A,-A],[-A,A]] with A = M_i (sum w J'J'^T) M_i^T and g = (-M_i v', M_i v').
+//    Per point we accumulate 28 + 7 f32 sums (not 105 + 14) and apply M_i once per
+//    edge in f64 — the same quantity as the reference up to summation order.
+//  * Parallelism: grid (E, S) — each edge's points split over S workgroups so that
+//    E*S fills the 256 CUs; wave64 butterfly + LDS reduction per workgroup.
+//  * Solve: a single-workgroup fp64 kernel assembles the dense 7(P-1) system, runs a
+//    right-looking Cholesky, the two triangular solves, the retraction of poses 1..P-1
+//    and the ||dx|| < delta test — all on device, no host round trip.  A device flag
+//    makes later iterations' kernels exit at once, so max_iter launches need no sync.
+#include "common.h"
+#include "sim3.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kEdgeThreads = 256;
+constexpr int kSolveThreads = 1024;
+constexpr int kAcc = 35;  // 28 upper-tri of sum w J'J'^T + 7 of sum w e J'
+
+enum : int { MODE_RAYS = 0, MODE_CALIB = 1, MODE_POINTS = 2 };
+
+struct GnParams {
+  float s0_inv, s1_inv;  // sigma_ray_inv/sigma_dist_inv, pixel/depth, point/-
+  float C_thresh, Q_thresh;
+  int height, width, pixel_border;
+  float z_eps;
+};
+
+struct GnWork {
+  int* flags;          // [0] done, [1] not-PD seen, [2] unique count, [3] iterations
+  int* rank_ii;        // [E]
+  int* rank_jj;        // [E]
+  float* partial;      // [E][S][kAcc]
+  double* A;           // [n][n]
+  double* bvec;        // [n]
+  double* G;           // [E][kAcc] reduced per edge (scratch for the solve kernel)
+};
+
+__device__ __forceinline__ float huber_ref(float r) {
+  // gn_kernels.cu:172-175 (constant hard-coded, compared and divided in double)
+  const float r_abs = fabsf(r);
+  return (double)r_abs < 1.345 ? 1.0f : (float)(1.345 / (double)r_abs);
+}
+
+__device__ __forceinline__ float inv_ref(float x) { return (float)(1.0 / (double)x); }
+
+// Accumulate one weighted row into the 35 sums.
+__device__ __forceinline__ void acc_row(float* acc, float w, float e, const float* J) {
+  int l = 0;
+#pragma unroll
+  for (int n = 0; n < 7; n++) {
+    const float wj = w * J[n];
+#pragma unroll
+    for (int m = 0; m <= n; m++) {
+      acc[l] += wj * J[m];
+      l++;
+    }
+  }
+  const float we = w * e;
+#pragma unroll
+  for (int n = 0; n < 7; n++) acc[28 + n] += we * J[n];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kEdgeThreads) void gn_edge_kernel(
+    const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
+    const float* __restrict__ K, const int* __restrict__ rank_ii,
+    const int* __restrict__ rank_jj, const int64_t* __restrict__ idx_ii2jj,
+    const uint8_t* __restrict__ valid_match, const float* __restrict__ Q,
+    float* __restrict__ partial, const int* __restrict__ flags, int64_t num_points, int S,
+    GnParams prm) {
+  if (flags[0]) return;  // converged in an earlier iteration
+  const int e = blockIdx.x;
+  const int s = blockIdx.y;
+  const int ix = rank_ii[e], jx = rank_jj[e];
+  const float* Ti = Twc + 8 * ix;
+  const float* Tj = Twc + 8 * jx;
+  float tij[3], qij[4], sij;
+  m3s_rel_sim3<float>(Ti, Ti + 3, Ti[7], Tj, Tj + 3, Tj[7], tij, qij, &sij);
+  float fx = 0.f, fy = 0.f, cx = 0.f, cy = 0.f;
+  if (MODE == MODE_CALIB) {
+    fx = K[0];
+    fy = K[4];
+    cx = K[2];
+    cy = K[5];
+  }
+
+  float acc[kAcc];
+#pragma unroll
+  for (int l = 0; l < kAcc; l++) acc[l] = 0.f;
+
+  const int64_t chunk = (num_points + S - 1) / S;
+  const int64_t k0 = (int64_t)s * chunk;
+  const int64_t k1 = min(num_points, k0 + chunk);
+  const float* Xi_base = Xs + (int64_t)ix * num_points * 3;
+  const float* Xj_base = Xs + (int64_t)jx * num_points * 3;
+  const float* Ci_base = Cs + (int64_t)ix * num_points;
+  const float* Cj_base = Cs + (int64_t)jx * num_points;
+  const int64_t eoff = (int64_t)e * num_points;
+
+  for (int64_t k = k0 + threadIdx.x; k < k1; k += kEdgeThreads) {
+    const bool vm = valid_match[eoff + k] != 0;
+    const int64_t ind = vm ? idx_ii2jj[eoff + k] : 0;
+    const float Xi[3] = {Xi_base[3 * ind], Xi_base[3 * ind + 1], Xi_base[3 * ind + 2]};
+    const float Xj[3] = {Xj_base[3 * k], Xj_base[3 * k + 1], Xj_base[3 * k + 2]};
+    float P[3];
+    m3s_act_sim3<float>(tij, qij, sij, Xj, P);
+    const float q = Q[eoff + k];
+    const float ci = Ci_base[ind];
+    const float cj = Cj_base[k];
+    bool valid = vm & (q > prm.Q_thresh) & (ci > prm.C_thresh) & (cj > prm.C_thresh);
+
+    if (MODE == MODE_RAYS) {
+      const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
+      const float n1i = sqrtf(n2i);
+      const float n1i_inv = inv_ref(n1i);
+      const float n2j = P[0] * P[0] + P[1] * P[1] + P[2] * P[2];
+      const float n1j = sqrtf(n2j);
+      const float n1j_inv = inv_ref(n1j);
+      const float rj[3] = {n1j_inv * P[0], n1j_inv * P[1], n1j_inv * P[2]};
+      const float err[4] = {rj[0] - n1i_inv * Xi[0], rj[1] - n1i_inv * Xi[1],
+                            rj[2] - n1i_inv * Xi[2], n1j - n1i};
+      const float sq = sqrtf(q);
+      const float swr = valid ? prm.s0_inv * sq : 0.f;
+      const float swd = valid ? prm.s1_inv * sq : 0.f;
+      const float cr = swr * swr, cd = swd * swd;
+      const float w[4] = {huber_ref(swr * err[0]) * cr, huber_ref(swr * err[1]) * cr,
+                          huber_ref(swr * err[2]) * cr, huber_ref(swd * err[3]) * cd};
+      const float n3_inv = n1j_inv / n2j;
+      const float dxx = n1j_inv - P[0] * P[0] * n3_inv;
+      const float dyy = n1j_inv - P[1] * P[1] * n3_inv;
+      const float dzz = n1j_inv - P[2] * P[2] * n3_inv;
+      const float dxy = -P[0] * P[1] * n3_inv;
+      const float dxz = -P[0] * P[2] * n3_inv;
+      const float dyz = -P[1] * P[2] * n3_inv;
+      const float J0[7] = {dxx, dxy, dxz, 0.f, rj[2], -rj[1], 0.f};
+      const float J1[7] = {dxy, dyy, dyz, -rj[2], 0.f, rj[0], 0.f};
+      const float J2[7] = {dxz, dyz, dzz, rj[1], -rj[0], 0.f, 0.f};
+      const float J3[7] = {rj[0], rj[1], rj[2], 0.f, 0.f, 0.f, n1j};
+      acc_row(acc, w[0], err[0], J0);
+      acc_row(acc, w[1], err[1], J1);
+      acc_row(acc, w[2], err[2], J2);
+      acc_row(acc, w[3], err[3], J3);
+    } else if (MODE == MODE_CALIB) {
+      const int u_t = (int)(ind % prm.width);
+      const int v_t = (int)(ind / prm.width);
+      const bool valid_z = (P[2] > prm.z_eps) && (Xi[2] > prm.z_eps);
+      const float zj_inv = valid_z ? inv_ref(P[2]) : 0.f;
+      const float zj_log = valid_z ? logf(P[2]) : 0.f;
+      const float zi_log = valid_z ? logf(Xi[2]) : 0.f;
+      const float xz = P[0] * zj_inv;
+      const float yz = P[1] * zj_inv;
+      const float u = fx * xz + cx;
+      const float v = fy * yz + cy;
+      const bool valid_u = (u > (float)prm.pixel_border) &&
+                           (u < (float)(prm.width - 1 - prm.pixel_border));
+      const bool valid_v = (v > (float)prm.pixel_border) &&
+                           (v < (float)(prm.height - 1 - prm.pixel_border));
+      valid = valid & valid_u & valid_v & valid_z;
+      const float err[3] = {u - (float)u_t, v - (float)v_t, zj_log - zi_log};
+      const float sq = sqrtf(q);
+      const float swp = valid ? prm.s0_inv * sq : 0.f;
+      const float swd = valid ? prm.s1_inv * sq : 0.f;
+      const float cp = swp * swp, cd = swd * swd;
+      const float w[3] = {huber_ref(swp * err[0]) * cp, huber_ref(swp * err[1]) * cp,
+                          huber_ref(swd * err[2]) * cd};
+      const float J0[7] = {fx * zj_inv, 0.f, -fx * xz * zj_inv, -fx * xz * yz,
+                           fx * (1.f + xz * xz), -fx * yz, 0.f};
+      const float J1[7] = {0.f, fy * zj_inv, -fy * yz * zj_inv, -fy * (1.f + yz * yz),
+                           fy * xz * yz, fy * xz, 0.f};
+      const float J2[7] = {0.f, 0.f, zj_inv, yz, -xz, 0.f, 1.f};
+      acc_row(acc, w[0], err[0], J0);
+      acc_row(acc, w[1], err[1], J1);
+      acc_row(acc, w[2], err[2], J2);
+    } else {  // MODE_POINTS
+      const float err[3] = {P[0] - Xi[0], P[1] - Xi[1], P[2] - Xi[2]};
+      const float swp = valid ? prm.s0_inv * sqrtf(q) : 0.f;
+      const float cp = swp * swp;
+      const float w[3] = {huber_ref(swp * err[0]) * cp, huber_ref(swp * err[1]) * cp,
+                          huber_ref(swp * err[2]) * cp};
+      const float J0[7] = {1.f, 0.f, 0.f, 0.f, P[2], -P[1], P[0]};
+      const float J1[7] = {0.f, 1.f, 0.f, -P[2], 0.f, P[0], P[1]};
+      const float J2[7] = {0.f, 0.f, 1.f, P[1], -P[0], 0.f, P[2]};
+      acc_row(acc, w[0], err[0], J0);
+      acc_row(acc, w[1], err[1], J1);
+      acc_row(acc, w[2], err[2], J2);
+    }
+  }
+
+  // workgroup reduction: wave butterfly, then 4 waves through LDS
+  __shared__ float red[kEdgeThreads / M3S_WAVE][kAcc];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int l = 0; l < kAcc; l++) {
+    const float v = m3s_wave_sum(acc[l]);
+    if (lane == 0) red[wid][l] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kAcc) {
+    float v = red[0][threadIdx.x];
+#pragma unroll
+    for (int wv = 1; wv < kEdgeThreads / M3S_WAVE; wv++) v += red[wv][threadIdx.x];
+    partial[((int64_t)e * S + s) * kAcc + threadIdx.x] = v;
+  }
+}
+
+// ranks of ii/jj in sorted unique(ii ∪ jj) (gn_kernels.cu:161-170, torch::_unique +
+// searchsorted).  Single workgroup, O(M^2) over M = 2E values held in global memory.
+__global__ __launch_bounds__(kSolveThreads) void gn_rank_kernel(const int64_t* __restrict__ ii,
+                                                               const int64_t* __restrict__ jj,
+                                                               int E, int* __restrict__ rank_ii,
+                                                               int* __restrict__ rank_jj,
+                                                               int* __restrict__ flags) {
+  const int M = 2 * E;  // E <= 65535 → M < 2^17 bits = 16 KiB of LDS
+  __shared__ unsigned first_bits[(2 * 65536) / 32];
+  __shared__ int s_unique;
+  if (threadIdx.x == 0) s_unique = 0;
+  for (int wd = threadIdx.x; wd < (M + 31) / 32; wd += blockDim.x) first_bits[wd] = 0u;
+  __syncthreads();
+  // pass 1: is position p the first occurrence of its value?
+  int local_unique = 0;
+  for (int p = threadIdx.x; p < M; p += blockDim.x) {
+    const int64_t v = p < E ? ii[p] : jj[p - E];
+    bool first = true;
+    for (int q = 0; q < p && first; q++) {
+      const int64_t u = q < E ? ii[q] : jj[q - E];
+      first = (u != v);
+    }
+    if (first) {
+      atomicOr(&first_bits[p >> 5], 1u << (p & 31));
+      local_unique++;
+    }
+  }
+  atomicAdd(&s_unique, local_unique);
+  __syncthreads();
+  // pass 2: rank = number of distinct values below v
+  for (int p = threadIdx.x; p < M; p += blockDim.x) {
+    const int64_t v = p < E ? ii[p] : jj[p - E];
+    int rank = 0;
+    for (int q = 0; q < M; q++) {
+      const int64_t u = q < E ? ii[q] : jj[q - E];
+      rank += ((u < v) && ((first_bits[q >> 5] >> (q & 31)) & 1u)) ? 1 : 0;
+    }
+    if (p < E) rank_ii[p] = rank;
+    else rank_jj[p - E] = rank;
+  }
+  if (threadIdx.x == 0) flags[2] = s_unique;
+}
+
+__device__ __forceinline__ int tri_idx(int n, int m) {  // n >= m
+  return n * (n + 1) / 2 + m;
+}
+
+// Single-workgroup fp64 assemble + Cholesky + solve + retraction + convergence.
+__global__ __launch_bounds__(kSolveThreads) void gn_solve_kernel(
+    float* __restrict__ Twc, const float* __restrict__ partial, const int* __restrict__ rank_ii,
+    const int* __restrict__ rank_jj, double* __restrict__ Ag, double* __restrict__ bg,
+    double* __restrict__ Gs, float* __restrict__ dx_out, int* __restrict__ flags, int E, int S,
+    int P, float delta_thresh) {
+  if (flags[0]) return;
+  const int tid = threadIdx.x;
+  const int n = 7 * (P - 1);
+  const int nt = blockDim.x;
+
+  // 1) reduce the S partials of every edge (fixed order, f64)
+  for (int idx = tid; idx < E * kAcc; idx += nt) {
+    const int e = idx / kAcc, l = idx % kAcc;
+    double v = 0.0;
+    for (int s = 0; s < S; s++) v += (double)partial[((int64_t)e * S + s) * kAcc + l];
+    Gs[idx] = v;
+  }
+  for (int idx = tid; idx < n * n; idx += nt) Ag[idx] = 0.0;
+  for (int idx = tid; idx < n; idx += nt) bg[idx] = 0.0;
+  __syncthreads();
+
+  // 2) per edge: A = M G M^T, vj = M v' (M from pose i), scatter into the system.
+  __shared__ double sM[7][7];
+  __shared__ double sG[7][7];
+  __shared__ double sT[7][7];
+  __shared__ double sA[7][7];
+  __shared__ double sv[7];
+  for (int e = 0; e < E; e++) {
+    const int ix = rank_ii[e], jx = rank_jj[e];
+    if (tid < 7) {
+      // column tid of M = M applied to unit vector e_tid (M is linear, f64)
+      const float* Ti = Twc + 8 * ix;
+      const double t[3] = {Ti[0], Ti[1], Ti[2]};
+      const double q[4] = {Ti[3], Ti[4], Ti[5], Ti[6]};
+      const double s = Ti[7];
+      double X[7] = {0, 0, 0, 0, 0, 0, 0};
+      X[tid] = 1.0;
+      double Y[7];
+      m3s_adj_inv_apply<double>(t, q, s, X, Y);
+      for (int r = 0; r < 7; r++) sM[r][tid] = Y[r];
+    } else if (tid >= 64 && tid < 64 + 49) {
+      const int r = (tid - 64) / 7, c = (tid - 64) % 7;
+      sG[r][c] = Gs[e * kAcc + (r >= c ? tri_idx(r, c) : tri_idx(c, r))];
+    }
+    __syncthreads();
+    if (tid < 49) {  // T = M G
+      const int r = tid / 7, c = tid % 7;
+      double v = 0.0;
+      for (int k = 0; k < 7; k++) v += sM[r][k] * sG[k][c];
+      sT[r][c] = v;
+    } else if (tid >= 64 && tid < 71) {  // vj = M v'
+      const int r = tid - 64;
+      double v = 0.0;
+      for (int k = 0; k < 7; k++) v += sM[r][k] * Gs[e * kAcc + 28 + k];
+      sv[r] = v;
+    }
+    __syncthreads();
+    if (tid < 49) {  // A = T M^T
+      const int r = tid / 7, c = tid % 7;
+      double v = 0.0;
+      for (int k = 0; k < 7; k++) v += sT[r][k] * sM[c][k];
+      sA[r][c] = v;
+    }
+    __syncthreads();
+    // scatter: Hii += A, Hij -= A, Hji -= A, Hjj += A; b_i += -vj, b_j += vj
+    // (one thread per entry handles all four blocks in order: no race even if i == j)
+    const int oi = ix - 1, oj = jx - 1;  // rank 0 is the fixed pose
+    if (tid < 49) {
+      const int r = tid / 7, c = tid % 7;
+      const double a = sA[r][c];
+      if (oi >= 0) Ag[(int64_t)(7 * oi + r) * n + 7 * oi + c] += a;
+      if (oi >= 0 && oj >= 0) Ag[(int64_t)(7 * oi + r) * n + 7 * oj + c] -= a;
+      if (oi >= 0 && oj >= 0) Ag[(int64_t)(7 * oj + r) * n + 7 * oi + c] -= a;
+      if (oj >= 0) Ag[(int64_t)(7 * oj + r) * n + 7 * oj + c] += a;
+    } else if (tid >= 64 && tid < 71) {
+      const int r = tid - 64;
+      if (oi >= 0) bg[7 * oi + r] -= sv[r];
+      if (oj >= 0) bg[7 * oj + r] += sv[r];
+    }
+    __syncthreads();
+  }
+
+  // 3) right-looking Cholesky, lower triangle in place (Eigen SimplicialLLT equivalent)
+  __shared__ int s_fail;
+  __shared__ double s_piv;
+  if (tid == 0) s_fail = 0;
+  __syncthreads();
+  for (int k = 0; k < n; k++) {
+    if (tid == 0) {
+      const double d = Ag[(int64_t)k * n + k];
+      if (!(d > 0.0)) s_fail = 1;
+      s_piv = sqrt(d);
+      Ag[(int64_t)k * n + k] = s_piv;
+    }
+    __syncthreads();
+    if (s_fail) break;
+    const double piv = s_piv;
+    for (int i = k + 1 + tid; i < n; i += nt) Ag[(int64_t)i * n + k] /= piv;
+    __syncthreads();
+    const int m = n - k - 1;  // trailing size
+    const int64_t tot = (int64_t)m * (m + 1) / 2;
+    for (int64_t idx = tid; idx < tot; idx += nt) {
+      // map idx -> (i, j) with k < j <= i < n  (row-major lower triangle)
+      int i = (int)((sqrt(8.0 * (double)idx + 1.0) - 1.0) * 0.5);
+      while ((int64_t)(i + 1) * (i + 2) / 2 <= idx) i++;
+      while ((int64_t)i * (i + 1) / 2 > idx) i--;
+      const int j = (int)(idx - (int64_t)i * (i + 1) / 2);
+      const int gi = k + 1 + i, gj = k + 1 + j;
+      Ag[(int64_t)gi * n + gj] -= Ag[(int64_t)gi * n + k] * Ag[(int64_t)gj * n + k];
+    }
+    __syncthreads();
+  }
+
+  // 4) solve L y = b, L^T x = y (column sweeps); x overwrites b.
+  if (!s_fail) {
+    for (int j = 0; j < n; j++) {
+      if (tid == 0) bg[j] /= Ag[(int64_t)j * n + j];
+      __syncthreads();
+      const double yj = bg[j];
+      for (int i = j + 1 + tid; i < n; i += nt) bg[i] -= Ag[(int64_t)i * n + j] * yj;
+      __syncthreads();
+    }
+    for (int j = n - 1; j >= 0; j--) {
+      if (tid == 0) bg[j] /= Ag[(int64_t)j * n + j];
+      __syncthreads();
+      const double xj = bg[j];
+      for (int i = tid; i < j; i += nt) bg[i] -= Ag[(int64_t)j * n + i] * xj;
+      __syncthreads();
+    }
+  }
+
+  // 5) dx = -x (f32, zero on failure: gn_kernels.cu:147-150), retract poses 1..P-1
+  for (int idx = tid; idx < n; idx += nt) dx_out[idx] = s_fail ? 0.f : (float)(-bg[idx]);
+  __syncthreads();
+  for (int p = 1 + tid; p < P; p += nt) {
+    float* T = Twc + 8 * p;
+    const float* xi = dx_out + 7 * (p - 1);
+    float t1[3], q1[4], s1;
+    m3s_retr_sim3<float>(xi, T, T + 3, T[7], t1, q1, &s1);
+    T[0] = t1[0];
+    T[1] = t1[1];
+    T[2] = t1[2];
+    T[3] = q1[0];
+    T[4] = q1[1];
+    T[5] = q1[2];
+    T[6] = q1[3];
+    T[7] = s1;
+  }
+  // 6) termination: ||dx|| < delta_thresh (gn_kernels.cu:1217-1222)
+  __shared__ float s_red[kSolveThreads / M3S_WAVE];
+  float ss = 0.f;
+  for (int idx = tid; idx < n; idx += nt) ss += dx_out[idx] * dx_out[idx];
+  ss = m3s_wave_sum(ss);
+  if ((tid & 63) == 0) s_red[tid >> 6] = ss;
+  __syncthreads();
+  if (tid == 0) {
+    float tot = 0.f;
+    for (int w = 0; w < nt / 64; w++) tot += s_red[w];
+    flags[3] += 1;
+    if (s_fail) flags[1] = 1;
+    if (sqrtf(tot) < delta_thresh) flags[0] = 1;
+  }
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int choose_splits(int64_t E, int64_t N) {
+  int64_t S = (2048 + E - 1) / E;
+  const int64_t max_by_points = (N + 1023) / 1024;  // >= ~1024 points per workgroup
+  if (S > max_by_points) S = max_by_points;
+  if (S < 1) S = 1;
+  if (S > 256) S = 256;
+  return (int)S;
+}
+
+struct Layout {
+  size_t flags, rank_ii, rank_jj, partial, A, b, G, total;
+};
+
+Layout make_layout(int64_t P, int64_t E, int S) {
+  Layout L;
+  const int64_t n = 7 * (P > 1 ? P - 1 : 0);
+  size_t off = 0;
+  L.flags = off;
+  off = align_up(off + 64, 256);
+  L.rank_ii = off;
+  off = align_up(off + 4 * E, 256);
+  L.rank_jj = off;
+  off = align_up(off + 4 * E, 256);
+  L.partial = off;
+  off = align_up(off + 4 * E * S * kAcc, 256);
+  L.A = off;
+  off = align_up(off + 8 * n * n, 256);
+  L.b = off;
+  off = align_up(off + 8 * n, 256);
+  L.G = off;
+  off = align_up(off + 8 * E * kAcc, 256);
+  L.total = off;
+  return L;
+}
+
+template <int MODE>
+int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
+           const int64_t* d_ii, const int64_t* d_jj, const int64_t* d_idx,
+           const uint8_t* d_valid, const float* d_Q, int64_t P, int64_t N, int64_t E,
+           GnParams prm, int max_iter, float delta_thresh, float* d_dx, void* d_ws,
+           int* h_status, void* stream) {
+  if (P < 1 || N < 1 || E < 1) return M3S_ERR_INVALID_ARG;
+  if (!d_Twc || !d_Xs || !d_Cs || !d_ii || !d_jj || !d_idx || !d_valid || !d_Q || !d_ws)
+    return M3S_ERR_INVALID_ARG;
+  if (MODE == MODE_CALIB && !d_K) return M3S_ERR_INVALID_ARG;
+  if (E > 65535 || 7 * P > 46000) return M3S_ERR_TOO_LARGE;
+  hipStream_t st = m3s_stream(stream);
+  const int S = choose_splits(E, N);
+  const Layout L = make_layout(P, E, S);
+  char* ws = reinterpret_cast<char*>(d_ws);
+  int* flags = reinterpret_cast<int*>(ws + L.flags);
+  int* rii = reinterpret_cast<int*>(ws + L.rank_ii);
+  int* rjj = reinterpret_cast<int*>(ws + L.rank_jj);
+  float* partial = reinterpret_cast<float*>(ws + L.partial);
+  double* A = reinterpret_cast<double*>(ws + L.A);
+  double* b = reinterpret_cast<double*>(ws + L.b);
+  double* G = reinterpret_cast<double*>(ws + L.G);
+  M3S_HIP_CHECK(hipMemsetAsync(flags, 0, 64, st));
+  if (P > 1) M3S_HIP_CHECK(hipMemsetAsync(d_dx, 0, sizeof(float) * 7 * (P - 1), st));
+  hipLaunchKernelGGL(gn_rank_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_ii, d_jj, (int)E, rii,
+                     rjj, flags);
+  M3S_LAUNCH_CHECK();
+  if (P > 1) {
+    for (int it = 0; it < max_iter; it++) {
+      hipLaunchKernelGGL(gn_edge_kernel<MODE>, dim3((unsigned)E, (unsigned)S),
+                         dim3(kEdgeThreads), 0, st, d_Twc, d_Xs, d_Cs, d_K, rii, rjj, d_idx,
+                         d_valid, d_Q, partial, flags, N, S, prm);
+      M3S_LAUNCH_CHECK();
+      hipLaunchKernelGGL(gn_solve_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_Twc, partial,
+                         rii, rjj, A, b, G, d_dx, flags, (int)E, S, (int)P, delta_thresh);
+      M3S_LAUNCH_CHECK();
+    }
+  }
+  if (h_status) {
+    int hflags[4] = {0, 0, 0, 0};
+    M3S_HIP_CHECK(hipMemcpyAsync(hflags, flags, sizeof(hflags), hipMemcpyDeviceToHost, st));
+    M3S_HIP_CHECK(hipStreamSynchronize(st));
+    if (hflags[2] != P) *h_status = M3S_ERR_INVALID_ARG;  // |unique(ii,jj)| != P
+    else *h_status = hflags[1] ? M3S_ERR_NOT_PD : M3S_OK;
+  }
+  return M3S_OK;
+}
+
+}  // namespace
+
+extern "C" size_t m3s_gn_workspace_bytes(int64_t num_poses, int64_t num_edges) {
+  if (num_poses < 1 || num_edges < 1) return 256;
+  // worst-case S for any N
+  const int S = choose_splits(num_edges, (int64_t)1 << 40);
+  return make_layout(num_poses, num_edges, S).total;
+}
+
+extern "C" int m3s_gauss_newton_rays(float* d_Twc, const float* d_Xs, const float* d_Cs,
+                                     const int64_t* d_ii, const int64_t* d_jj,
+                                     const int64_t* d_idx, const uint8_t* d_valid,
+                                     const float* d_Q, int64_t P, int64_t N, int64_t E,
+                                     float sigma_ray, float sigma_dist, float C_thresh,
+                                     float Q_thresh, int max_iter, float delta_thresh,
+                                     float* d_dx, void* d_ws, int* h_status, void* stream) {
+  GnParams prm{};
+  prm.s0_inv = (float)(1.0 / (double)sigma_ray);
+  prm.s1_inv = (float)(1.0 / (double)sigma_dist);
+  prm.C_thresh = C_thresh;
+  prm.Q_thresh = Q_thresh;
+  return run_gn<MODE_RAYS>(d_Twc, d_Xs, d_Cs, nullptr, d_ii, d_jj, d_idx, d_valid, d_Q, P, N, E,
+                           prm, max_iter, delta_thresh, d_dx, d_ws, h_status, stream);
+}
+
+extern "C" int m3s_gauss_newton_calib(float* d_Twc, const float* d_Xs, const float* d_Cs,
+                                      const float* d_K, const int64_t* d_ii, const int64_t* d_jj,
+                                      const int64_t* d_idx, const uint8_t* d_valid,
+                                      const float* d_Q, int64_t P, int64_t N, int64_t E,
+                                      int height, int width, int pixel_border, float z_eps,
+                                      float sigma_pixel, float sigma_depth, float C_thresh,
+                                      float Q_thresh, int max_iter, float delta_thresh,
+                                      float* d_dx, void* d_ws, int* h_status, void* stream) {
+  GnParams prm{};
+  prm.s0_inv = (float)(1.0 / (double)sigma_pixel);
+  prm.s1_inv = (float)(1.0 / (double)sigma_depth);
+  prm.C_thresh = C_thresh;
+  prm.Q_thresh = Q_thresh;
+  prm.height = height;
+  prm.width = width;
+  prm.pixel_border = pixel_border;
+  prm.z_eps = z_eps;
+  if (width < 1 || height < 1) return M3S_ERR_INVALID_ARG;
+  return run_gn<MODE_CALIB>(d_Twc, d_Xs, d_Cs, d_K, d_ii, d_jj, d_idx, d_valid, d_Q, P, N, E,
+                            prm, max_iter, delta_thresh, d_dx, d_ws, h_status, stream);
+}
+
+extern "C" int m3s_gauss_newton_points(float* d_Twc, const float* d_Xs, const float* d_Cs,
+                                       const int64_t* d_ii, const int64_t* d_jj,
+                                       const int64_t* d_idx, const uint8_t* d_valid,
+                                       const float* d_Q, int64_t P, int64_t N, int64_t E,
+                                       float sigma_point, float C_thresh, float Q_thresh,
+                                       int max_iter, float delta_thresh, float* d_dx, void* d_ws,
+                                       int* h_status, void* stream) {
+  GnParams prm{};
+  prm.s0_inv = (float)(1.0 / (double)sigma_point);
+  prm.C_thresh = C_thresh;
+  prm.Q_thresh = Q_thresh;
+  return run_gn<MODE_POINTS>(d_Twc, d_Xs, d_Cs, nullptr, d_ii, d_jj, d_idx, d_valid, d_Q, P, N,
+                             E, prm, max_iter, delta_thresh, d_dx, d_ws, h_status, stream);
+}

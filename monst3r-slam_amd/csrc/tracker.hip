@@ -1,0 +1,378 @@
+// Frontend pose tracker (FrameTracker2.opt_pose_ray_dist_sim3 / opt_pose_calib_sim3,
+// tracker2.py:299-409) as three gfx950 kernels per Gauss-Newton iteration-pair:
+//   track_points_kernel<MODE>: per point residual (4 rows ray+dist, or 3 rows u,v,log z),
+//     Jacobian J = -d(rd)/dP * [I, -[P]x, P], Huber-robust whitening, and the 28+7+1
+//     sums of A^T A, -A^T b and 0.5 b^T b; wave64 butterfly + LDS per workgroup.
+//   track_solve_kernel: one workgroup reduces the partials (f64, fixed order), 7x7
+//     Cholesky, tau = H^-1 g, T <- Exp(tau) * T (lietorch retr), check_convergence
+//     (nonlinear_optimizer.py:5-25, NaN-aware on iteration 0) and sets a done flag.
+// All max_iters iterations are enqueued without a host sync; once the flag is set the
+// remaining launches return at entry.
+#include "common.h"
+#include "sim3.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kBlocks = 512;
+constexpr int kAcc = 36;  // 28 H upper, 7 g, 1 cost
+
+enum : int { TRACK_RAYS = 0, TRACK_CALIB = 1 };
+
+struct TrackState {
+  float T[8];        // current T_CkCf
+  double old_cost;
+  int done, fail, iters, conv;
+};
+
+struct TrackParams {
+  float si0, si1;  // 1/sigma for the two residual groups
+  float huber_k;
+  float fx, fy, cx, cy;  // calib only (read from K on device in init)
+  float border, depth_eps;
+  int h, w;
+};
+
+__device__ __forceinline__ float huber_w(float r, float k) {
+  // nonlinear_optimizer.huber: 1 if |r| < k else k / |r|
+  const float a = fabsf(r);
+  return a < k ? 1.0f : k / a;
+}
+
+__device__ __forceinline__ void acc_row(float* acc, float ws, const float* J, float r) {
+  // A_row = ws * J_row, b = ws * r
+  float a[7];
+#pragma unroll
+  for (int n = 0; n < 7; n++) a[n] = ws * J[n];
+  const float bb = ws * r;
+  int l = 0;
+#pragma unroll
+  for (int n = 0; n < 7; n++) {
+#pragma unroll
+    for (int m = 0; m <= n; m++) {
+      acc[l] += a[n] * a[m];
+      l++;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < 7; n++) acc[28 + n] -= a[n] * bb;
+  acc[35] += 0.5f * bb * bb;
+}
+
+// J row = -(d row) * [I, -[P]x, P], with d = d(residual row)/dP (1x3)
+__device__ __forceinline__ void jac_row(const float* d, const float* P, float* J) {
+  J[0] = -d[0];
+  J[1] = -d[1];
+  J[2] = -d[2];
+  // d * (-[P]x): -[P]x = [[0, z, -y], [-z, 0, x], [y, -x, 0]]
+  J[3] = -(d[1] * -P[2] + d[2] * P[1]);
+  J[4] = -(d[0] * P[2] + d[2] * -P[0]);
+  J[5] = -(d[0] * -P[1] + d[1] * P[0]);
+  J[6] = -(d[0] * P[0] + d[1] * P[1] + d[2] * P[2]);
+}
+
+__global__ void track_init_kernel(const float* __restrict__ Twc_k, const float* __restrict__ Twc_f,
+                                  TrackState* st) {
+  if (threadIdx.x != 0) return;
+  // T_CkCf = T_WCk^-1 * T_WCf
+  m3s_rel_sim3<float>(Twc_k, Twc_k + 3, Twc_k[7], Twc_f, Twc_f + 3, Twc_f[7], st->T, st->T + 3,
+                      st->T + 7);
+  st->old_cost = __builtin_inf();
+  st->done = 0;
+  st->fail = 0;
+  st->iters = 0;
+  st->conv = 0;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void track_points_kernel(
+    const TrackState* __restrict__ st, TrackParams prm, const float* __restrict__ K,
+    const float* __restrict__ Xf, const float* __restrict__ Xk, const float* __restrict__ Qk,
+    const uint8_t* __restrict__ valid, const float* __restrict__ meas_k,
+    const uint8_t* __restrict__ valid_meas, int64_t n, float* __restrict__ partial) {
+  if (st->done) return;
+  if (MODE == TRACK_CALIB) {
+    prm.fx = K[0];
+    prm.fy = K[4];
+    prm.cx = K[2];
+    prm.cy = K[5];
+  }
+  float T[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) T[i] = st->T[i];
+  float acc[kAcc];
+#pragma unroll
+  for (int l = 0; l < kAcc; l++) acc[l] = 0.f;
+
+  for (int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * kThreads) {
+    const float X[3] = {Xf[3 * k], Xf[3 * k + 1], Xf[3 * k + 2]};
+    float P[3];
+    m3s_act_sim3<float>(T, T + 3, T[7], X, P);
+    const float vq = (valid[k] ? 1.f : 0.f) * sqrtf(Qk[k]);
+    if (MODE == TRACK_RAYS) {
+      // rd_k (precomputed in the reference, tracker2.py:327)
+      const float K3[3] = {Xk[3 * k], Xk[3 * k + 1], Xk[3 * k + 2]};
+      const float dk = sqrtf(K3[0] * K3[0] + K3[1] * K3[1] + K3[2] * K3[2]);
+      const float dk_inv = 1.0f / dk;
+      const float d = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2]);
+      const float d_inv = 1.0f / d;
+      const float r[3] = {d_inv * P[0], d_inv * P[1], d_inv * P[2]};
+      const float res[4] = {dk_inv * K3[0] - r[0], dk_inv * K3[1] - r[1], dk_inv * K3[2] - r[2],
+                            dk - d};
+      const float d_inv2 = d_inv * d_inv;
+      const float si[4] = {prm.si0 * vq, prm.si0 * vq, prm.si0 * vq, prm.si1 * vq};
+#pragma unroll
+      for (int row = 0; row < 4; row++) {
+        float drow[3];
+        if (row < 3) {
+#pragma unroll
+          for (int c = 0; c < 3; c++)
+            drow[c] = d_inv * ((row == c ? 1.f : 0.f) - d_inv2 * (P[row] * P[c]));
+        } else {
+          drow[0] = r[0];
+          drow[1] = r[1];
+          drow[2] = r[2];
+        }
+        float J[7];
+        jac_row(drow, P, J);
+        const float wr = si[row] * res[row];
+        const float ws = si[row] * sqrtf(huber_w(wr, prm.huber_k));
+        acc_row(acc, ws, J, res[row]);
+      }
+    } else {
+      const float x = P[0], y = P[1], z = P[2];
+      // p = K P / (K P)_z  (geometry.project_calib)
+      const float pu = prm.fx * x + 0.f * y + prm.cx * z;
+      const float pv = 0.f * x + prm.fy * y + prm.cy * z;
+      const float pw = 0.f * x + 0.f * y + 1.f * z;
+      const float u = pu / pw, v = pv / pw;
+      const bool valid_u = (u > prm.border) && (u < (float)(prm.w - 1) - prm.border);
+      const bool valid_v = (v > prm.border) && (v < (float)(prm.h - 1) - prm.border);
+      const bool valid_z = z > prm.depth_eps;
+      const float logz = valid_z ? logf(z) : 0.f;
+      const float z_inv = 1.0f / z;
+      const bool v2 = valid_u && valid_v && valid_z && (valid_meas[k] != 0);
+      const float vq2 = v2 ? vq : 0.f;
+      const float res[3] = {meas_k[3 * k] - u, meas_k[3 * k + 1] - v, meas_k[3 * k + 2] - logz};
+      const float d0[3] = {prm.fx * z_inv, 0.f * z_inv, (-prm.fx * x * z_inv) * z_inv};
+      const float d1[3] = {0.f * z_inv, prm.fy * z_inv, (-prm.fy * y * z_inv) * z_inv};
+      const float d2[3] = {0.f, 0.f, z_inv};
+      const float* drows[3] = {d0, d1, d2};
+      const float si[3] = {prm.si0 * vq2, prm.si0 * vq2, prm.si1 * vq2};
+#pragma unroll
+      for (int row = 0; row < 3; row++) {
+        float J[7];
+        jac_row(drows[row], P, J);
+        const float wr = si[row] * res[row];
+        const float ws = si[row] * sqrtf(huber_w(wr, prm.huber_k));
+        acc_row(acc, ws, J, res[row]);
+      }
+    }
+  }
+  __shared__ float red[kThreads / M3S_WAVE][kAcc];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int l = 0; l < kAcc; l++) {
+    const float v = m3s_wave_sum(acc[l]);
+    if (lane == 0) red[wid][l] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kAcc) {
+    float v = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kThreads / M3S_WAVE; w++) v += red[w][threadIdx.x];
+    partial[blockIdx.x * kAcc + threadIdx.x] = v;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void track_solve_kernel(TrackState* st,
+                                                               const float* __restrict__ partial,
+                                                               int nblocks, float rel_error,
+                                                               float delta_norm) {
+  if (st->done) return;
+  __shared__ double sacc[kAcc];
+  // f64 reduction of the partials: lane-per-(accumulator, block-slice), then fixed order
+  const int tid = threadIdx.x;
+  __shared__ double tmp[kThreads / M3S_WAVE][kAcc];
+  for (int l = 0; l < kAcc; l++) {
+    double v = 0.0;
+    for (int b = tid; b < nblocks; b += kThreads) v += (double)partial[b * kAcc + l];
+    v = m3s_wave_sum_d(v);
+    if ((tid & 63) == 0) tmp[tid >> 6][l] = v;
+  }
+  __syncthreads();
+  if (tid < kAcc) {
+    double v = 0.0;
+    for (int w = 0; w < kThreads / M3S_WAVE; w++) v += tmp[w][tid];
+    sacc[tid] = v;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  double H[7][7], g[7];
+  int l = 0;
+  for (int n = 0; n < 7; n++)
+    for (int m = 0; m <= n; m++) {
+      H[n][m] = sacc[l];
+      H[m][n] = sacc[l];
+      l++;
+    }
+  for (int n = 0; n < 7; n++) g[n] = sacc[28 + n];
+  const double new_cost = sacc[35];
+  // Cholesky H = L L^T (torch.linalg.cholesky raises on failure → frame lost)
+  double L[7][7] = {};
+  bool ok = true;
+  for (int j = 0; j < 7 && ok; j++) {
+    double s = H[j][j];
+    for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
+    if (!(s > 0.0)) {
+      ok = false;
+      break;
+    }
+    L[j][j] = sqrt(s);
+    for (int i = j + 1; i < 7; i++) {
+      double t = H[i][j];
+      for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
+      L[i][j] = t / L[j][j];
+    }
+  }
+  if (!ok) {
+    st->fail = 1;
+    st->done = 1;
+    return;
+  }
+  double y[7], x[7];
+  for (int i = 0; i < 7; i++) {
+    double t = g[i];
+    for (int k = 0; k < i; k++) t -= L[i][k] * y[k];
+    y[i] = t / L[i][i];
+  }
+  for (int i = 6; i >= 0; i--) {
+    double t = y[i];
+    for (int k = i + 1; k < 7; k++) t -= L[k][i] * x[k];
+    x[i] = t / L[i][i];
+  }
+  float tau[7];
+  for (int i = 0; i < 7; i++) tau[i] = (float)x[i];
+  float t1[3], q1[4], s1;
+  m3s_retr_sim3<float>(tau, st->T, st->T + 3, st->T[7], t1, q1, &s1);
+  for (int i = 0; i < 3; i++) st->T[i] = t1[i];
+  for (int i = 0; i < 4; i++) st->T[3 + i] = q1[i];
+  st->T[7] = s1;
+  // check_convergence: rel_dec = |(old - new) / old| (NaN on iteration 0: inf/inf)
+  const double old_cost = st->old_cost;
+  const double rel_dec = fabs((old_cost - new_cost) / old_cost);
+  float dn = 0.f;
+  for (int i = 0; i < 7; i++) dn += tau[i] * tau[i];
+  dn = sqrtf(dn);
+  st->iters += 1;
+  if (rel_dec < (double)rel_error || dn < delta_norm) {
+    st->conv = 1;
+    st->done = 1;
+  }
+  st->old_cost = new_cost;
+}
+
+__global__ void track_finish_kernel(const float* __restrict__ Twc_k, const TrackState* st,
+                                    float* __restrict__ T_WCf, float* __restrict__ T_CkCf,
+                                    int* __restrict__ info) {
+  if (threadIdx.x != 0) return;
+  // T_WCf = T_WCk * T_CkCf: q = qk*q, s = sk*s, t = tk + sk * Rk t
+  const float* Tk = Twc_k;
+  float q[4], t[3];
+  m3s_quat_comp<float>(Tk + 3, st->T + 3, q);
+  m3s_act_so3<float>(Tk + 3, st->T, t);
+  for (int i = 0; i < 3; i++) T_WCf[i] = Tk[i] + Tk[7] * t[i];
+  for (int i = 0; i < 4; i++) T_WCf[3 + i] = q[i];
+  T_WCf[7] = Tk[7] * st->T[7];
+  for (int i = 0; i < 8; i++) T_CkCf[i] = st->T[i];
+  info[0] = st->iters;
+  info[1] = st->fail;
+  info[2] = st->conv;
+  info[3] = 0;
+}
+
+struct Layout {
+  size_t state, partial, total;
+};
+Layout layout() {
+  Layout L;
+  L.state = 0;
+  L.partial = 512;
+  L.total = 512 + sizeof(float) * kBlocks * kAcc;
+  return L;
+}
+
+template <int MODE>
+int run_track(const float* Twc_k, const float* Twc_f, const float* Xf, const float* Xk,
+              const float* Qk, const uint8_t* valid, const float* meas_k,
+              const uint8_t* valid_meas, const float* K, int64_t n, TrackParams prm,
+              int max_iters, float rel_error, float delta_norm, float* T_WCf, float* T_CkCf,
+              int* info, void* ws, void* stream) {
+  if (n < 1 || !Twc_k || !Twc_f || !Xf || !Qk || !valid || !T_WCf || !T_CkCf || !info || !ws)
+    return M3S_ERR_INVALID_ARG;
+  if (MODE == TRACK_RAYS && !Xk) return M3S_ERR_INVALID_ARG;
+  if (MODE == TRACK_CALIB && (!meas_k || !valid_meas || !K)) return M3S_ERR_INVALID_ARG;
+  hipStream_t s = m3s_stream(stream);
+  const Layout L = layout();
+  char* w = reinterpret_cast<char*>(ws);
+  TrackState* st = reinterpret_cast<TrackState*>(w + L.state);
+  float* partial = reinterpret_cast<float*>(w + L.partial);
+  hipLaunchKernelGGL(track_init_kernel, dim3(1), dim3(64), 0, s, Twc_k, Twc_f, st);
+  M3S_LAUNCH_CHECK();
+  int nb = (int)((n + kThreads - 1) / kThreads);
+  if (nb > kBlocks) nb = kBlocks;
+  for (int it = 0; it < max_iters; it++) {
+    hipLaunchKernelGGL(track_points_kernel<MODE>, dim3(nb), dim3(kThreads), 0, s, st, prm, K, Xf,
+                       Xk, Qk, valid, meas_k, valid_meas, n, partial);
+    M3S_LAUNCH_CHECK();
+    hipLaunchKernelGGL(track_solve_kernel, dim3(1), dim3(kThreads), 0, s, st, partial, nb,
+                       rel_error, delta_norm);
+    M3S_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(track_finish_kernel, dim3(1), dim3(64), 0, s, Twc_k, st, T_WCf, T_CkCf,
+                     info);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+}  // namespace
+
+extern "C" size_t m3s_track_workspace_bytes(int64_t n) {
+  (void)n;
+  return layout().total;
+}
+
+extern "C" int m3s_track_rays(const float* d_Twc_k, const float* d_Twc_f, const float* d_Xf,
+                              const float* d_Xk, const float* d_Qk, const uint8_t* d_valid,
+                              int64_t n, float sigma_ray, float sigma_dist, float huber_k,
+                              int max_iters, float rel_error, float delta_norm, float* d_T_WCf,
+                              float* d_T_CkCf, int* d_info, void* d_ws, void* stream) {
+  TrackParams prm{};
+  prm.si0 = 1.0f / sigma_ray;
+  prm.si1 = 1.0f / sigma_dist;
+  prm.huber_k = huber_k;
+  return run_track<TRACK_RAYS>(d_Twc_k, d_Twc_f, d_Xf, d_Xk, d_Qk, d_valid, nullptr, nullptr,
+                               nullptr, n, prm, max_iters, rel_error, delta_norm, d_T_WCf,
+                               d_T_CkCf, d_info, d_ws, stream);
+}
+
+extern "C" int m3s_track_calib(const float* d_Twc_k, const float* d_Twc_f, const float* d_Xf,
+                               const float* d_Qk, const uint8_t* d_valid, const float* d_meas_k,
+                               const uint8_t* d_valid_meas_k, const float* d_K, int64_t n,
+                               int64_t h, int64_t w, float sigma_pixel, float sigma_depth, float huber_k,
+                               float pixel_border, float depth_eps, int max_iters,
+                               float rel_error, float delta_norm, float* d_T_WCf,
+                               float* d_T_CkCf, int* d_info, void* d_ws, void* stream) {
+  TrackParams prm{};
+  prm.si0 = 1.0f / sigma_pixel;
+  prm.si1 = 1.0f / sigma_depth;
+  prm.huber_k = huber_k;
+  prm.border = pixel_border;
+  prm.depth_eps = depth_eps;
+  prm.h = (int)h;
+  prm.w = (int)w;
+  return run_track<TRACK_CALIB>(d_Twc_k, d_Twc_f, d_Xf, nullptr, d_Qk, d_valid, d_meas_k,
+                                d_valid_meas_k, d_K, n, prm, max_iters, rel_error, delta_norm,
+                                d_T_WCf, d_T_CkCf, d_info, d_ws, stream);
+}

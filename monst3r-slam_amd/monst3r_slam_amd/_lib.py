@@ -1,0 +1,100 @@
+"""ctypes binding of the C-ABI library libmonst3r_slam_amd.so (include/monst3r_slam_amd.h).
+
+The HIP library is the product path: if it is missing this module raises; there is no
+CPU or PyTorch fallback.  torch is imported first so that torch's libamdhip64.so.7 is the
+one HIP runtime in the process (same SONAME; the loader reuses it for this library).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmonst3r_slam_amd.so")
+HEADER = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "monst3r_slam_amd.h"))
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I = ctypes.c_int
+_F = ctypes.c_float
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/monst3r_slam_amd.h
+SIGNATURES = {
+    "m3s_status_string": (ctypes.c_char_p, [_I]),
+    "m3s_version": (_I, []),
+    "m3s_device_count": (_I, []),
+    "m3s_iter_proj": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _F, _F, _P]),
+    "m3s_refine_matches": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
+    "m3s_match_prep": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P]),
+    "m3s_match_occlusion": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _P]),
+    "m3s_pixel_to_lin": (_I, [_P, _P, _I64, _I64, _I64, _P]),
+    "m3s_gn_workspace_bytes": (_SZ, [_I64, _I64]),
+    "m3s_gauss_newton_rays": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _F, _F,
+                                   _F, _I, _F, _P, _P, _P, _P]),
+    "m3s_gauss_newton_calib": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I, _I,
+                                    _I, _F, _F, _F, _F, _F, _I, _F, _P, _P, _P, _P]),
+    "m3s_gauss_newton_points": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _F,
+                                     _F, _I, _F, _P, _P, _P, _P]),
+    "m3s_track_workspace_bytes": (_SZ, [_I64]),
+    "m3s_track_rays": (_I, [_P, _P, _P, _P, _P, _P, _I64, _F, _F, _F, _I, _F, _F, _P, _P, _P, _P,
+                            _P]),
+    "m3s_track_calib": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _F, _F, _F, _F,
+                             _I, _F, _F, _P, _P, _P, _P, _P]),
+}
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the native library; raises if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"monst3r_slam_amd: native HIP library not found at {LIB_PATH}; build it with "
+                "`make -C monst3r-slam_amd/csrc` or `python -c 'import __graft_entry__ as g; "
+                "g.build()'` (there is no CPU fallback)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def status_string(status: int) -> str:
+    return load().m3s_status_string(int(status)).decode()
+
+
+def check(status: int, what: str):
+    if status != 0:
+        raise RuntimeError(f"{what}: {status_string(status)} (status {status})")
+
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_cuda(*tensors, names=()):
+    for i, t in enumerate(tensors):
+        if t is None:
+            continue
+        if not t.is_cuda:
+            nm = names[i] if i < len(names) else f"arg{i}"
+            raise RuntimeError(f"{nm} must be a GPU (HIP) tensor: the MI355X path has no CPU "
+                               "fallback")
+
+
+def require_contiguous(**tensors):
+    # reference: CHECK_CONTIGUOUS → TORCH_CHECK(x.is_contiguous(), #x " must be contiguous")
+    for name, t in tensors.items():
+        if t is not None and not t.is_contiguous():
+            raise RuntimeError(f"{name} must be contiguous")

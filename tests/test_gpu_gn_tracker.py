@@ -1,0 +1,132 @@
+"""GPU parity: backend GN (mast3r_slam_backends.gauss_newton_*) and the fused tracker vs
+the CPU oracle.  Floating-point work with a different reduction order (f32 partial sums,
+f64 solve): poses compared with an absolute tolerance stated per test."""
+import numpy as np
+import pytest
+import torch
+
+from monst3r_slam_amd import synthetic as syn
+from monst3r_slam_amd.config import default_config
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 2e-5   # |ΔT| elementwise after the same number of GN iterations
+TRACK_TOL = 1e-4  # tracker: up to 50 f32 iterations, convergence test on f32 cost
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _gn_case(g, dev):
+    return [_t(g[k], dev) for k in ("Twc", "Xs", "Cs", "ii", "jj", "idx", "valid", "Q")]
+
+
+@pytest.mark.parametrize("P,h,w,iters", [(5, 48, 64, 1), (5, 48, 64, 10), (8, 96, 128, 3)])
+def test_gn_rays_parity(oracle, dev, P, h, w, iters):
+    import mast3r_slam_backends as mb
+    g = syn.keyframe_graph(P=P, h=h, w=w, seed=P + h)
+    Twc_ref = g["Twc"].copy()
+    ref = oracle.gauss_newton("rays", Twc_ref, g["Xs"], g["Cs"], g["ii"], g["jj"], g["idx"],
+                              g["valid"], g["Q"], sig0=0.003, sig1=10.0, C_thresh=0.0,
+                              Q_thresh=1.5, max_iter=iters, delta_thresh=1e-8)
+    Twc, Xs, Cs, ii, jj, idx, valid, Q = _gn_case(g, dev)
+    (dx,) = mb.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.003, 10.0, 0.0, 1.5,
+                                 iters, 1e-8)
+    np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=POSE_TOL, rtol=0)
+    np.testing.assert_allclose(dx.cpu().numpy(), ref["dx"], atol=POSE_TOL, rtol=0)
+
+
+def test_gn_points_parity(oracle, dev):
+    import mast3r_slam_backends as mb
+    g = syn.keyframe_graph(P=4, h=48, w=64, seed=3)
+    Twc_ref = g["Twc"].copy()
+    oracle.gauss_newton("points", Twc_ref, g["Xs"], g["Cs"], g["ii"], g["jj"], g["idx"],
+                        g["valid"], g["Q"], sig0=0.05, C_thresh=0.0, Q_thresh=1.5, max_iter=5,
+                        delta_thresh=1e-8)
+    Twc, Xs, Cs, ii, jj, idx, valid, Q = _gn_case(g, dev)
+    mb.gauss_newton_points(Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.05, 0.0, 1.5, 5, 1e-8)
+    np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=POSE_TOL, rtol=0)
+
+
+def test_gn_calib_parity(oracle, dev):
+    import mast3r_slam_backends as mb
+    g = syn.keyframe_graph(P=4, h=48, w=64, seed=4)
+    Twc_ref = g["Twc"].copy()
+    oracle.gauss_newton("calib", Twc_ref, g["Xs"], g["Cs"], g["ii"], g["jj"], g["idx"],
+                        g["valid"], g["Q"], sig0=1.0, sig1=10.0, C_thresh=0.0, Q_thresh=1.5,
+                        max_iter=3, delta_thresh=1e-8, K=g["K"], height=48, width=64,
+                        pixel_border=-10, z_eps=1e-6)
+    Twc, Xs, Cs, ii, jj, idx, valid, Q = _gn_case(g, dev)
+    mb.gauss_newton_calib(Twc, Xs, Cs, _t(g["K"], dev), ii, jj, idx, valid, Q, 48, 64, -10, 1e-6,
+                          1.0, 10.0, 0.0, 1.5, 3, 1e-8)
+    np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=1e-4, rtol=0)
+
+
+def test_gn_global_ids_and_not_pd(oracle, dev):
+    # keyframe ids are global (sparse) and all matches invalid → zero step, poses untouched
+    import mast3r_slam_backends as mb
+    g = syn.keyframe_graph(P=3, h=8, w=8, seed=2)
+    Twc, Xs, Cs, ii, jj, idx, valid, Q = _gn_case(g, dev)
+    ii, jj = ii * 7 + 3, jj * 7 + 3
+    before = Twc.clone()
+    (dx,) = mb.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx, torch.zeros_like(valid), Q, 0.003,
+                                 10.0, 0.0, 1.5, 10, 1e-8)
+    assert torch.equal(Twc, before)
+    assert torch.count_nonzero(dx) == 0
+
+
+def test_gn_global_ids_parity(oracle, dev):
+    import mast3r_slam_backends as mb
+    g = syn.keyframe_graph(P=5, h=24, w=32, seed=9)
+    Twc_ref = g["Twc"].copy()
+    ii_g, jj_g = g["ii"] * 3 + 100, g["jj"] * 3 + 100
+    oracle.gauss_newton("rays", Twc_ref, g["Xs"], g["Cs"], ii_g, jj_g, g["idx"], g["valid"],
+                        g["Q"], sig0=0.003, sig1=10.0, C_thresh=0.0, Q_thresh=1.5, max_iter=4,
+                        delta_thresh=1e-8)
+    Twc, Xs, Cs, _, _, idx, valid, Q = _gn_case(g, dev)
+    mb.gauss_newton_rays(Twc, Xs, Cs, _t(ii_g, dev), _t(jj_g, dev), idx, valid, Q, 0.003, 10.0,
+                         0.0, 1.5, 4, 1e-8)
+    np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=POSE_TOL, rtol=0)
+
+
+@pytest.mark.parametrize("h,w", [(384, 512), (96, 128)])
+def test_tracker_rays_parity(dev, h, w):
+    from oracle import tracker_ref as tr
+    from monst3r_slam_amd import tracker as T
+    p = syn.tracking_problem(h, w, seed=1)
+    cfg = default_config()["tracking"]
+    Tf_ref, Trel_ref, it_ref = tr.opt_pose_ray_dist_sim3(p["Xf"], p["Xk"], p["T_WCf"],
+                                                         p["T_WCk"], p["Qk"], p["valid"], cfg)
+    Tf, Trel, info = T.opt_pose_ray_dist_sim3(_t(p["Xf"], dev), _t(p["Xk"], dev),
+                                              _t(p["T_WCf"], dev), _t(p["T_WCk"], dev),
+                                              _t(p["Qk"], dev), _t(p["valid"], dev), cfg)
+    np.testing.assert_allclose(Trel.cpu().numpy(), Trel_ref, atol=TRACK_TOL, rtol=0)
+    np.testing.assert_allclose(Tf.cpu().numpy(), Tf_ref, atol=TRACK_TOL, rtol=0)
+    assert abs(int(info[0]) - it_ref) <= 1
+
+
+def test_tracker_calib_parity(dev):
+    from oracle import tracker_ref as tr
+    from monst3r_slam_amd import tracker as T
+    p = syn.tracking_problem(96, 128, seed=2)
+    cfg = default_config()["tracking"]
+    Tf_ref, Trel_ref, it_ref = tr.opt_pose_calib_sim3(
+        p["Xf"], p["T_WCf"], p["T_WCk"], p["Qk"], p["valid"], p["meas_k"], p["valid_meas"],
+        p["K"], (p["h"], p["w"]), cfg)
+    Tf, Trel, info = T.opt_pose_calib_sim3(
+        _t(p["Xf"], dev), _t(p["T_WCf"], dev), _t(p["T_WCk"], dev), _t(p["Qk"], dev),
+        _t(p["valid"], dev), _t(p["meas_k"], dev), _t(p["valid_meas"], dev), _t(p["K"], dev),
+        (p["h"], p["w"]), cfg)
+    np.testing.assert_allclose(Trel.cpu().numpy(), Trel_ref, atol=TRACK_TOL, rtol=0)
+    assert abs(int(info[0]) - it_ref) <= 1
+
+
+def test_tracker_cholesky_failure_reported(dev):
+    from monst3r_slam_amd import tracker as T
+    p = syn.tracking_problem(32, 32, seed=3)
+    cfg = default_config()["tracking"]
+    with pytest.raises(T.CholeskyError):
+        T.opt_pose_ray_dist_sim3(_t(p["Xf"], dev), _t(p["Xk"], dev), _t(p["T_WCf"], dev),
+                                 _t(p["T_WCk"], dev), _t(p["Qk"], dev),
+                                 torch.zeros(32 * 32, dtype=torch.bool, device=dev), cfg)

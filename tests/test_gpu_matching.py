@@ -1,0 +1,105 @@
+"""GPU parity: HIP matching kernels vs the CPU oracle, through the C ABI.
+
+Bar: bit-exact (p, converged, match indices, valid masks) on identical inputs."""
+import numpy as np
+import pytest
+import torch
+
+from monst3r_slam_amd import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+@pytest.mark.parametrize("b,h,w", [(1, 384, 512), (2, 384, 512), (1, 224, 224), (2, 24, 40)])
+def test_iter_proj_bit_exact(oracle, dev, b, h, w):
+    import mast3r_slam_backends as mb
+    X11, X21, _, _ = syn.pointmap_pair_batch(b, h, w, seed=b * 7 + h)
+    rwg, pts, p_init = oracle.prep_for_iter_proj(X11, X21)
+    # perturb the init so the LM iterations do real work
+    rng = np.random.default_rng(1)
+    p_init = (p_init + rng.uniform(-3, 3, p_init.shape)).astype(np.float32)
+    p_ref, c_ref = oracle.iter_proj(rwg, pts, p_init, 10, 1e-8, 1e-6)
+    p_gpu, c_gpu = mb.iter_proj(_t(rwg, dev), _t(pts, dev), _t(p_init, dev), 10, 1e-8, 1e-6)
+    np.testing.assert_array_equal(p_gpu.cpu().numpy(), p_ref)
+    np.testing.assert_array_equal(c_gpu.cpu().numpy(), c_ref)
+
+
+def test_iter_proj_ragged_tail(oracle, dev):
+    # n % 16 != 0 (the reference would read out of bounds; ours must be exact)
+    import mast3r_slam_backends as mb
+    X11, X21, _, _ = syn.pointmap_pair_batch(1, 30, 41, seed=5)
+    rwg, pts, p_init = oracle.prep_for_iter_proj(X11, X21)
+    n = 30 * 41 - 7
+    pts, p_init = pts[:, :n].copy(), p_init[:, :n].copy()
+    p_ref, c_ref = oracle.iter_proj(rwg, pts, p_init, 10, 1e-8, 1e-6)
+    p_gpu, c_gpu = mb.iter_proj(_t(rwg, dev), _t(pts, dev), _t(p_init, dev), 10, 1e-8, 1e-6)
+    np.testing.assert_array_equal(p_gpu.cpu().numpy(), p_ref)
+    np.testing.assert_array_equal(c_gpu.cpu().numpy(), c_ref)
+
+
+@pytest.mark.parametrize("b,h,w", [(1, 384, 512), (2, 96, 128), (1, 31, 37)])
+def test_refine_matches_bit_exact(oracle, dev, b, h, w):
+    import mast3r_slam_backends as mb
+    X11, X21, D11, D21 = syn.pointmap_pair_batch(b, h, w, seed=3)
+    rng = np.random.default_rng(2)
+    yy, xx = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    p1 = np.stack([xx, yy], -1).reshape(1, -1, 2).repeat(b, 0)
+    p1 = np.clip(p1 + rng.integers(-4, 5, p1.shape), 0, [w - 1, h - 1]).astype(np.int64)
+    d11 = D11.astype(np.float16)
+    d21 = D21.reshape(b, h * w, -1).astype(np.float16)
+    ref = oracle.refine_matches(d11, d21, p1, 3, 5)
+    (got,) = mb.refine_matches(_t(d11, dev), _t(d21, dev), _t(p1, dev), 3, 5)
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+def test_refine_generic_fdim(oracle, dev):
+    import mast3r_slam_backends as mb
+    rng = np.random.default_rng(4)
+    b, h, w, f = 1, 20, 24, 17
+    d11 = rng.normal(size=(b, h, w, f)).astype(np.float16)
+    d21 = rng.normal(size=(b, h * w, f)).astype(np.float16)
+    p1 = rng.integers(0, [w, h], size=(b, h * w, 2)).astype(np.int64)
+    ref = oracle.refine_matches(d11, d21, p1, 2, 3)
+    (got,) = mb.refine_matches(_t(d11, dev), _t(d21, dev), _t(p1, dev), 2, 3)
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+def test_prep_matches_golden(dev):
+    import os
+    from monst3r_slam_amd import matching as M
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "matching_prep.npz")))
+    rwg, pts, p_init = M.prep_for_iter_proj(_t(g["X11"], dev), _t(g["X21"], dev))
+    np.testing.assert_array_equal(rwg.cpu().numpy(), g["rays_with_grad"])
+    np.testing.assert_array_equal(pts.cpu().numpy(), g["pts3d_norm"])
+    np.testing.assert_array_equal(p_init.cpu().numpy(), g["p_init"])
+    _, _, p2 = M.prep_for_iter_proj(_t(g["X11"], dev), _t(g["X21"], dev), _t(g["idx_init"], dev))
+    np.testing.assert_array_equal(p2.cpu().numpy(), g["p_init_from_idx"])
+
+
+@pytest.mark.parametrize("b,h,w", [(1, 384, 512), (2, 384, 512), (1, 224, 224)])
+def test_match_end_to_end_bit_exact(oracle, dev, b, h, w):
+    from monst3r_slam_amd import matching as M
+    X11, X21, D11, D21 = syn.pointmap_pair_batch(b, h, w, seed=11)
+    idx_ref, valid_ref = oracle.match(X11, X21, D11, D21)
+    idx, valid = M.match(_t(X11, dev), _t(X21, dev), _t(D11, dev), _t(D21, dev))
+    np.testing.assert_array_equal(idx.cpu().numpy(), idx_ref)
+    np.testing.assert_array_equal(valid.cpu().numpy(), valid_ref)
+    # sanity: the synthetic shift is recovered for most pixels
+    assert valid_ref.mean() > 0.5
+
+
+def test_match_with_init_bit_exact(oracle, dev):
+    from monst3r_slam_amd import matching as M
+    b, h, w = 1, 384, 512
+    X11, X21, D11, D21 = syn.pointmap_pair_batch(b, h, w, seed=12)
+    rng = np.random.default_rng(0)
+    idx0 = np.clip(np.arange(h * w)[None] + rng.integers(-600, 600, (b, h * w)), 0,
+                   h * w - 1).astype(np.int64)
+    idx_ref, valid_ref = oracle.match(X11, X21, D11, D21, idx0)
+    idx, valid = M.match(_t(X11, dev), _t(X21, dev), _t(D11, dev), _t(D21, dev), _t(idx0, dev))
+    np.testing.assert_array_equal(idx.cpu().numpy(), idx_ref)
+    np.testing.assert_array_equal(valid.cpu().numpy(), valid_ref)
