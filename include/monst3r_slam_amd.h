@@ -158,6 +158,91 @@ int m3s_track_calib(const float* d_Twc_k, const float* d_Twc_f, const float* d_X
                     float* d_T_WCf_out, float* d_T_CkCf_out, int* d_info, void* d_workspace,
                     void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * ViT / DPT building blocks (bf16 MFMA).  The reference runs these as PyTorch ops
+ * (cuBLAS/cuDNN, fp32/TF32: croco/blocks.py, croco/dpt_block.py, d3r/heads/dpt_head.py,
+ * mast3r/catmlp_dpt_head.py); they have no FFI in the reference, so this is the
+ * native surface the host-side model (monst3r_slam_amd/model.py) drives.
+ * Activations: bf16 row-major [rows][channels] (tokens, or NHWC pixels);
+ * residual stream f32; weights bf16 [N][K] (torch Linear layout; convs repacked
+ * [Cout][ky][kx][Cin]; ConvTranspose repacked [(a,b,Cout)][Cin]).
+ * ------------------------------------------------------------------------- */
+enum {
+  M3S_EPI_BIAS = 1,       /* + bias[n] (f32)                                  */
+  M3S_EPI_GELU = 2,       /* exact-erf GELU                                    */
+  M3S_EPI_RELU = 4,       /* ReLU on the output                                */
+  M3S_EPI_RES_F32 = 8,    /* + R[m][n] (f32 residual)                          */
+  M3S_EPI_RES_BF16 = 16,  /* + R[m][n] (bf16 residual)                         */
+  M3S_EPI_OUT_F32 = 32,   /* store f32 (default bf16)                          */
+  M3S_PRO_RELU = 64,      /* ReLU applied to A while loading (conv prologue)   */
+  M3S_EPI_CONVT = 128     /* scatter rows/cols as ConvTranspose(k=s, stride=s) */
+};
+
+typedef struct {
+  const void* A; int64_t lda, strideA;     /* bf16 [M][lda]; per-batch element stride */
+  const void* B; int64_t ldb, strideB;     /* bf16 [N][ldb]                         */
+  void* C; int64_t ldc, strideC;           /* bf16 or f32 [M][ldc]                  */
+  const float* bias; int64_t strideBias;   /* f32 [N] (or [Cout] for CONVT)          */
+  const void* R; int64_t ldr, strideR;     /* residual [M][ldr]                     */
+  int32_t M, N, K, batch;
+  int32_t flags;                           /* OR of M3S_EPI_x / M3S_PRO_x bits       */
+  int32_t mode;                            /* 0: GEMM; 1: implicit 3x3 conv, pad 1  */
+  int32_t Hin, Win, Cin, Hout, Wout, stride; /* conv geometry (mode 1); K = 9*Cin   */
+  int32_t ct_s, ct_cout, ct_gw;            /* CONVT: kernel=stride=s, Cout, grid w  */
+} m3s_gemm_desc;
+
+/* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 32 == 0; conv: Cin % 32 == 0. */
+int m3s_vit_gemm(const m3s_gemm_desc* desc, void* stream);
+
+/* LayerNorm over the last dim (eps), x f32/bf16 [rows][dim] → y bf16 or f32
+ * (x_is_bf16 / y_is_f32 flags); batch strides in elements.  dim ≤ 4096, dim % 4 == 0. */
+int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_gamma,
+                      const float* d_beta, void* d_y, int y_is_f32, int64_t rows, int64_t dim,
+                      float eps, int64_t batch, int64_t stride_x, int64_t stride_y,
+                      int64_t stride_param, void* stream);
+
+/* In-place 2-D RoPE (curope kernels.cu:17-82; pos_embed.py:106-158) on a bf16 view
+ * t [B][S] rows of ld (head h at column h*64): dims [0,32) rotate by pos y, [32,64) by
+ * pos x, pairs (i, i+16), angle = pos * base^(-i/16).  pos int64 [B][S][2] (y, x). */
+int m3s_vit_rope(void* d_t, int64_t ld, int64_t stride, const int64_t* d_pos,
+                 int64_t stride_pos, int64_t batch, int64_t S, int64_t heads, float base,
+                 void* stream);
+
+/* Multi-head attention, head dim 64 (croco/blocks.py:81-112 self, :132-169 cross):
+ * o = softmax(q k^T / 8) v.  q [B][Sq] rows of ld_q bf16 (head h at column h*64), k,v
+ * [B][Sk] rows of ld_kv; RoPE already applied (m3s_vit_rope).  o bf16 [B][Sq][ld_o].
+ * The pos/rope arguments are reserved (must be NULL/0). */
+int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q, const void* d_k,
+                      const void* d_v, int64_t ld_kv, int64_t stride_kv, const int64_t* d_qpos,
+                      const int64_t* d_kpos, int64_t stride_pos, void* d_o, int64_t ld_o,
+                      int64_t stride_o, int64_t batch, int64_t heads, int64_t sq, int64_t sk,
+                      float rope_base, void* stream);
+
+/* Patch-embed im2col: img f32 NCHW [B][3][H][W] → bf16 [B][(H/16)(W/16)][3*16*16]
+ * with K ordered (c, ky, kx) like the conv weight [1024][3][16][16]. */
+int m3s_vit_patchify(const float* d_img, void* d_out, int64_t batch, int64_t h, int64_t w,
+                     void* stream);
+
+/* Bilinear x2 upsample, align_corners=True, NHWC bf16 [B][H][W][C] → [B][2H][2W][C]. */
+int m3s_vit_upsample2x(const void* d_in, void* d_out, int64_t batch, int64_t h, int64_t w,
+                       int64_t c, void* stream);
+
+/* DPT regression head tail, fused: t = relu(conv3x3 output) [P][128] bf16 is reduced by
+ * the final 1x1 conv (128 → 4, W4 f32 [4][128], b4 [4]) and post-processed
+ * (d3r/heads/postprocess.py:10-58): pts3d = xyz/max(|xyz|,1e-8) * expm1(|xyz|),
+ * conf = conf_min + exp(c).  pts3d f32 [P][3], conf f32 [P]. */
+int m3s_vit_dpt_out(const void* d_t, const float* d_w4, const float* d_b4, float* d_pts3d,
+                    float* d_conf, int64_t pixels, float conf_min, int64_t batch,
+                    int64_t stride_t, int64_t stride_out, void* stream);
+
+/* MASt3R local-feature tail (catmlp_dpt_head.py:25-39,84-96): feats bf16 or f32
+ * [B][S][25*256] (fc2 output, per token) → pixel_shuffle(16) → desc = normalise(ch 0..23)
+ * as f32 [B][H][W][24] and f16 [B][H][W][24], desc_conf = 0 + exp(ch 24) f32 [B][H][W].
+ * gw = W/16 token-grid width. */
+int m3s_vit_local_features(const float* d_feats, float* d_desc, uint16_t* d_desc_f16,
+                           float* d_desc_conf, int64_t batch, int64_t h, int64_t w,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,19 @@
+// Shared types for the ViT / DPT kernels (bf16 MFMA path, gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "common.h"
+
+typedef __bf16 bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return (float)v; }
+__device__ __forceinline__ bf16_t f2bf(float v) { return (bf16_t)v; }  // RNE (v_cvt_pk_bf16_f32)
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  // nn.GELU() default (approximate='none'): 0.5 x (1 + erf(x / sqrt(2)))
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}

