@@ -1,16 +1,18 @@
 """Headline benchmark: tracking frames/sec @512x384 (+ pairwise pointmap-inference ms) on
-MI355X — BASELINE.json metric, configs[1]/[2] workload.
+one MI355X — BASELINE.json metric; workload configs[1]+[2] (bf16 ViT pair inference inside
+the full tracking step).
 
-One "step" = one tracked frame of the per-frame hot path on synthetic 384x512 input with
-everything resident in HBM:
-  [vit]   pair inference (MonST3R encoder of the new frame, MonST3R decoder + 2 DPT heads,
-          MASt3R decoder + 2 catmlp+DPT heads; keyframe features cached) — when built
-  [match] projective matching frame→keyframe (prep, iter_proj, occlusion, refine, lin)
-  [track] 7-dof Sim3 ray-distance Gauss-Newton (≤50 iterations, on-device convergence)
+One "step" = one tracked frame of the per-frame hot path, synthetic 384x512 input,
+seeded random weights (no checkpoints offline), everything resident in HBM:
+  pair inference  MonST3R encoder (new frame) + MonST3R decoder + 2 DPT heads +
+                  MASt3R decoder + 2 catmlp+DPT heads (keyframe features cached)
+  matching        prep + iter_proj + occlusion + refine_matches + linear index
+  tracking        glue (Qk, valid, pointmap fusion, keyframe test) + fused Sim3 GN (≤50 it)
+The step is captured once in a HIP graph and replayed (no host work per frame).
 Multi-GPU: tracking is sequential per sequence → one independent replica per rank
 ("replicas only"); value = frames of all ranks / max rank time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--eager]
 """
 from __future__ import annotations
 
@@ -25,109 +27,120 @@ for _p in (ROOT, os.path.join(ROOT, "monst3r-slam_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 H, W = 384, 512
-HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-BF16_DENSE_TFLOPS = 2500.0   # dense bf16 MFMA (no sparsity)
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+BF16_DENSE_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (spec, no sparsity)
+METRIC = "tracking frames/sec @512x384 + pairwise pointmap-inference ms, 1/8 MI355X"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph (debug)")
     return ap.parse_args()
 
 
-class Frame:
-    """Synthetic per-frame inputs (what the ViT heads hand to matching and tracking)."""
-
-    def __init__(self, dev, seed):
-        from monst3r_slam_amd import synthetic as syn
-        X11, X21, D11, D21 = syn.pair(H, W, seed=seed)
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-        self.Xkk = t(X11)[None]   # keyframe pointmap in keyframe frame (Xii)
-        self.Xfk = t(X21)[None]   # frame pointmap in keyframe frame (Xji)
-        self.Dk = t(D11)[None]
-        self.Df = t(D21)[None]
-        p = syn.tracking_problem(H, W, seed=seed)
-        self.Xf = t(p["Xf"])
-        self.Xk = t(p["Xk"])
-        self.Qk = t(p["Qk"])
-        self.valid = t(p["valid"])
-        self.T_WCk = t(p["T_WCk"])
-        self.T_WCf = t(p["T_WCf"])
+def setup(dev, seed):
+    from monst3r_slam_amd import model as Mdl
+    from monst3r_slam_amd.frontend import Tracker
+    model, _ = Mdl.build(dev)
+    g = torch.Generator(device=dev).manual_seed(100 + seed)
+    img_k = torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1
+    img_f = torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1
+    tr = Tracker(model)
+    T0 = torch.tensor([0, 0, 0, 0, 0, 0, 1, 1], dtype=torch.float32, device=dev)
+    tr.add_keyframe(img_k, T0)
+    return model, tr, img_f
 
 
-def run_step(fr, cfg, ev=None):
-    from monst3r_slam_amd import matching as M
-    from monst3r_slam_amd import tracker as T
-    idx, valid = M.match(fr.Xkk, fr.Xfk, fr.Dk, fr.Df, None, cfg["matching"])
-    Tf, Trel, info = T.opt_pose_ray_dist_sim3(fr.Xf, fr.Xk, fr.T_WCf, fr.T_WCk, fr.Qk, fr.valid,
-                                              cfg["tracking"], check=False)
-    return idx, valid, Tf
-
-
-def kernel_timing(fr, cfg, reps=20):
-    """Average device time per launch of the matching kernels (HIP events on the stream
-    the kernels run on)."""
-    from monst3r_slam_amd import _lib
-    from monst3r_slam_amd import matching as M
-    lib = _lib.load()
-    dev = fr.Xkk.device
-    s = torch.cuda.current_stream(dev)
-    rwg, pts, p_init = M.prep_for_iter_proj(fr.Xkk, fr.Xfk)
-    n = H * W
-    p = torch.empty((1, n, 2), dtype=torch.float32, device=dev)
-    conv = torch.empty((1, n), dtype=torch.uint8, device=dev)
-    d11 = fr.Dk.half().contiguous()
-    d21 = fr.Df.reshape(1, n, -1).half().contiguous()
-    p1 = (torch.stack(torch.meshgrid(torch.arange(W, device=dev), torch.arange(H, device=dev),
-                                     indexing="xy"), -1).reshape(1, n, 2)).contiguous()
-    p1n = torch.empty_like(p1)
-    out = {}
-
-    def timeit(fn):
-        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+def capture(fn, dev):
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
         fn()
-        st.record(s)
-        for _ in range(reps):
-            fn()
-        en.record(s)
-        en.synchronize()
-        return st.elapsed_time(en) / reps * 1e3  # us
-
-    mc = cfg["matching"]
-    out["iter_proj_us"] = timeit(lambda: lib.m3s_iter_proj(
-        _lib.ptr(rwg), _lib.ptr(pts), _lib.ptr(p_init), _lib.ptr(p), _lib.ptr(conv), 1, H, W, n,
-        mc["max_iter"], mc["lambda_init"], mc["convergence_thresh"], _lib.stream(dev)))
-    out["refine_us"] = timeit(lambda: lib.m3s_refine_matches(
-        _lib.ptr(d11), _lib.ptr(d21), _lib.ptr(p1), _lib.ptr(p1n), 1, H, W, n, 24, mc["radius"],
-        mc["dilation_max"], _lib.stream(dev)))
-    return out
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    torch.cuda.synchronize(dev)
+    return g
 
 
-def cpu_baseline(cfg):
-    """Oracle (C port of the reference kernels + numpy tracker) on the host cores, on a
-    bounded sample: one full 384x512 frame of matching + tracking."""
+def time_replays(g, dev, n):
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(n):
+        g.replay()
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def gemm_roofline(model, img, feat_k, dev):
+    """Live HIP-event timing of every GEMM launch of one eager pair inference (events on
+    the stream the kernels run on): algorithmic FLOPs / summed kernel time."""
+    model.ops.probe = []
+    model.pair(img, feat_j=feat_k)
+    torch.cuda.synchronize(dev)
+    model.ops.probe = []
+    model.pair(img, feat_j=feat_k)
+    torch.cuda.synchronize(dev)
+    probe, model.ops.probe = model.ops.probe, None
+    t_ms = sum(a.elapsed_time(b) for a, b, _ in probe)
+    flops = sum(f for _, _, f in probe)
+    return dict(launches=len(probe), gemm_ms=t_ms, gemm_flops=flops,
+                avg_launch_us=t_ms / len(probe) * 1e3,
+                tflops=flops / (t_ms * 1e-3) / 1e12)
+
+
+def cpu_baseline():
+    """The reference-equivalent CPU path on this box's host cores, bounded sample:
+    the fp32 PyTorch restatement of the pair inference at 224x224 (configs[0] plumbing
+    case) scaled by FLOPs to 384x512, plus the C oracle of matching and the
+    numpy tracker on one 384x512 frame."""
+    import numpy as np
     from monst3r_slam_amd import synthetic as syn
+    from monst3r_slam_amd import weights as Wt
+    from monst3r_slam_amd.config import default_config
     from oracle import oracle as O
     from oracle import tracker_ref as TR
+    from oracle import vit_ref as V
+    torch.set_flush_denormal(True)
+    nthreads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(nthreads)
+    am, aM = Wt.MONST3R, Wt.MAST3R
+    sdm = Wt.make_state_dict(am, 0)
+    sdM = Wt.make_state_dict(aM, 1)
+    g = torch.Generator().manual_seed(1)
+    img_i = torch.rand(1, 3, 224, 224, generator=g) * 2 - 1
+    img_j = torch.rand(1, 3, 224, 224, generator=g) * 2 - 1
+    t0 = time.perf_counter()
+    V.asymmetric_inference(sdm, am, sdM, aM, img_i, img_j)
+    t_vit224 = time.perf_counter() - t0
+    # pair FLOPs 384x512 vs 224x224 (both encoders at 224: one extra encoder pass there)
+    scale = 2324.8 / (2324.8 * (196 / 768) + 523.0 * 196 / 768)
+    t_vit = t_vit224 * scale
     O.build()
     X11, X21, D11, D21 = syn.pair(H, W, seed=0)
     p = syn.tracking_problem(H, W, seed=0)
     t0 = time.perf_counter()
     O.match(X11[None], X21[None], D11[None], D21[None])
     TR.opt_pose_ray_dist_sim3(p["Xf"], p["Xk"], p["T_WCf"], p["T_WCk"], p["Qk"], p["valid"],
-                              cfg["tracking"])
-    dt = time.perf_counter() - t0
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": 1.0 / dt, "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": "1 frame 384x512: oracle match (C, OpenMP) + numpy tracker GN "
-                      "(ViT excluded)"}
+                              default_config()["tracking"])
+    t_match = time.perf_counter() - t0
+    del np
+    return {"value": 1.0 / (t_vit + t_match), "unit": "frames/s", "cores": nthreads,
+            "kind": "port",
+            "sample": f"fp32 torch-CPU pair inference at 224x224 ({t_vit224:.2f} s, scaled by "
+                      f"FLOPs x{scale:.2f} to 384x512) + C-oracle matching + numpy tracker GN "
+                      f"on one 384x512 frame ({t_match:.2f} s)"}
 
 
 def main():
@@ -140,19 +153,27 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local_rank)
-    from monst3r_slam_amd.config import default_config
-    cfg = default_config()
-    fr = Frame(dev, seed=rank)
+    torch.cuda.set_device(dev)
+    model, tr, img_f = setup(dev, rank)
+
+    def step():
+        return tr.track(img_f)
 
     for _ in range(args.warmup):
-        run_step(fr, cfg)
+        step()
     torch.cuda.synchronize(dev)
+    g_step = None if args.eager else capture(step, dev)
+    g_pair = None if args.eager else capture(lambda: model.pair(img_f, feat_j=tr.kf.feat), dev)
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        run_step(fr, cfg)
+        if g_step is not None:
+            g_step.replay()
+        else:
+            step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -162,16 +183,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kt = kernel_timing(fr, cfg)
     if rank == 0:
+        pair_ms = time_replays(g_pair, dev, max(5, args.steps // 2)) if g_pair else None
+        roof = gemm_roofline(model, img_f, tr.kf.feat, dev)
         ms = elapsed / args.steps * 1e3
-        # dominant kernel: refine_matches; algorithmic bytes per launch = D11 (f16) read
-        # once + D21 row + p1 in + p1 out per pixel (~25.2 MB per direction)
-        n = H * W
-        refine_bytes = n * 24 * 2 + n * 24 * 2 + n * 16 + n * 16
-        achieved = refine_bytes / (kt["refine_us"] * 1e-6) / 1e9
         line = {
-            "metric": "tracking frames/sec @512x384 + pairwise pointmap-inference ms, 1/8 MI355X",
+            "metric": METRIC,
             "value": world * args.steps / elapsed,
             "unit": "frames/s",
             "n_gpus": world,
@@ -181,19 +198,24 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32+f16",
-            "data": "synthetic",
-            "config": {"workload": "tracking step 384x512 (match + pose GN; ViT not yet in step)",
-                       "h": H, "w": W, "parallelism": f"replicas{world}"},
-            "pair_inference_ms": None,
-            "stages_us": kt,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "refine_matches_kernel<24>"},
+            "dtype": "bf16",
+            "data": "synthetic (seeded random images and weights; no checkpoints offline)",
+            "config": {"workload": "tracking step 384x512: MonST3R+MASt3R pair inference + "
+                                   "projective matching + Sim3 ray GN (configs[1]+[2])",
+                       "h": H, "w": W, "models": "MonST3R ViT-L/B dpt + MASt3R ViT-L/B catmlp+dpt",
+                       "parallelism": f"replicas{world}"},
+            "pair_inference_ms": pair_ms,
+            "roofline": {"bound": "mfma", "achieved": roof["tflops"], "peak": BF16_DENSE_TFLOPS,
+                         "unit": "TFLOP/s", "frac": roof["tflops"] / BF16_DENSE_TFLOPS,
+                         "traffic": None, "kernel": "gemm_kernel (bf16 MFMA GEMM / implicit conv)",
+                         "gemm_launches_per_pair": roof["launches"],
+                         "gemm_ms_per_pair": roof["gemm_ms"],
+                         "gemm_gflop_per_pair": roof["gemm_flops"] / 1e9,
+                         "avg_launch_us": roof["avg_launch_us"]},
         }
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(cfg)
-        print(json.dumps(line))
+            line["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

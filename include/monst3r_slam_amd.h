@@ -195,11 +195,13 @@ typedef struct {
 int m3s_vit_gemm(const m3s_gemm_desc* desc, void* stream);
 
 /* LayerNorm over the last dim (eps), x f32/bf16 [rows][dim] → y bf16 or f32
- * (x_is_bf16 / y_is_f32 flags); batch strides in elements.  dim ≤ 4096, dim % 4 == 0. */
+ * (x_is_bf16 / y_is_f32 flags); batch strides in elements.  dim ≤ 4096, dim % 4 == 0.
+ * Batch b of y normalises batch (b ^ x_batch_xor) of x: with x_batch_xor = 1 the
+ * decoder's norm_y(other side) (croco/blocks.py:187) runs for both sides in one launch. */
 int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_gamma,
                       const float* d_beta, void* d_y, int y_is_f32, int64_t rows, int64_t dim,
                       float eps, int64_t batch, int64_t stride_x, int64_t stride_y,
-                      int64_t stride_param, void* stream);
+                      int64_t stride_param, int x_batch_xor, void* stream);
 
 /* In-place 2-D RoPE (curope kernels.cu:17-82; pos_embed.py:106-158) on a bf16 view
  * t [B][S] rows of ld (head h at column h*64): dims [0,32) rotate by pos y, [32,64) by
@@ -223,12 +225,14 @@ int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q, const voi
 int m3s_vit_patchify(const float* d_img, void* d_out, int64_t batch, int64_t h, int64_t w,
                      void* stream);
 
-/* Bilinear x2 upsample, align_corners=True, NHWC bf16 [B][H][W][C] → [B][2H][2W][C]. */
-int m3s_vit_upsample2x(const void* d_in, void* d_out, int64_t batch, int64_t h, int64_t w,
-                       int64_t c, void* stream);
+/* Bilinear x2 upsample, align_corners=True (dpt_block.py:215-216), NHWC bf16
+ * [B][h][w][C] → [B][oh][ow][C] (oh ≤ 2h, ow ≤ 2w: the DPT crop of dpt_head.py:57);
+ * optional d_add [B][oh][ow][C] is added (fuses the fusion block's skip add). C % 8 == 0. */
+int m3s_vit_upsample2x(const void* d_in, void* d_out, const void* d_add, int64_t batch,
+                       int64_t h, int64_t w, int64_t c, int64_t oh, int64_t ow, void* stream);
 
-/* DPT regression head tail, fused: t = relu(conv3x3 output) [P][128] bf16 is reduced by
- * the final 1x1 conv (128 → 4, W4 f32 [4][128], b4 [4]) and post-processed
+/* DPT regression head tail, fused: t = relu(conv3x3 output) [B][P][128] bf16 is reduced
+ * by the final 1x1 conv (128 → 4, per-head W4 f32 [B][4][128], b4 [B][4]) and post-processed
  * (d3r/heads/postprocess.py:10-58): pts3d = xyz/max(|xyz|,1e-8) * expm1(|xyz|),
  * conf = conf_min + exp(c).  pts3d f32 [P][3], conf f32 [P]. */
 int m3s_vit_dpt_out(const void* d_t, const float* d_w4, const float* d_b4, float* d_pts3d,

@@ -13,7 +13,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
                                                         const float* __restrict__ beta,
                                                         void* __restrict__ y, int64_t rows,
                                                         int dim, float eps, int64_t sx,
-                                                        int64_t sy, int64_t sp) {
+                                                        int64_t sy, int64_t sp, int xxor) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t b = blockIdx.y;
@@ -29,13 +29,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
     const int c4 = lane + i * 64;
     if (c4 < nvec) {
       if (XBF) {
-        const bf16_t* xr = reinterpret_cast<const bf16_t*>(x) + b * sx + row * dim;
+        const bf16_t* xr = reinterpret_cast<const bf16_t*>(x) + (b ^ xxor) * sx + row * dim;
         const uint2 raw = *reinterpret_cast<const uint2*>(xr + 4 * c4);
         const bf16_t* e = reinterpret_cast<const bf16_t*>(&raw);
 #pragma unroll
         for (int k = 0; k < 4; k++) v[i][k] = bf2f(e[k]);
       } else {
-        const float* xr = reinterpret_cast<const float*>(x) + b * sx + row * dim;
+        const float* xr = reinterpret_cast<const float*>(x) + (b ^ xxor) * sx + row * dim;
         const float4 f = *reinterpret_cast<const float4*>(xr + 4 * c4);
         v[i][0] = f.x;
         v[i][1] = f.y;
@@ -115,18 +115,20 @@ __global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__
 
 // ---- bilinear x2, align_corners=True (torch upsample_bilinear2d formula) -------------
 __global__ __launch_bounds__(256) void upsample2x_kernel(const bf16_t* __restrict__ in,
-                                                         bf16_t* __restrict__ out, int h, int w,
-                                                         int c, int64_t total) {
+                                                         bf16_t* __restrict__ out,
+                                                         const bf16_t* __restrict__ addend,
+                                                         int h, int w, int c, int oh, int ow,
+                                                         int64_t total) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
   const int c8 = c / 8;
   const int cc = (int)(idx % c8) * 8;
   int64_t t = idx / c8;
-  const int H2 = 2 * h, W2 = 2 * w;
-  const int ox = (int)(t % W2);
-  t /= W2;
-  const int oy = (int)(t % H2);
-  const int64_t b = t / H2;
+  const int H2 = 2 * h, W2 = 2 * w;  // interpolation grid; the output keeps [0,oh)x[0,ow)
+  const int ox = (int)(t % ow);
+  t /= ow;
+  const int oy = (int)(t % oh);
+  const int64_t b = t / oh;
   const float sh = H2 > 1 ? (float)(h - 1) / (float)(H2 - 1) : 0.f;
   const float sw = W2 > 1 ? (float)(w - 1) / (float)(W2 - 1) : 0.f;
   const float fy = sh * (float)oy, fx = sw * (float)ox;
@@ -139,14 +141,18 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const bf16_t* __restric
   const bf16x8 bb = *reinterpret_cast<const bf16x8*>(base + ((int64_t)y0 * w + x1) * c + cc);
   const bf16x8 cq = *reinterpret_cast<const bf16x8*>(base + ((int64_t)y1 * w + x0) * c + cc);
   const bf16x8 dq = *reinterpret_cast<const bf16x8*>(base + ((int64_t)y1 * w + x1) * c + cc);
+  const int64_t oidx = (((b * oh + oy) * (int64_t)ow) + ox) * c + cc;
+  bf16x8 ad = {};
+  if (addend) ad = *reinterpret_cast<const bf16x8*>(addend + oidx);
   bf16x8 o;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    const float v = hy * (hx * bf2f(a[k]) + lx * bf2f(bb[k])) +
-                    ly * (hx * bf2f(cq[k]) + lx * bf2f(dq[k]));
+    float v = hy * (hx * bf2f(a[k]) + lx * bf2f(bb[k])) +
+              ly * (hx * bf2f(cq[k]) + lx * bf2f(dq[k]));
+    if (addend) v += bf2f(ad[k]);
     o[k] = f2bf(v);
   }
-  *reinterpret_cast<bf16x8*>(out + (((b * H2 + oy) * (int64_t)W2) + ox) * c + cc) = o;
+  *reinterpret_cast<bf16x8*>(out + oidx) = o;
 }
 
 // ---- DPT output tail: 1x1 conv 128→4 + postprocess ------------------------------------
@@ -157,10 +163,12 @@ __global__ __launch_bounds__(256) void dpt_out_kernel(const bf16_t* __restrict__
                                                       float* __restrict__ conf, int64_t pixels,
                                                       float conf_min, int64_t st, int64_t so) {
   __shared__ float sw[4 * 128];
+  const int64_t b = blockIdx.y;
+  w4 += b * 512;  // per-head weights: w4 [B][4][128], b4 [B][4]
+  b4 += b * 4;
   for (int i = threadIdx.x; i < 512; i += 256) sw[i] = w4[i];
   __syncthreads();
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t b = blockIdx.y;
   if (p >= pixels) return;
   const bf16_t* row = t + b * st + p * 128;
   float acc[4] = {b4[0], b4[1], b4[2], b4[3]};
@@ -223,23 +231,24 @@ __global__ __launch_bounds__(256) void local_feat_kernel(const float* __restrict
 extern "C" int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_gamma,
                                  const float* d_beta, void* d_y, int y_is_f32, int64_t rows,
                                  int64_t dim, float eps, int64_t batch, int64_t stride_x,
-                                 int64_t stride_y, int64_t stride_param, void* stream) {
+                                 int64_t stride_y, int64_t stride_param, int x_batch_xor,
+                                 void* stream) {
   if (!d_x || !d_gamma || !d_beta || !d_y || rows <= 0 || batch <= 0) return M3S_ERR_INVALID_ARG;
   if (dim % 4 || dim > 4096 || dim <= 0) return M3S_ERR_INVALID_ARG;
   dim3 grid(m3s_div_up(rows, 4), (unsigned)batch);
   hipStream_t s = m3s_stream(stream);
   if (x_is_bf16 && !y_is_f32)
     hipLaunchKernelGGL((layernorm_kernel<true, false>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param);
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, x_batch_xor);
   else if (x_is_bf16 && y_is_f32)
     hipLaunchKernelGGL((layernorm_kernel<true, true>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param);
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, x_batch_xor);
   else if (!x_is_bf16 && !y_is_f32)
     hipLaunchKernelGGL((layernorm_kernel<false, false>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param);
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, x_batch_xor);
   else
     hipLaunchKernelGGL((layernorm_kernel<false, true>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param);
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, x_batch_xor);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }
@@ -256,13 +265,16 @@ extern "C" int m3s_vit_patchify(const float* d_img, void* d_out, int64_t batch, 
   return M3S_OK;
 }
 
-extern "C" int m3s_vit_upsample2x(const void* d_in, void* d_out, int64_t batch, int64_t h,
-                                  int64_t w, int64_t c, void* stream) {
+extern "C" int m3s_vit_upsample2x(const void* d_in, void* d_out, const void* d_add,
+                                  int64_t batch, int64_t h, int64_t w, int64_t c, int64_t oh,
+                                  int64_t ow, void* stream) {
   if (!d_in || !d_out || batch <= 0 || h <= 0 || w <= 0 || c % 8) return M3S_ERR_INVALID_ARG;
-  const int64_t total = batch * 4 * h * w * (c / 8);
+  if (oh <= 0 || ow <= 0 || oh > 2 * h || ow > 2 * w) return M3S_ERR_INVALID_ARG;
+  const int64_t total = batch * oh * ow * (c / 8);
   hipLaunchKernelGGL(upsample2x_kernel, dim3(m3s_div_up(total, 256)), dim3(256), 0,
                      m3s_stream(stream), reinterpret_cast<const bf16_t*>(d_in),
-                     reinterpret_cast<bf16_t*>(d_out), (int)h, (int)w, (int)c, total);
+                     reinterpret_cast<bf16_t*>(d_out), reinterpret_cast<const bf16_t*>(d_add),
+                     (int)h, (int)w, (int)c, (int)oh, (int)ow, total);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }

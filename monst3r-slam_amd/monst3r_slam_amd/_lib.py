@@ -43,7 +43,35 @@ SIGNATURES = {
                             _P]),
     "m3s_track_calib": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _F, _F, _F, _F,
                              _I, _F, _F, _P, _P, _P, _P, _P]),
+    "m3s_vit_gemm": (_I, [_P, _P]),
+    "m3s_vit_layernorm": (_I, [_P, _I, _P, _P, _P, _I, _I64, _I64, _F, _I64, _I64, _I64, _I64, _I,
+                               _P]),
+    "m3s_vit_rope": (_I, [_P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _F, _P]),
+    "m3s_vit_attention": (_I, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _I64, _I64,
+                               _I64, _I64, _I64, _I64, _F, _P]),
+    "m3s_vit_patchify": (_I, [_P, _P, _I64, _I64, _I64, _P]),
+    "m3s_vit_upsample2x": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "m3s_vit_dpt_out": (_I, [_P, _P, _P, _P, _P, _I64, _F, _I64, _I64, _I64, _P]),
+    "m3s_vit_local_features": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P]),
 }
+
+
+class GemmDesc(ctypes.Structure):
+    """m3s_gemm_desc (include/monst3r_slam_amd.h)."""
+    _fields_ = [("A", _P), ("lda", _I64), ("strideA", _I64),
+                ("B", _P), ("ldb", _I64), ("strideB", _I64),
+                ("C", _P), ("ldc", _I64), ("strideC", _I64),
+                ("bias", _P), ("strideBias", _I64),
+                ("R", _P), ("ldr", _I64), ("strideR", _I64),
+                ("M", ctypes.c_int32), ("N", ctypes.c_int32), ("K", ctypes.c_int32),
+                ("batch", ctypes.c_int32), ("flags", ctypes.c_int32), ("mode", ctypes.c_int32),
+                ("Hin", ctypes.c_int32), ("Win", ctypes.c_int32), ("Cin", ctypes.c_int32),
+                ("Hout", ctypes.c_int32), ("Wout", ctypes.c_int32), ("stride", ctypes.c_int32),
+                ("ct_s", ctypes.c_int32), ("ct_cout", ctypes.c_int32), ("ct_gw", ctypes.c_int32)]
+
+
+EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT = (
+    1, 2, 4, 8, 16, 32, 64, 128)
 
 _lib = None
 

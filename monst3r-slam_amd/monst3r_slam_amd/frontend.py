@@ -1,0 +1,114 @@
+"""Frontend tracking step — mirror of FrameTracker2.track (tracker2.py:70-270) with
+use_dynamic_mask=False, on the MI355X path:
+
+  pair inference  monst3r_asymmetric_inference (monst3r_utils.py:255-297) → model.PairModel
+  matching        matching.match (matching.py:8-90)                     → matching.match
+  glue            Qk, update_pointmap, get_points_poses, valid_opt (tracker2.py:127-213,
+                  272-297; frame.py:60-124 'weighted_pointmap')         → torch plumbing
+  pose GN         opt_pose_ray_dist_sim3 / opt_pose_calib_sim3          → tracker (fused HIP)
+  keyframe update T_CkCf.act(Xkf) + weighted fusion, new-keyframe test (tracker2.py:238-257)
+
+State kept on the device (the reference keeps it in shared-memory tensors, frame.py:243):
+keyframe X_canon / C / N / T_WC / cached encoder features.  `track` performs no host
+synchronisation except for the returned booleans (read lazily)."""
+from __future__ import annotations
+
+import dataclasses
+
+import torch
+
+from . import matching as M
+from . import tracker as T
+from .config import config as _config
+
+
+@dataclasses.dataclass
+class KeyframeState:
+    X_canon: torch.Tensor   # [N,3] f32
+    C: torch.Tensor         # [N,1] f32 (accumulated confidence)
+    N: torch.Tensor         # [1] f32 update count (device: graph-capturable)
+    T_WC: torch.Tensor      # [8] f32
+    feat: torch.Tensor      # [1,S,E] bf16 (MonST3R encoder features)
+    img: torch.Tensor       # [1,3,H,W]
+
+
+def sim3_act(T, X):
+    """lietorch Sim3.act on [...,3] points (s R X + t), T = [t, q xyzw, s]."""
+    t, q, s = T[:3], T[3:7], T[7]
+    uv = 2.0 * torch.cross(q[:3].expand_as(X), X, dim=-1)
+    return s * (X + q[3] * uv + torch.cross(q[:3].expand_as(X), uv, dim=-1)) + t
+
+
+class Tracker:
+    def __init__(self, model, cfg=None):
+        self.model = model
+        self.cfg = cfg or _config
+        self.idx_f2k = None
+        self.kf = None
+
+    def add_keyframe(self, img, T_WC, X=None, C=None, feat=None):
+        if feat is None:
+            feat, _ = self.model.encode(img)
+            feat = feat.clone()
+        if X is None:
+            out = self.model.pair(img, feat_j=feat)
+            n = out["X"].shape[1] * out["X"].shape[2]
+            X = out["X"][0].reshape(n, 3).clone()
+            C = out["C"][0].reshape(n, 1).clone()
+        self.kf = KeyframeState(X, C, torch.ones(1, device=X.device), T_WC.clone(), feat, img)
+        self.reset_idx_f2k(X.shape[0], X.device)
+
+    def reset_idx_f2k(self, n, device):
+        """tracker2.py:66-67 (None → identity mapping); kept as a persistent buffer so a
+        captured graph sees the previous frame's matches."""
+        self.idx_f2k = torch.arange(n, device=device, dtype=torch.int64)[None].contiguous()
+
+    def track(self, img, T_WCf_init=None):
+        """One frame.  Returns dict(new_kf, lost, T_WCf, idx_f2k, match_frac, info, ...);
+        the scalar flags are device tensors."""
+        cfg_t = self.cfg["tracking"]
+        kf = self.kf
+        out = self.model.pair(img, feat_j=kf.feat)
+        Xii, Xji = out["X"][0:1], out["X"][1:2]
+        H, W = Xii.shape[1:3]
+        n = H * W
+        # matching.match(Xii, Xji, Dii, Dji, idx_init)  (monst3r_utils.py:498-499)
+        idx, valid_match = M.match(Xii, Xji, out["D16"][0:1], out["D16"][1:2], self.idx_f2k,
+                                   self.cfg["matching"])
+        self.idx_f2k.copy_(idx)
+        idx = idx[0]
+        valid_match = valid_match[0]                       # [N,1]
+        Qff = out["Q"][0].reshape(n, 1)
+        Qkf = out["Q"][1].reshape(n, 1)
+        Qk = torch.sqrt(Qff[idx] * Qkf)                    # tracker2.py:130
+        # frame.update_pointmap(Xff, Cff) on a fresh frame (N == 0): X_canon = X, C = C
+        Xf_canon = out["X"][0].reshape(n, 3)
+        Cf = out["C"][0].reshape(n, 1)
+        Xkf = out["X"][1].reshape(n, 3)
+        Ckf = out["C"][1].reshape(n, 1)
+        # get_points_poses (use_calib False): Xf[idx], Xk, Cf[idx], Ck = C/N
+        Xf = Xf_canon[idx]
+        Ck = kf.C / kf.N
+        Cfi = Cf[idx]
+        valid_Q = Qk > cfg_t["Q_conf"]
+        valid_opt = valid_match & (Cfi > cfg_t["C_conf"]) & (Ck > cfg_t["C_conf"]) & valid_Q
+        valid_kf = valid_match & valid_Q
+        match_frac = valid_opt.float().mean()
+        T_WCf0 = kf.T_WC if T_WCf_init is None else T_WCf_init
+        T_WCf, T_CkCf, info = T.opt_pose_ray_dist_sim3(Xf, kf.X_canon, T_WCf0, kf.T_WC, Qk,
+                                                       valid_opt, cfg_t, check=False)
+        # keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) — weighted_pointmap (frame.py:105-109)
+        Xkk = sim3_act(T_CkCf, Xkf)
+        kf.X_canon.copy_((kf.C * kf.X_canon + Ckf * Xkk) / (kf.C + Ckf))
+        kf.C.add_(Ckf)
+        kf.N.add_(1.0)
+        # keyframe selection (tracker2.py:246-257)
+        match_frac_k = valid_kf.float().mean()
+        sel = torch.zeros(n, dtype=torch.int32, device=idx.device)
+        sel.index_add_(0, idx, valid_match[:, 0].int())    # |unique(idx[valid])|, no sort/sync
+        unique_frac_f = (sel > 0).sum().float() / n
+        new_kf = torch.minimum(match_frac_k, unique_frac_f) < cfg_t["match_frac_thresh"]
+        lost = (match_frac < cfg_t["min_match_frac"]) | (info[1] != 0)
+        return dict(new_kf=new_kf, lost=lost, T_WCf=T_WCf, T_CkCf=T_CkCf, idx_f2k=idx,
+                    valid_match=valid_match, match_frac=match_frac, info=info,
+                    feat_i=out["feat_i"], pair=out)

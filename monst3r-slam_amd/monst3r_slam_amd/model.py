@@ -1,0 +1,528 @@
+"""MonST3R + MASt3R pair inference on the MI355X kernels (C ABI, bf16 MFMA).
+
+Mirrors the reference's model-level operator API used by the SLAM frontend:
+  _encode_image (d3r/model.py:127-139)  → PairModel.encode
+  _decoder      (d3r/model.py:171-190)  → both models x both sides in ONE batched pass
+  _downstream_head + postprocess        → all four DPT heads batched; MASt3R catmlp tail
+  monst3r_asymmetric_inference (mast3r_slam/monst3r_utils.py:255-297) → PairModel.pair
+Design:
+  * residual streams f32, GEMM operands bf16, MFMA f32 accumulation;
+  * z = model*2 + side batches the two decoder sides and the two models (4 independent
+    problems with their own weights) into every decoder GEMM / attention / LN launch,
+    and the four DPT heads likewise — M = 768 tokens alone fills only ~1/2 of the CUs;
+  * DPT on NHWC bf16 with implicit-GEMM 3x3 convs (ReLU prologue, bias + residual
+    epilogue), ConvTranspose(k=s) as GEMM + scatter epilogue, the fusion block's 1x1
+    out_conv applied BEFORE the x2 upsample (linear ops commute; bilinear weights sum to
+    one) and the skip add fused into the upsample;
+  * the final 1x1 conv (128→4) + reg_dense_depth/conf fused in one tail kernel; the
+    MASt3R MLP tail fused with pixel_shuffle + desc normalisation, emitting f16
+    descriptors for matching directly (== .half() of the f32 unit vectors).
+Weights: seeded random (monst3r_slam_amd.weights) — no checkpoints offline.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from . import weights as Wt
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+LN_EPS = 1e-6
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class Ops:
+    """Thin, checked wrappers over the ViT C ABI on the current torch stream."""
+
+    def __init__(self, dev):
+        self.lib = _lib.load()
+        self.dev = dev
+        self.probe = None  # list → (start_event, end_event, flops) per GEMM (bench roofline)
+
+    def _s(self):
+        return _lib.stream(self.dev)
+
+    def gemm(self, A, B, C, M, N, K, batch=1, *, lda=None, ldb=None, ldc=None, sA=0, sB=0,
+             sC=0, bias=None, sBias=0, R=None, ldr=None, sR=0, flags=0, conv=None, convt=None):
+        d = _lib.GemmDesc()
+        d.A, d.lda, d.strideA = _p(A), lda if lda is not None else K, sA
+        d.B, d.ldb, d.strideB = _p(B), ldb if ldb is not None else K, sB
+        d.C, d.ldc, d.strideC = _p(C), ldc if ldc is not None else N, sC
+        d.bias, d.strideBias = _p(bias), sBias
+        d.R, d.ldr, d.strideR = _p(R), ldr if ldr is not None else N, sR
+        d.M, d.N, d.K, d.batch, d.flags = M, N, K, batch, flags
+        if bias is not None:
+            d.flags |= _lib.EPI_BIAS
+        if conv is not None:
+            d.mode = 1
+            d.Hin, d.Win, d.Cin, d.Hout, d.Wout, d.stride = conv
+        if convt is not None:
+            d.flags |= _lib.EPI_CONVT
+            d.ct_s, d.ct_cout, d.ct_gw = convt
+        if self.probe is not None:
+            st = torch.cuda.current_stream(self.dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            _lib.check(self.lib.m3s_vit_gemm(ctypes.byref(d), self._s()), "vit_gemm")
+            e1.record(st)
+            self.probe.append((e0, e1, 2.0 * M * N * K * batch))
+            return
+        _lib.check(self.lib.m3s_vit_gemm(ctypes.byref(d), self._s()), "vit_gemm")
+
+    def ln(self, x, g, b, y, rows, dim, batch=1, sx=0, sy=0, sp=0, y_f32=False, xor=0):
+        _lib.check(self.lib.m3s_vit_layernorm(
+            _p(x), int(x.dtype == BF16), _p(g), _p(b), _p(y), int(y_f32), rows, dim, LN_EPS,
+            batch, sx, sy, sp, xor, self._s()), "vit_layernorm")
+
+    def rope(self, t, ld, stride, pos, stride_pos, batch, S, heads, base):
+        _lib.check(self.lib.m3s_vit_rope(_p(t), ld, stride, _p(pos), stride_pos, batch, S, heads,
+                                         float(base), self._s()), "vit_rope")
+
+    def attn(self, q, ldq, sq_b, k, v, ldkv, skv_b, o, ldo, so_b, batch, heads, sq, sk):
+        _lib.check(self.lib.m3s_vit_attention(_p(q), ldq, sq_b, _p(k), _p(v), ldkv, skv_b, None,
+                                              None, 0, _p(o), ldo, so_b, batch, heads, sq, sk, 0.0,
+                                              self._s()), "vit_attention")
+
+    def patchify(self, img, out, b, h, w):
+        _lib.check(self.lib.m3s_vit_patchify(_p(img), _p(out), b, h, w, self._s()), "patchify")
+
+    def up2(self, x, out, b, h, w, c, oh=None, ow=None, add=None):
+        _lib.check(self.lib.m3s_vit_upsample2x(_p(x), _p(out), _p(add), b, h, w, c,
+                                               oh or 2 * h, ow or 2 * w, self._s()), "upsample2x")
+
+    def dpt_out(self, t, w4, b4, pts, conf, pixels, conf_min, batch, st, so):
+        _lib.check(self.lib.m3s_vit_dpt_out(_p(t), _p(w4), _p(b4), _p(pts), _p(conf), pixels,
+                                            float(conf_min), batch, st, so, self._s()), "dpt_out")
+
+    def local_features(self, feats, desc, desc16, dconf, b, h, w):
+        _lib.check(self.lib.m3s_vit_local_features(_p(feats), _p(desc), _p(desc16), _p(dconf), b,
+                                                   h, w, self._s()), "local_features")
+
+
+# ---------------------------------------------------------------------------------------
+# weight packing
+# ---------------------------------------------------------------------------------------
+def _conv_pack(w):
+    """[Cout][Cin][k][k] → [Cout][k][k][Cin] flattened (implicit-GEMM K order ky, kx, ci)."""
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+
+
+def _convt_pack(w):
+    """ConvTranspose [Cin][Cout][s][s] → [(a, b, co)][ci]."""
+    return w.permute(2, 3, 1, 0).reshape(-1, w.shape[0])
+
+
+class PackedWeights:
+    """Device weights.  Encoder from MonST3R; decoders and heads stacked over
+    z = model*2 + side (model 0 = MonST3R, 1 = MASt3R; side 0 = dec_blocks/head1,
+    side 1 = dec_blocks2/head2)."""
+
+    def __init__(self, sd_monst3r, arch_monst3r, sd_mast3r, arch_mast3r, device):
+        am, aM = arch_monst3r, arch_mast3r
+        assert (am.enc_dim, am.dec_dim, am.enc_depth, am.dec_depth) == \
+               (aM.enc_dim, aM.dec_dim, aM.enc_depth, aM.dec_depth)
+        self.arch, self.arch_mast3r = am, aM
+        dev = device
+        bf = lambda t: t.to(device=dev, dtype=BF16).contiguous()  # noqa: E731
+        f32 = lambda t: t.to(device=dev, dtype=F32).contiguous()  # noqa: E731
+        sdm = sd_monst3r
+        E, L = am.enc_dim, am.enc_depth
+        # ---- encoder (MonST3R weights only: monst3r_utils.py:262-269) ----
+        self.patch_w = bf(sdm["patch_embed.proj.weight"].reshape(E, -1))
+        self.patch_b = f32(sdm["patch_embed.proj.bias"])
+        st = lambda key: torch.stack([sdm[f"enc_blocks.{i}.{key}"] for i in range(L)])  # noqa
+        self.enc = dict(
+            ln1_g=f32(st("norm1.weight")), ln1_b=f32(st("norm1.bias")),
+            qkv_w=bf(st("attn.qkv.weight")), qkv_b=f32(st("attn.qkv.bias")),
+            proj_w=bf(st("attn.proj.weight")), proj_b=f32(st("attn.proj.bias")),
+            ln2_g=f32(st("norm2.weight")), ln2_b=f32(st("norm2.bias")),
+            fc1_w=bf(st("mlp.fc1.weight")), fc1_b=f32(st("mlp.fc1.bias")),
+            fc2_w=bf(st("mlp.fc2.weight")), fc2_b=f32(st("mlp.fc2.bias")))
+        self.enc_norm_g = f32(sdm["enc_norm.weight"])
+        self.enc_norm_b = f32(sdm["enc_norm.bias"])
+        # ---- decoders, z = model*2 + side ----
+        sds = [sd_monst3r, sd_monst3r, sd_mast3r, sd_mast3r]
+        blk = ["dec_blocks", "dec_blocks2", "dec_blocks", "dec_blocks2"]
+
+        def dz(key, layer=None):
+            ts = []
+            for z in range(4):
+                name = key if layer is None else f"{blk[z]}.{layer}.{key}"
+                ts.append(sds[z][name])
+            return torch.stack(ts)
+
+        self.dec_embed_w = bf(dz("decoder_embed.weight"))
+        self.dec_embed_b = f32(dz("decoder_embed.bias"))
+        self.dec = []
+        for i in range(am.dec_depth):
+            kv_w = torch.cat([dz("cross_attn.projk.weight", i), dz("cross_attn.projv.weight", i)], 1)
+            kv_b = torch.cat([dz("cross_attn.projk.bias", i), dz("cross_attn.projv.bias", i)], 1)
+            self.dec.append(dict(
+                ln1_g=f32(dz("norm1.weight", i)), ln1_b=f32(dz("norm1.bias", i)),
+                qkv_w=bf(dz("attn.qkv.weight", i)), qkv_b=f32(dz("attn.qkv.bias", i)),
+                proj_w=bf(dz("attn.proj.weight", i)), proj_b=f32(dz("attn.proj.bias", i)),
+                ln2_g=f32(dz("norm2.weight", i)), ln2_b=f32(dz("norm2.bias", i)),
+                lny_g=f32(dz("norm_y.weight", i)), lny_b=f32(dz("norm_y.bias", i)),
+                q_w=bf(dz("cross_attn.projq.weight", i)), q_b=f32(dz("cross_attn.projq.bias", i)),
+                kv_w=bf(kv_w), kv_b=f32(kv_b),
+                cproj_w=bf(dz("cross_attn.proj.weight", i)),
+                cproj_b=f32(dz("cross_attn.proj.bias", i)),
+                ln3_g=f32(dz("norm3.weight", i)), ln3_b=f32(dz("norm3.bias", i)),
+                fc1_w=bf(dz("mlp.fc1.weight", i)), fc1_b=f32(dz("mlp.fc1.bias", i)),
+                fc2_w=bf(dz("mlp.fc2.weight", i)), fc2_b=f32(dz("mlp.fc2.bias", i))))
+        self.dec_norm_g = f32(dz("dec_norm.weight"))
+        self.dec_norm_b = f32(dz("dec_norm.bias"))
+        # ---- DPT heads, z = model*2 + side ----
+        hd = ["downstream_head1", "downstream_head2", "downstream_head1", "downstream_head2"]
+
+        def hz(key, pack=None):
+            ts = []
+            for z in range(4):
+                t = sds[z][f"{hd[z]}.dpt.{key}"]
+                ts.append(pack(t) if pack else t)
+            return torch.stack(ts)
+
+        ap = "act_postprocess."
+        self.h = dict(
+            ap0_w=bf(hz(ap + "0.0.weight", _conv_pack)), ap0_b=f32(hz(ap + "0.0.bias")),
+            ap0t_w=bf(hz(ap + "0.1.weight", _convt_pack)), ap0t_b=f32(hz(ap + "0.1.bias")),
+            ap1_w=bf(hz(ap + "1.0.weight", _conv_pack)), ap1_b=f32(hz(ap + "1.0.bias")),
+            ap1t_w=bf(hz(ap + "1.1.weight", _convt_pack)), ap1t_b=f32(hz(ap + "1.1.bias")),
+            ap2_w=bf(hz(ap + "2.0.weight", _conv_pack)), ap2_b=f32(hz(ap + "2.0.bias")),
+            ap3_w=bf(hz(ap + "3.0.weight", _conv_pack)), ap3_b=f32(hz(ap + "3.0.bias")),
+            ap3c_w=bf(hz(ap + "3.1.weight", _conv_pack)), ap3c_b=f32(hz(ap + "3.1.bias")),
+            head0_w=bf(hz("head.0.weight", _conv_pack)), head0_b=f32(hz("head.0.bias")),
+            head2_w=bf(hz("head.2.weight", _conv_pack)), head2_b=f32(hz("head.2.bias")),
+            head4_w=f32(hz("head.4.weight", lambda t: t.reshape(t.shape[0], -1))),
+            head4_b=f32(hz("head.4.bias")))
+        for k in range(4):
+            self.h[f"rn{k}_w"] = bf(hz(f"scratch.layer{k + 1}_rn.weight", _conv_pack))
+        for k in range(1, 5):
+            q = f"scratch.refinenet{k}."
+            self.h[f"r{k}_out_w"] = bf(hz(q + "out_conv.weight", _conv_pack))
+            self.h[f"r{k}_out_b"] = f32(hz(q + "out_conv.bias"))
+            for u in (1, 2):
+                for c in (1, 2):
+                    key = f"resConfUnit{u}.conv{c}"
+                    self.h[f"r{k}_u{u}c{c}_w"] = bf(hz(q + key + ".weight", _conv_pack))
+                    self.h[f"r{k}_u{u}c{c}_b"] = f32(hz(q + key + ".bias"))
+        # ---- MASt3R local features (model 1 only: z = 2, 3) ----
+        lf = ["downstream_head1", "downstream_head2"]
+        self.lf_fc1_w = bf(torch.stack([sd_mast3r[f"{h}.head_local_features.fc1.weight"] for h in lf]))
+        self.lf_fc1_b = f32(torch.stack([sd_mast3r[f"{h}.head_local_features.fc1.bias"] for h in lf]))
+        self.lf_fc2_w = bf(torch.stack([sd_mast3r[f"{h}.head_local_features.fc2.weight"] for h in lf]))
+        self.lf_fc2_b = f32(torch.stack([sd_mast3r[f"{h}.head_local_features.fc2.bias"] for h in lf]))
+
+
+# ---------------------------------------------------------------------------------------
+# model runner
+# ---------------------------------------------------------------------------------------
+class PairModel:
+    """Frame/keyframe pair inference.  Buffers are allocated once per image size."""
+
+    def __init__(self, packed: PackedWeights, device):
+        self.w = packed
+        self.a = packed.arch
+        self.dev = device
+        self.ops = Ops(device)
+        self._bufs = {}
+
+    # ---- buffers ----
+    def _buf(self, key, shape, dtype):
+        t = self._bufs.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=self.dev)
+            self._bufs[key] = t
+        return t
+
+    def positions(self, b, gh, gw):
+        key = ("pos", b, gh, gw)
+        t = self._bufs.get(key)
+        if t is None:
+            y = torch.arange(gh, device=self.dev)
+            x = torch.arange(gw, device=self.dev)
+            t = torch.cartesian_prod(y, x).view(1, gh * gw, 2).expand(b, -1, 2).contiguous()
+            self._bufs[key] = t
+        return t
+
+    # ---- encoder: PatchEmbed + 24 blocks + enc_norm (batch of B images as M = B*S) ----
+    def encode(self, img, out=None):
+        """img f32 [B,3,H,W] → feat bf16 [B,S,E], pos int64 [B,S,2]."""
+        o, a, W = self.ops, self.a, self.w
+        B, _, H, Wd = img.shape
+        gh, gw = H // a.patch, Wd // a.patch
+        S, E = gh * gw, a.enc_dim
+        M = B * S
+        img = img.to(F32).contiguous()
+        patches = self._buf("enc_patch", (M, 3 * a.patch * a.patch), BF16)
+        o.patchify(img, patches, B, H, Wd)
+        x = self._buf("enc_x", (M, E), F32)
+        o.gemm(patches, W.patch_w, x, M, E, 3 * a.patch * a.patch, bias=W.patch_b,
+               flags=_lib.EPI_OUT_F32)
+        xn = self._buf("enc_xn", (M, E), BF16)
+        qkv = self._buf("enc_qkv", (M, 3 * E), BF16)
+        att = self._buf("enc_att", (M, E), BF16)
+        hid = self._buf("enc_hid", (M, a.mlp_ratio * E), BF16)
+        pos = self.positions(B, gh, gw)
+        P = W.enc
+        for i in range(a.enc_depth):
+            o.ln(x, P["ln1_g"][i], P["ln1_b"][i], xn, M, E)
+            o.gemm(xn, P["qkv_w"][i], qkv, M, 3 * E, E, bias=P["qkv_b"][i])
+            o.rope(qkv, 3 * E, S * 3 * E, pos, S * 2, B, S, a.enc_heads, a.rope_base)
+            o.rope(qkv[:, E:], 3 * E, S * 3 * E, pos, S * 2, B, S, a.enc_heads, a.rope_base)
+            o.attn(qkv, 3 * E, S * 3 * E, qkv[:, E:], qkv[:, 2 * E:], 3 * E, S * 3 * E, att, E,
+                   S * E, B, a.enc_heads, S, S)
+            o.gemm(att, P["proj_w"][i], x, M, E, E, bias=P["proj_b"][i], R=x,
+                   flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32)
+            o.ln(x, P["ln2_g"][i], P["ln2_b"][i], xn, M, E)
+            o.gemm(xn, P["fc1_w"][i], hid, M, a.mlp_ratio * E, E, bias=P["fc1_b"][i],
+                   flags=_lib.EPI_GELU)
+            o.gemm(hid, P["fc2_w"][i], x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][i], R=x,
+                   flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32)
+        feat = out if out is not None else torch.empty((B, S, E), dtype=BF16, device=self.dev)
+        o.ln(x, W.enc_norm_g, W.enc_norm_b, feat, M, E)
+        return feat, pos
+
+    # ---- decoders: both models x both sides, batch z = model*2 + side ----
+    def decode(self, feat_i, feat_j, pos, gh, gw):
+        """feat_i/feat_j bf16 [S,E] (frame i = side 1, keyframe j = side 2).
+        Returns hooks dict: h0 bf16 [4,S,E], h6/h9/h12 bf16 [4,S,D] (h12 = dec_norm)."""
+        o, a, W = self.ops, self.a, self.w
+        S, E, D = gh * gw, a.enc_dim, a.dec_dim
+        Z = 4
+        h0 = self._buf("h0", (Z, S, E), BF16)
+        h0[0::2].copy_(feat_i.reshape(1, S, E).expand(2, S, E))
+        h0[1::2].copy_(feat_j.reshape(1, S, E).expand(2, S, E))
+        x = self._buf("dec_x", (Z, S, D), F32)
+        o.gemm(h0, W.dec_embed_w, x, S, D, E, Z, sA=S * E, sB=D * E, sC=S * D,
+               bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32)
+        xn = self._buf("dec_xn", (Z, S, D), BF16)
+        yn = self._buf("dec_yn", (Z, S, D), BF16)
+        qkv = self._buf("dec_qkv", (Z, S, 3 * D), BF16)
+        kv = self._buf("dec_kv", (Z, S, 2 * D), BF16)
+        q = self._buf("dec_q", (Z, S, D), BF16)
+        att = self._buf("dec_att", (Z, S, D), BF16)
+        hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), BF16)
+        hooks = {"h0": h0}
+        hk = set(a.hooks[1:3])
+        R32 = _lib.EPI_OUT_F32 | _lib.EPI_RES_F32
+        for i in range(a.dec_depth):
+            P = W.dec[i]
+            # y_ = norm_y(previous output of the other side) — before this layer updates x
+            o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1)
+            # self-attention
+            o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D)
+            o.gemm(xn, P["qkv_w"], qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
+                   bias=P["qkv_b"], sBias=3 * D)
+            o.rope(qkv, 3 * D, S * 3 * D, pos, 0, Z, S, a.dec_heads, a.rope_base)
+            o.rope(qkv[:, :, D:], 3 * D, S * 3 * D, pos, 0, Z, S, a.dec_heads, a.rope_base)
+            o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,
+                   D, S * D, Z, a.dec_heads, S, S)
+            o.gemm(att, P["proj_w"], x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["proj_b"],
+                   sBias=D, R=x, sR=S * D, flags=R32)
+            # cross-attention: q from norm2(x), k/v from y_
+            o.ln(x, P["ln2_g"], P["ln2_b"], xn, S, D, Z, S * D, S * D, D)
+            o.gemm(xn, P["q_w"], q, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["q_b"],
+                   sBias=D)
+            o.gemm(yn, P["kv_w"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D, sC=S * 2 * D,
+                   bias=P["kv_b"], sBias=2 * D)
+            o.rope(q, D, S * D, pos, 0, Z, S, a.dec_heads, a.rope_base)
+            o.rope(kv, 2 * D, S * 2 * D, pos, 0, Z, S, a.dec_heads, a.rope_base)
+            o.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, att, D, S * D, Z, a.dec_heads,
+                   S, S)
+            o.gemm(att, P["cproj_w"], x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D,
+                   bias=P["cproj_b"], sBias=D, R=x, sR=S * D, flags=R32)
+            # MLP
+            o.ln(x, P["ln3_g"], P["ln3_b"], xn, S, D, Z, S * D, S * D, D)
+            o.gemm(xn, P["fc1_w"], hid, S, a.mlp_ratio * D, D, Z, sA=S * D,
+                   sB=a.mlp_ratio * D * D, sC=S * a.mlp_ratio * D, bias=P["fc1_b"],
+                   sBias=a.mlp_ratio * D, flags=_lib.EPI_GELU)
+            o.gemm(hid, P["fc2_w"], x, S, D, a.mlp_ratio * D, Z, sA=S * a.mlp_ratio * D,
+                   sB=a.mlp_ratio * D * D, sC=S * D, bias=P["fc2_b"], sBias=D, R=x, sR=S * D,
+                   flags=R32)
+            if (i + 1) in hk:
+                hooks[f"h{i + 1}"] = x.to(BF16)
+        h12 = self._buf("h12", (Z, S, D), BF16)
+        o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D)
+        hooks["h12"] = h12
+        return hooks
+
+    # ---- DPT heads (batched over z) ----
+    def _conv3(self, x, wkey, out, b, hin, win, cin, cout, stride=1, bias_key=None, R=None,
+               flags=0):
+        o, H = self.ops, self.w.h
+        hout = (hin + 2 - 3) // stride + 1
+        wout = (win + 2 - 3) // stride + 1
+        o.gemm(x, H[wkey], out, hout * wout, cout, 9 * cin, b, sA=hin * win * cin,
+               sB=cout * 9 * cin, sC=hout * wout * cout,
+               bias=H[bias_key] if bias_key else None, sBias=cout, R=R,
+               sR=hout * wout * cout, flags=flags, conv=(hin, win, cin, hout, wout, stride))
+        return hout, wout
+
+    def _rcu(self, x, k, u, b, h, w, out, addend_res=None):
+        """ResidualConvUnit: out = conv2(relu(conv1(relu(x)))) + (x or addend_res)."""
+        F = self.a.feature_dim
+        t = self._buf(("rcu_t", h, w), (b, h, w, F), BF16)
+        self._conv3(x, f"r{k}_u{u}c1_w", t, b, h, w, F, F, bias_key=f"r{k}_u{u}c1_b",
+                    flags=_lib.PRO_RELU)
+        self._conv3(t, f"r{k}_u{u}c2_w", out, b, h, w, F, F, bias_key=f"r{k}_u{u}c2_b",
+                    R=addend_res if addend_res is not None else x,
+                    flags=_lib.PRO_RELU | _lib.EPI_RES_BF16)
+
+    def _fusion(self, k, path, skip, b, h, w, next_hw, next_skip, out):
+        """FeatureFusionBlock (dpt_block.py:185-218) at resolution (h, w):
+        s = path + RCU1(skip) (path given; skip None for refinenet4); s = RCU2(s);
+        out = up2(out_conv(s)) (+ next_skip)  — out_conv commuted before the upsample."""
+        o, H = self.ops, self.w.h
+        F = self.a.feature_dim
+        s1 = self._buf(("fus_s1", h, w), (b, h, w, F), BF16)
+        if skip is not None:
+            self._rcu(skip, k, 1, b, h, w, s1, addend_res=path)   # path + conv(..)+skip
+            # RCU1's own residual is `skip`; path is added too → addend = path + skip
+        else:
+            s1 = path
+        s2 = self._buf(("fus_s2", h, w), (b, h, w, F), BF16)
+        self._rcu(s1, k, 2, b, h, w, s2)
+        oc = self._buf(("fus_oc", h, w), (b, h, w, F), BF16)
+        o.gemm(s2, H[f"r{k}_out_w"], oc, h * w, F, F, b, sA=h * w * F, sB=F * F, sC=h * w * F,
+               bias=H[f"r{k}_out_b"], sBias=F)
+        oh, ow = next_hw
+        o.up2(oc, out, b, h, w, F, oh, ow, add=next_skip)
+
+    def heads(self, hooks, gh, gw, H, W):
+        """Four DPT heads (z = model*2 + side) + MASt3R local features.
+        Returns pts3d f32 [4,H,W,3], conf f32 [4,H,W], desc16 f16 [2,H,W,24],
+        desc f32 [2,H,W,24], desc_conf f32 [2,H,W] (the latter three for z = 2, 3)."""
+        o, a, Hw = self.ops, self.a, self.w.h
+        Z = 4
+        S, E, D = gh * gw, a.enc_dim, a.dec_dim
+        Ld = a.layer_dims
+        F = a.feature_dim
+        # act_postprocess
+        t0 = self._buf("ap_t0", (Z, S, Ld[0]), BF16)
+        o.gemm(hooks["h0"], Hw["ap0_w"], t0, S, Ld[0], E, Z, sA=S * E, sB=Ld[0] * E,
+               sC=S * Ld[0], bias=Hw["ap0_b"], sBias=Ld[0])
+        L0 = self._buf("ap_L0", (Z, 4 * gh, 4 * gw, Ld[0]), BF16)
+        o.gemm(t0, Hw["ap0t_w"], L0, S, 16 * Ld[0], Ld[0], Z, sA=S * Ld[0],
+               sB=16 * Ld[0] * Ld[0], sC=16 * S * Ld[0], bias=Hw["ap0t_b"], sBias=Ld[0],
+               convt=(4, Ld[0], gw))
+        t1 = self._buf("ap_t1", (Z, S, Ld[1]), BF16)
+        o.gemm(hooks["h6"], Hw["ap1_w"], t1, S, Ld[1], D, Z, sA=S * D, sB=Ld[1] * D,
+               sC=S * Ld[1], bias=Hw["ap1_b"], sBias=Ld[1])
+        L1 = self._buf("ap_L1", (Z, 2 * gh, 2 * gw, Ld[1]), BF16)
+        o.gemm(t1, Hw["ap1t_w"], L1, S, 4 * Ld[1], Ld[1], Z, sA=S * Ld[1], sB=4 * Ld[1] * Ld[1],
+               sC=4 * S * Ld[1], bias=Hw["ap1t_b"], sBias=Ld[1], convt=(2, Ld[1], gw))
+        L2 = self._buf("ap_L2", (Z, gh, gw, Ld[2]), BF16)
+        o.gemm(hooks["h9"], Hw["ap2_w"], L2, S, Ld[2], D, Z, sA=S * D, sB=Ld[2] * D,
+               sC=S * Ld[2], bias=Hw["ap2_b"], sBias=Ld[2])
+        t3 = self._buf("ap_t3", (Z, gh, gw, Ld[3]), BF16)
+        o.gemm(hooks["h12"], Hw["ap3_w"], t3, S, Ld[3], D, Z, sA=S * D, sB=Ld[3] * D,
+               sC=S * Ld[3], bias=Hw["ap3_b"], sBias=Ld[3])
+        g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
+        L3 = self._buf("ap_L3", (Z, g3h, g3w, Ld[3]), BF16)
+        self._conv3(t3, "ap3c_w", L3, Z, gh, gw, Ld[3], Ld[3], stride=2, bias_key="ap3c_b")
+        # layer_rn (3x3, no bias) → F channels
+        dims = [(4 * gh, 4 * gw), (2 * gh, 2 * gw), (gh, gw), (g3h, g3w)]
+        R = []
+        for k, Lk in enumerate([L0, L1, L2, L3]):
+            hh, ww = dims[k]
+            r = self._buf(f"rn{k}", (Z, hh, ww, F), BF16)
+            self._conv3(Lk, f"rn{k}_w", r, Z, hh, ww, Ld[k], F)
+            R.append(r)
+        # refinenets: path_k = up2(out_conv(RCU2(path_{k+1} + RCU1(R_k)))) with the next
+        # level's skip pre-added by the upsample (consumed as RCU1's residual addend)
+        p4 = self._buf("path4", (Z, gh, gw, F), BF16)
+        self._fusion(4, R[3], None, Z, g3h, g3w, (gh, gw), None, p4)
+        p3 = self._buf("path3", (Z, 2 * gh, 2 * gw, F), BF16)
+        self._fusion_skip(3, p4, R[2], Z, gh, gw, (2 * gh, 2 * gw), p3)
+        p2 = self._buf("path2", (Z, 4 * gh, 4 * gw, F), BF16)
+        self._fusion_skip(2, p3, R[1], Z, 2 * gh, 2 * gw, (4 * gh, 4 * gw), p2)
+        p1 = self._buf("path1", (Z, 8 * gh, 8 * gw, F), BF16)
+        self._fusion_skip(1, p2, R[0], Z, 4 * gh, 4 * gw, (8 * gh, 8 * gw), p1)
+        # head: conv3x3 F→F/2 @ (H/2, W/2), up2, conv3x3 → last_dim + ReLU, 1x1 → 4 + post
+        h2, w2 = 8 * gh, 8 * gw
+        hd0 = self._buf("head0", (Z, h2, w2, F // 2), BF16)
+        self._conv3(p1, "head0_w", hd0, Z, h2, w2, F, F // 2, bias_key="head0_b")
+        hup = self._buf("head_up", (Z, H, W, F // 2), BF16)
+        o.up2(hd0, hup, Z, h2, w2, F // 2, H, W)
+        hd2 = self._buf("head2", (Z, H, W, a.last_dim), BF16)
+        self._conv3(hup, "head2_w", hd2, Z, H, W, F // 2, a.last_dim, bias_key="head2_b",
+                    flags=_lib.EPI_RELU)
+        pts = self._buf("pts3d", (Z, H, W, 3), F32)
+        conf = self._buf("conf", (Z, H, W), F32)
+        o.dpt_out(hd2, Hw["head4_w"], Hw["head4_b"], pts, conf, H * W, a.conf_min, Z,
+                  H * W * a.last_dim, H * W)
+        # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle
+        aM = self.w.arch_mast3r
+        idim = E + D
+        hidd = 4 * idim
+        odim = (aM.desc_dim + 1) * aM.patch ** 2
+        cat = self._buf("lf_cat", (2, S, idim), BF16)
+        cat[:, :, :E].copy_(hooks["h0"][2:])
+        cat[:, :, E:].copy_(hooks["h12"][2:])
+        lh = self._buf("lf_hid", (2, S, hidd), BF16)
+        o.gemm(cat, self.w.lf_fc1_w, lh, S, hidd, idim, 2, sA=S * idim, sB=hidd * idim,
+               sC=S * hidd, bias=self.w.lf_fc1_b, sBias=hidd, flags=_lib.EPI_GELU)
+        lo = self._buf("lf_out", (2, S, odim), F32)
+        o.gemm(lh, self.w.lf_fc2_w, lo, S, odim, hidd, 2, sA=S * hidd, sB=odim * hidd,
+               sC=S * odim, bias=self.w.lf_fc2_b, sBias=odim, flags=_lib.EPI_OUT_F32)
+        desc = self._buf("desc", (2, H, W, aM.desc_dim), F32)
+        desc16 = self._buf("desc16", (2, H, W, aM.desc_dim), torch.float16)
+        dconf = self._buf("desc_conf", (2, H, W), F32)
+        o.local_features(lo, desc, desc16, dconf, 2, H, W)
+        return pts, conf, desc16, desc, dconf
+
+    def _fusion_skip(self, k, path, skip, b, h, w, next_hw, out):
+        """refinenet_k(path, skip): s = path + RCU1(skip) = conv2(...) + (skip + path)."""
+        F = self.a.feature_dim
+        sp = self._buf(("fus_sp", h, w), (b, h, w, F), BF16)
+        torch.add(skip, path, out=sp)
+        self._fusion(k, sp, skip, b, h, w, next_hw, None, out)
+
+    # ---- monst3r_asymmetric_inference ----
+    def pair(self, img_i, feat_j=None, img_j=None):
+        """Frame i vs keyframe j (keyframe features cached as in monst3r_utils.py:262-269).
+        Returns dict X [2,H,W,3] (ii, ji), C [2,H,W], D16 f16 [2,H,W,24], D f32, Q [2,H,W],
+        feat_i (to cache when the frame becomes a keyframe)."""
+        a = self.a
+        H, W = img_i.shape[-2:]
+        gh, gw = H // a.patch, W // a.patch
+        if feat_j is None:
+            feat_j, _ = self.encode(img_j)
+            feat_j = feat_j.clone()
+        feat_i, pos = self.encode(img_i)
+        hooks = self.decode(feat_i[0], feat_j.reshape(-1, a.enc_dim), pos, gh, gw)
+        pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W)
+        return dict(X=pts[0:2], C=conf[0:2], D16=desc16, D=desc, Q=dconf, feat_i=feat_i,
+                    mast3r_X=pts[2:4], mast3r_C=conf[2:4])
+
+
+def build(device, seed_monst3r=0, seed_mast3r=1, small=False):
+    am, aM = Wt.MONST3R, Wt.MAST3R
+    if small:
+        am, aM = Wt.small(am), Wt.small(aM)
+    sdm = Wt.make_state_dict(am, seed_monst3r)
+    sdM = Wt.make_state_dict(aM, seed_mast3r)
+    return PairModel(PackedWeights(sdm, am, sdM, aM, device), device), (sdm, am, sdM, aM)
+
+
+def smoke(device):
+    """Small-width pair inference on the GPU vs the reference goldens (tests/golden)."""
+    import os
+
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    g = dict(np.load(os.path.join(root, "tests", "golden", "vit_small.npz")))
+    m, _ = build(device, small=True)
+    t = lambda k: torch.from_numpy(g[k]).to(device)  # noqa: E731
+    out = m.pair(t("img_i"), img_j=t("img_j"))
+    cos = torch.nn.functional.cosine_similarity(out["D"], t("D"), dim=-1)
+    rel_c = ((out["C"] - t("C")).abs() / t("C")).median()
+    assert float(cos.median()) > 0.995 and float(rel_c) < 0.03, (float(cos.median()), float(rel_c))
+    return float(cos.median()), float(rel_c)

@@ -1,0 +1,209 @@
+"""GPU numerics of the ViT/DPT HIP kernels (bf16 MFMA, f32 accumulate) against a plain
+PyTorch fp32 reference of the same op, and the full pair model against the fp32
+restatement (oracle/vit_ref.py, itself pinned to the reference goldens) and the goldens.
+
+Tolerances are stated per test: bf16 operands carry 8 significant bits (rel. 2^-9 per
+rounding), so single GEMMs are checked at ~1e-2 relative to the output scale and the
+36-layer network by distribution metrics."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+@pytest.fixture(scope="module")
+def ops(dev):
+    from monst3r_slam_amd.model import Ops
+    return Ops(dev)
+
+
+@pytest.mark.parametrize("M,N,K,batch", [(768, 3072, 1024, 1), (200, 96, 96, 2),
+                                         (768, 768, 3072, 4), (130, 257, 64, 1)])
+def test_gemm_bias_gelu(ops, dev, M, N, K, batch):
+    from monst3r_slam_amd import _lib
+    g = torch.Generator(device=dev).manual_seed(0)
+    A = torch.randn(batch, M, K, device=dev, generator=g).bfloat16()
+    B = (torch.randn(batch, N, K, device=dev, generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(batch, N, device=dev, generator=g)
+    C = torch.empty(batch, M, N, device=dev, dtype=torch.bfloat16)
+    ops.gemm(A, B, C, M, N, K, batch, sA=M * K, sB=N * K, sC=M * N, bias=bias, sBias=N,
+             flags=_lib.EPI_GELU)
+    ref = F.gelu(torch.bmm(A.float(), B.float().transpose(1, 2)) + bias[:, None])
+    assert _rel(C, ref) < 1e-2
+
+
+def test_gemm_residual_f32(ops, dev):
+    from monst3r_slam_amd import _lib
+    M, N, K = 768, 1024, 4096
+    g = torch.Generator(device=dev).manual_seed(1)
+    A = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    B = (torch.randn(N, K, device=dev, generator=g) / K ** 0.5).bfloat16()
+    x = torch.randn(M, N, device=dev, generator=g)
+    ref = x + A.float() @ B.float().t()
+    ops.gemm(A, B, x, M, N, K, R=x, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32)
+    assert _rel(x, ref) < 1e-3  # f32 out: only the f32-accumulation order differs
+
+
+@pytest.mark.parametrize("H,W,cin,cout,stride,relu_in,res", [
+    (24, 32, 256, 256, 1, True, True), (12, 16, 768, 768, 2, False, False),
+    (96, 128, 96, 256, 1, False, False), (7, 9, 64, 32, 1, True, False)])
+def test_conv3x3_implicit_gemm(ops, dev, H, W, cin, cout, stride, relu_in, res):
+    from monst3r_slam_amd import _lib
+    from monst3r_slam_amd.model import _conv_pack
+    g = torch.Generator(device=dev).manual_seed(2)
+    x = torch.randn(2, H, W, cin, device=dev, generator=g).bfloat16()
+    w = (torch.randn(cout, cin, 3, 3, device=dev, generator=g) / (9 * cin) ** 0.5)
+    b = torch.randn(cout, device=dev, generator=g)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    R = torch.randn(2, Ho, Wo, cout, device=dev, generator=g).bfloat16() if res else None
+    out = torch.empty(2, Ho, Wo, cout, device=dev, dtype=torch.bfloat16)
+    wp = _conv_pack(w).bfloat16().contiguous()
+    flags = (_lib.PRO_RELU if relu_in else 0) | (_lib.EPI_RES_BF16 if res else 0)
+    ops.gemm(x, wp, out, Ho * Wo, cout, 9 * cin, 2, sA=H * W * cin, sB=0, sC=Ho * Wo * cout,
+             bias=b, sBias=0, R=R, sR=Ho * Wo * cout, flags=flags,
+             conv=(H, W, cin, Ho, Wo, stride))
+    xin = x.float().permute(0, 3, 1, 2)
+    if relu_in:
+        xin = F.relu(xin)
+    ref = F.conv2d(xin, w.bfloat16().float(), b, stride=stride, padding=1).permute(0, 2, 3, 1)
+    if res:
+        ref = ref + R.float()
+    assert _rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("s", [4, 2])
+def test_convtranspose_scatter(ops, dev, s):
+    from monst3r_slam_amd.model import _convt_pack
+    gh, gw, cin, cout = 24, 32, 96, 96 if s == 4 else 192
+    if s == 2:
+        cin = 192
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(1, gh * gw, cin, device=dev, generator=g).bfloat16()
+    w = torch.randn(cin, cout, s, s, device=dev, generator=g) / cin ** 0.5
+    b = torch.randn(cout, device=dev, generator=g)
+    out = torch.empty(1, gh * s, gw * s, cout, device=dev, dtype=torch.bfloat16)
+    ops.gemm(x, _convt_pack(w).bfloat16().contiguous(), out, gh * gw, s * s * cout, cin,
+             bias=b, convt=(s, cout, gw))
+    xin = x.float().reshape(1, gh, gw, cin).permute(0, 3, 1, 2)
+    ref = F.conv_transpose2d(xin, w.bfloat16().float(), b, stride=s).permute(0, 2, 3, 1)
+    assert _rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("S,heads,batch", [(768, 16, 1), (196, 12, 4), (12, 4, 2)])
+def test_attention(ops, dev, S, heads, batch):
+    g = torch.Generator(device=dev).manual_seed(4)
+    C = heads * 64
+    qkv = torch.randn(batch, S, 3 * C, device=dev, generator=g).bfloat16()
+    o = torch.empty(batch, S, C, device=dev, dtype=torch.bfloat16)
+    ops.attn(qkv, 3 * C, S * 3 * C, qkv[:, :, C:], qkv[:, :, 2 * C:], 3 * C, S * 3 * C, o, C, S * C,
+             batch, heads, S, S)
+    q, k, v = qkv.float().reshape(batch, S, 3, heads, 64).permute(2, 0, 3, 1, 4)
+    ref = torch.softmax(q @ k.transpose(-1, -2) / 8.0, -1) @ v
+    ref = ref.transpose(1, 2).reshape(batch, S, C)
+    assert _rel(o, ref) < 2e-2
+
+
+def test_cross_attention_lengths(ops, dev):
+    g = torch.Generator(device=dev).manual_seed(5)
+    Sq, Sk, heads = 64, 100, 3
+    q = torch.randn(2, Sq, heads * 64, device=dev, generator=g).bfloat16()
+    kv = torch.randn(2, Sk, 2 * heads * 64, device=dev, generator=g).bfloat16()
+    o = torch.empty(2, Sq, heads * 64, device=dev, dtype=torch.bfloat16)
+    D = heads * 64
+    ops.attn(q, D, Sq * D, kv, kv[:, :, D:], 2 * D, Sk * 2 * D, o, D, Sq * D, 2, heads, Sq, Sk)
+    qq = q.float().reshape(2, Sq, heads, 64).transpose(1, 2)
+    kk, vv = kv.float().reshape(2, Sk, 2, heads, 64).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(qq @ kk.transpose(-1, -2) / 8.0, -1) @ vv).transpose(1, 2).reshape(2, Sq, D)
+    assert _rel(o, ref) < 2e-2
+
+
+def test_rope_matches_reference_formula(ops, dev):
+    from oracle import vit_ref as V
+    g = torch.Generator(device=dev).manual_seed(6)
+    B, S, heads = 2, 24 * 32, 4
+    t = torch.randn(B, S, heads * 64, device=dev, generator=g).bfloat16()
+    pos = V.positions(B, 24, 32, dev).contiguous()
+    ref = V.rope2d(t.float().reshape(B, S, heads, 64).transpose(1, 2), pos, 100.0)
+    ref = ref.transpose(1, 2).reshape(B, S, heads * 64)
+    ops.rope(t, heads * 64, S * heads * 64, pos, S * 2, B, S, heads, 100.0)
+    assert _rel(t, ref) < 1e-2
+
+
+def test_layernorm_and_swap(ops, dev):
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn(4, 768, 768, device=dev, generator=g) * 3 + 1
+    gam = torch.randn(4, 768, device=dev, generator=g)
+    bet = torch.randn(4, 768, device=dev, generator=g)
+    y = torch.empty(4, 768, 768, device=dev, dtype=torch.bfloat16)
+    ops.ln(x, gam, bet, y, 768, 768, 4, 768 * 768, 768 * 768, 768, xor=1)
+    ref = torch.stack([F.layer_norm(x[b ^ 1], (768,), gam[b], bet[b], 1e-6) for b in range(4)])
+    assert _rel(y, ref) < 1e-2
+
+
+def test_upsample_align_corners_crop_add(ops, dev):
+    g = torch.Generator(device=dev).manual_seed(8)
+    x = torch.randn(2, 6, 8, 16, device=dev, generator=g).bfloat16()
+    add = torch.randn(2, 11, 15, 16, device=dev, generator=g).bfloat16()
+    out = torch.empty(2, 11, 15, 16, device=dev, dtype=torch.bfloat16)
+    ops.up2(x, out, 2, 6, 8, 16, 11, 15, add=add)
+    ref = F.interpolate(x.float().permute(0, 3, 1, 2), scale_factor=2, mode="bilinear",
+                        align_corners=True).permute(0, 2, 3, 1)[:, :11, :15] + add.float()
+    assert _rel(out, ref) < 1e-2
+
+
+# ------------------------------------------------------------------------------------
+# model level
+# ------------------------------------------------------------------------------------
+def _cos(a, b):
+    return F.cosine_similarity(a.float(), b.float(), dim=-1)
+
+
+def _compare_pair(out, X, C, D, Q, tag):
+    rel_X = ((out["X"] - X).norm(dim=-1) / X.norm(dim=-1).clamp_min(1e-6))
+    rel_C = ((out["C"] - C).abs() / C.abs())
+    cos_D = _cos(out["D"], D)
+    rel_Q = ((out["Q"] - Q).abs() / Q.abs())
+    stats = dict(X_med=float(rel_X.median()), X_p99=float(rel_X.quantile(0.99)),
+                 C_med=float(rel_C.median()), D_cos_min=float(cos_D.min()),
+                 D_cos_med=float(cos_D.median()), Q_med=float(rel_Q.median()))
+    print(tag, stats)
+    # bf16 ViT vs fp32 reference (TF32 in the reference): stated tolerances
+    assert stats["X_med"] < 0.03 and stats["X_p99"] < 0.15, stats
+    assert stats["C_med"] < 0.03, stats
+    assert stats["D_cos_med"] > 0.995 and stats["D_cos_min"] > 0.9, stats
+    assert stats["Q_med"] < 0.05, stats
+    # f16 descriptors are exactly .half() of the f32 unit descriptors
+    assert torch.equal(out["D16"], out["D"].half())
+
+
+def test_small_model_vs_reference_goldens(dev):
+    from monst3r_slam_amd import model as Mdl
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "vit_small.npz")))
+    m, _ = Mdl.build(dev, small=True)
+    t = lambda k: torch.from_numpy(g[k]).to(dev)  # noqa: E731
+    out = m.pair(t("img_i"), img_j=t("img_j"))
+    _compare_pair(out, t("X"), t("C"), t("D"), t("Q"), "small-vs-golden")
+
+
+def test_full_model_vs_fp32_restatement(dev):
+    from monst3r_slam_amd import model as Mdl
+    from oracle import vit_ref as V
+    m, (sdm, am, sdM, aM) = Mdl.build(dev)
+    gen = torch.Generator(device=dev).manual_seed(2)
+    img_i = torch.rand(1, 3, 384, 512, device=dev, generator=gen) * 2 - 1
+    img_j = torch.rand(1, 3, 384, 512, device=dev, generator=gen) * 2 - 1
+    out = m.pair(img_i, img_j=img_j)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    sdm = {k: v.to(dev) for k, v in sdm.items()}
+    sdM = {k: v.to(dev) for k, v in sdM.items()}
+    X, C, D, Q, _, _ = V.asymmetric_inference(sdm, am, sdM, aM, img_i, img_j)
+    _compare_pair(out, X, C, D, Q, "full-vs-fp32")
