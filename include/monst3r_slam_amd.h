@@ -189,9 +189,13 @@ typedef struct {
   int32_t mode;                            /* 0: GEMM; 1: implicit 3x3 conv, pad 1  */
   int32_t Hin, Win, Cin, Hout, Wout, stride; /* conv geometry (mode 1); K = 9*Cin   */
   int32_t ct_s, ct_cout, ct_gw;            /* CONVT: kernel=stride=s, Cout, grid w  */
+  void* workspace; int64_t workspace_bytes; /* optional f32 split-K scratch (device) */
+  int32_t split_k;                         /* 0 = auto (uses workspace if it pays)  */
 } m3s_gemm_desc;
 
-/* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 32 == 0; conv: Cin % 32 == 0. */
+/* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 32 == 0; conv: Cin % 32 == 0.
+ * With a workspace, GEMMs whose tile grid cannot fill the chip (M = 768 tokens) split K
+ * over workgroups into f32 partials; a reduce kernel then applies the epilogue. */
 int m3s_vit_gemm(const m3s_gemm_desc* desc, void* stream);
 
 /* LayerNorm over the last dim (eps), x f32/bf16 [rows][dim] → y bf16 or f32

@@ -67,7 +67,8 @@ class GemmDesc(ctypes.Structure):
                 ("batch", ctypes.c_int32), ("flags", ctypes.c_int32), ("mode", ctypes.c_int32),
                 ("Hin", ctypes.c_int32), ("Win", ctypes.c_int32), ("Cin", ctypes.c_int32),
                 ("Hout", ctypes.c_int32), ("Wout", ctypes.c_int32), ("stride", ctypes.c_int32),
-                ("ct_s", ctypes.c_int32), ("ct_cout", ctypes.c_int32), ("ct_gw", ctypes.c_int32)]
+                ("ct_s", ctypes.c_int32), ("ct_cout", ctypes.c_int32), ("ct_gw", ctypes.c_int32),
+                ("workspace", _P), ("workspace_bytes", _I64), ("split_k", ctypes.c_int32)]
 
 
 EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT = (

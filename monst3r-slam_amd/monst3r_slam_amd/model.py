@@ -44,6 +44,8 @@ class Ops:
         self.lib = _lib.load()
         self.dev = dev
         self.probe = None  # list → (start_event, end_event, flops) per GEMM (bench roofline)
+        # f32 split-K scratch (the M = 768 GEMMs split K when their grid cannot fill 256 CUs)
+        self.ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
 
     def _s(self):
         return _lib.stream(self.dev)
@@ -57,6 +59,7 @@ class Ops:
         d.bias, d.strideBias = _p(bias), sBias
         d.R, d.ldr, d.strideR = _p(R), ldr if ldr is not None else N, sR
         d.M, d.N, d.K, d.batch, d.flags = M, N, K, batch, flags
+        d.workspace, d.workspace_bytes, d.split_k = _p(self.ws), self.ws.numel(), 0
         if bias is not None:
             d.flags |= _lib.EPI_BIAS
         if conv is not None:
