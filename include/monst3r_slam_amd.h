@@ -175,7 +175,8 @@ enum {
   M3S_EPI_RES_BF16 = 16,  /* + R[m][n] (bf16 residual)                         */
   M3S_EPI_OUT_F32 = 32,   /* store f32 (default bf16)                          */
   M3S_PRO_RELU = 64,      /* ReLU applied to A while loading (conv prologue)   */
-  M3S_EPI_CONVT = 128     /* scatter rows/cols as ConvTranspose(k=s, stride=s) */
+  M3S_EPI_CONVT = 128,    /* scatter rows/cols as ConvTranspose(k=s, stride=s) */
+  M3S_EPI_ROPE = 256      /* 2D RoPE on columns < rope_cols (head dim 64), after bias */
 };
 
 typedef struct {
@@ -191,12 +192,22 @@ typedef struct {
   int32_t ct_s, ct_cout, ct_gw;            /* CONVT: kernel=stride=s, Cout, grid w  */
   void* workspace; int64_t workspace_bytes; /* optional f32 split-K scratch (device) */
   int32_t split_k;                         /* 0 = auto (uses workspace if it pays)  */
+  const float* rope_table;                 /* ROPE: m3s_vit_rope_table output        */
+  int32_t rope_cols, rope_tokens;          /* ROPE: rotated columns; row m → token m % rope_tokens */
 } m3s_gemm_desc;
 
-/* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 32 == 0; conv: Cin % 32 == 0.
+/* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 8 == 0; conv: Cin % 32 == 0.
+ * A, B 16-B aligned, lda/ldb/batch strides % 8 == 0; per-batch operand spans < 2 GiB.
  * With a workspace, GEMMs whose tile grid cannot fill the chip (M = 768 tokens) split K
- * over workgroups into f32 partials; a reduce kernel then applies the epilogue. */
+ * over workgroups into f32 partials; a reduce kernel then applies the epilogue.
+ * ROPE (croco/pos_embed.py RoPE2D as applied in croco/blocks.py:64-66, 110-112) rotates
+ * the q / k columns in the epilogue, replacing a separate pass over q and k. */
 int m3s_vit_gemm(const m3s_gemm_desc* desc, void* stream);
+
+/* RoPE2D cos/sin table for the GEMM epilogue: pos int64 [tokens][2] (y, x) →
+ * table f32 [tokens][2][2][16] = {cos, sin}(pos[t][h] · base^(−i/16)), i < 16. */
+int m3s_vit_rope_table(const int64_t* d_pos, int64_t tokens, float base, float* d_table,
+                       void* stream);
 
 /* LayerNorm over the last dim (eps), x f32/bf16 [rows][dim] → y bf16 or f32
  * (x_is_bf16 / y_is_f32 flags); batch strides in elements.  dim ≤ 4096, dim % 4 == 0.

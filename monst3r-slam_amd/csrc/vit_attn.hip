@@ -3,20 +3,20 @@
 // rope2d_kernel: in-place RoPE100 on a bf16 q or k view (croco curope kernels.cu:17-82,
 //   pos_embed.py:106-158): head dim 64 = [y half | x half]; within a half, pairs
 //   (i, i+16), angle = pos * base^(-i/16); f32 math, one bf16 rounding.
-// attn_kernel: flash-style softmax(q k^T / 8) v, one wave per 32 query rows.
+// attn_kernel: flash-style softmax(q k^T / 8) v.  A block = 4 waves x 32 query rows of
+//   one (batch, head); 64-key K/V tiles are shared by the 4 waves through an LDS ring
+//   filled by LDS-DMA buffer loads (3 stages, counted vmcnt + raw barrier, as in
+//   vit_gemm.hip; keys beyond sk read as zeros and are masked).
 //   S^T = K Q^T with v_mfma_f32_32x32x16_bf16 (keys on the accumulator rows, queries on
 //   the lanes), so the online-softmax max / sum per query are lane-local (+ one xor-32
 //   exchange).  P^T stays in registers as the B operand of O^T = V^T P^T; V^T fragments
-//   come from an LDS image of the V tile via ds_read_b64_tr_b16 (hardware transpose).
-//   Keys beyond sk are masked (any token count, e.g. 14x14 at 224^2).
+//   come from the V tile via ds_read_b64_tr_b16 (hardware transpose).
 #include "vit_common.h"
 
 namespace {
 
 constexpr int HD = 64;
 constexpr int QT = 32;   // query rows per wave
-constexpr int KT = 32;   // keys per tile
-constexpr int VS = 72;   // LDS row stride (bf16) of the V tile: 144 B, 16-B aligned rows
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
@@ -59,30 +59,117 @@ __global__ __launch_bounds__(256) void rope2d_kernel(bf16_t* __restrict__ t, int
     reinterpret_cast<uint4*>(row)[c] = reinterpret_cast<const uint4*>(outv)[c];
 }
 
+// cos/sin table for the GEMM-epilogue RoPE: same f32 angle math as rope2d_kernel.
+__global__ __launch_bounds__(256) void rope_table_kernel(const int64_t* __restrict__ pos,
+                                                         int64_t tokens, float base,
+                                                         float* __restrict__ tab) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (token, half, i)
+  if (idx >= tokens * 32) return;
+  const int i = (int)(idx & 15);
+  const int half = (int)((idx >> 4) & 1);
+  const int64_t t = idx >> 5;
+  const float p = (float)pos[t * 2 + half];
+  const float inv_freq = 1.0f / powf(base, (float)i / 16.0f);
+  const float f = p * inv_freq;
+  float* row = tab + (t * 2 + half) * 32;
+  row[i] = cosf(f);
+  row[16 + i] = sinf(f);
+}
+
 __device__ __forceinline__ bf16x8 load8(const bf16_t* p) {
   return *reinterpret_cast<const bf16x8*>(p);
 }
 
-__global__ __launch_bounds__(64) void attn_kernel(
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(lds), 16,
+                                           voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void block_sync_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS images of one K/V tile (64 keys x 64 d, 128-B rows, lane-linear as the DMA writes
+// them).  16-B chunk swizzles: K (read by ds_read_b128 down 32 rows) chunk ^ ((r>>1)&7);
+// V (read by ds_read_b64_tr_b16, 4 rows x 64 B per half-wave) chunk ^ 4*((r>>1)&1).
+__device__ __forceinline__ s16x4 tr_read(const char* p) {
+  s16x4 v;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+
+__device__ __forceinline__ int k_swz(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ int v_swz(int r) { return ((r >> 1) & 1) * 4; }
+
+constexpr int AW = 4;                      // waves per block, QT query rows each
+constexpr int AKT = 64;                    // keys per tile
+constexpr int ASTAGES = 3;                 // DMA ring depth
+constexpr int TILE_BYTES = AKT * HD * 2;   // 8 KiB
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+constexpr int ACH = TILE_BYTES / 16 / (AW * 64);  // DMA chunks per thread per operand (2)
+constexpr uint32_t OOB = 0x80000000u;
+
+__global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, bf16_t* __restrict__ o,
     int64_t ldo, int64_t so_b, int Sq, int Sk, float c_log2) {
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[KT][VS];
-  const int lane = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) char lds[ASTAGES * STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
-  const int q0 = blockIdx.x * QT;
+  const int q0 = blockIdx.x * (AW * QT) + wid * QT;
   const int h = blockIdx.y;
   const int64_t b = blockIdx.z;
   const bf16_t* Q = q + b * sq_b + h * HD;
-  const bf16_t* K = k + b * skv_b + h * HD;
-  const bf16_t* V = v + b * skv_b + h * HD;
 
+  // Q fragments (B operand of S^T = K Q^T): query q0 + r, d = 16 ks + 8 hh .. +7
   const int qrow = q0 + r;
   bf16x8 qf[4];
   const bf16x8 zero8 = {};
 #pragma unroll
   for (int ks = 0; ks < 4; ks++)
     qf[ks] = qrow < Sq ? load8(Q + (int64_t)qrow * ldq + ks * 16 + 8 * hh) : zero8;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q ready before the DMA queue fills
+  // launder: the compiler would otherwise wait vmcnt(0) (draining the DMA ring) at every
+  // use of these ordinary-load results inside the loop
+#pragma unroll
+  for (int ks = 0; ks < 4; ks++) asm volatile("" : "+v"(qf[ks]));
+
+  const __amdgpu_buffer_rsrc_t rK = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(k + b * skv_b + h * HD), (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rV = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(v + b * skv_b + h * HD), (short)0, 0x7ffffff0, 0x00020000);
+  // DMA chunk c = i*256 + tid → tile row c / 8, slot c % 8
+  int k_row[ACH];
+  uint32_t k_off[ACH], v_off[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; i++) {
+    const int c = i * AW * 64 + tid;
+    const int row = c >> 3, slot = c & 7;
+    k_row[i] = row;
+    k_off[i] = (uint32_t)(((int64_t)row * ldkv + (slot ^ k_swz(row)) * 8) * 2);
+    v_off[i] = (uint32_t)(((int64_t)row * ldkv + (slot ^ v_swz(row)) * 8) * 2);
+  }
+  const int nkt = (Sk + AKT - 1) / AKT;
+  auto issue = [&](int kt, int stage) {
+    char* sb = lds + stage * STAGE_BYTES;
+    const uint32_t t0 = (uint32_t)((int64_t)kt * AKT * ldkv * 2);
+#pragma unroll
+    for (int i = 0; i < ACH; i++) {
+      const bool ok = kt * AKT + k_row[i] < Sk;
+      glds16(rK, sb + (i * AW * 64 + wid * 64) * 16, ok ? t0 + k_off[i] : OOB);
+      glds16(rV, sb + TILE_BYTES + (i * AW * 64 + wid * 64) * 16, ok ? t0 + v_off[i] : OOB);
+    }
+  };
 
   f32x16 oacc[2];
 #pragma unroll
@@ -90,50 +177,62 @@ __global__ __launch_bounds__(64) void attn_kernel(
 #pragma unroll
     for (int i = 0; i < 16; i++) oacc[d][i] = 0.f;
   float m = -INFINITY, l = 0.f;
-
-  const int nkt = (Sk + KT - 1) / KT;
-  // V staging: lane -> key row (lane >> 1), 32-wide d half (lane & 1)
-  const int vr = lane >> 1, vh = (lane & 1) * 32;
-  // tr-read addressing inside a 16-lane group
+  // tr-read lane roles inside a 16-lane group
   const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gsel = (lane >> 4) & 1;
 
+#pragma unroll
+  for (int st = 0; st < ASTAGES - 1; st++)
+    if (st < nkt) issue(st, st);
+
   for (int kt = 0; kt < nkt; kt++) {
-    const int key = kt * KT + r;
-    const bool kvalid = key < Sk;
-    bf16x8 kf[4];
+    if (kt + 1 < nkt) vm_wait<2 * ACH>();
+    else vm_wait<0>();
+    block_sync_lds();
+    if (kt + ASTAGES - 1 < nkt) issue(kt + ASTAGES - 1, (kt + ASTAGES - 1) % ASTAGES);
+    const char* sK = lds + (kt % ASTAGES) * STAGE_BYTES;
+    const char* sV = sK + TILE_BYTES;
+
+    // S^T (keys x queries), two 32-key halves
+    f32x16 s[2];
 #pragma unroll
-    for (int ks = 0; ks < 4; ks++)
-      kf[ks] = kvalid ? load8(K + (int64_t)key * ldkv + ks * 16 + 8 * hh) : zero8;
-    // stage V tile (previous tile's reads are complete after the barrier below)
-    const int vkey = kt * KT + vr;
-    uint4 vv[4];
+    for (int hs = 0; hs < 2; hs++) {
 #pragma unroll
-    for (int c = 0; c < 4; c++)
-      vv[c] = vkey < Sk ? *reinterpret_cast<const uint4*>(V + (int64_t)vkey * ldkv + vh + 8 * c)
-                        : make_uint4(0, 0, 0, 0);
-    f32x16 s;
+      for (int i = 0; i < 16; i++) s[hs][i] = 0.f;
+      const int row = hs * 32 + r;
 #pragma unroll
-    for (int i = 0; i < 16; i++) s[i] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], qf[ks], s, 0, 0, 0);
-    // online softmax over this tile's keys (rows of s)
+      for (int ks = 0; ks < 4; ks++) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(
+            sK + row * 128 + (((2 * ks + hh) ^ k_swz(row)) * 16));
+        s[hs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[hs], 0, 0, 0);
+      }
+    }
+    // online softmax over the tile's keys (accumulator rows), per query (lane)
+    const bool tail = (kt + 1) * AKT > Sk;
     float tmax = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int kr = kt * KT + (i & 3) + 8 * (i >> 2) + 4 * hh;
-      if (kr >= Sk) s[i] = -INFINITY;
-      tmax = fmaxf(tmax, s[i]);
-    }
+    for (int hs = 0; hs < 2; hs++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        if (tail) {
+          const int key = kt * AKT + hs * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (key >= Sk) s[hs][i] = -INFINITY;
+        }
+        tmax = fmaxf(tmax, s[hs][i]);
+      }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_new = fmaxf(m, tmax);
-    const float alpha = (m == -INFINITY) ? 0.f : exp2f((m - m_new) * c_log2);
+    const float alpha = __builtin_amdgcn_exp2f((m - m_new) * c_log2);  // m = -inf → 0
+    const float mc = m_new * c_log2;
     float rs = 0.f;
-    float p[16];
+    bf16x8 pf[4];  // P^T B operands, 16-key chunks (2 hs + ss)
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      p[i] = (s[i] == -INFINITY) ? 0.f : exp2f((s[i] - m_new) * c_log2);
-      rs += p[i];
-    }
+    for (int hs = 0; hs < 2; hs++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const float p = __builtin_amdgcn_exp2f(s[hs][i] * c_log2 - mc);  // -inf → 0
+        rs += p;
+        pf[2 * hs + (i >> 3)][i & 7] = f2bf(p);
+      }
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
     m = m_new;
@@ -141,29 +240,33 @@ __global__ __launch_bounds__(64) void attn_kernel(
     for (int d = 0; d < 2; d++)
 #pragma unroll
       for (int i = 0; i < 16; i++) oacc[d][i] *= alpha;
-    bf16x8 pf[2];
-#pragma unroll
-    for (int ss = 0; ss < 2; ss++)
-#pragma unroll
-      for (int j = 0; j < 8; j++) pf[ss][j] = f2bf(p[8 * ss + j]);
-
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 4; c++) *reinterpret_cast<uint4*>(&Vs[vr][vh + 8 * c]) = vv[c];
-    __syncthreads();
+    // O^T += V^T P^T; chunk (hs, ss) B rows are keys 32hs + 16ss + {0-3, 8-11} + 4hh.
+    // The transposed reads are inline asm: as an intrinsic the compiler cannot tell they
+    // do not alias the DMA ring and would drain it (vmcnt(0)) before each of them.
+    s16x4 vt[2][4][2];
 #pragma unroll
     for (int d = 0; d < 2; d++) {
       const int d0 = d * 32 + 16 * gsel + 4 * gp;
 #pragma unroll
-      for (int ss = 0; ss < 2; ss++) {
-        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)&Vs[16 * ss + 4 * hh + gq][d0]);
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s16x4*)&Vs[16 * ss + 8 + 4 * hh + gq][d0]);
+      for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+          const int rr = 16 * c + 8 * x + 4 * hh + gq;
+          vt[d][c][x] = tr_read(sV + rr * 128 + (((d0 >> 3) ^ v_swz(rr)) * 16) + (d0 & 7) * 2);
+        }
+    }
+    // the waits name the read results as operands, so no MFMA can be hoisted above them
+#define M3S_VT(d) "+v"(vt[d][0][0]), "+v"(vt[d][0][1]), "+v"(vt[d][1][0]), "+v"(vt[d][1][1]), \
+                  "+v"(vt[d][2][0]), "+v"(vt[d][2][1]), "+v"(vt[d][3][0]), "+v"(vt[d][3][1])
+    asm volatile("s_waitcnt lgkmcnt(8)" : M3S_VT(0)::"memory");
+#pragma unroll
+    for (int d = 0; d < 2; d++) {
+      if (d == 1) asm volatile("s_waitcnt lgkmcnt(0)" : M3S_VT(1)::"memory");
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const bf16x4 lob = __builtin_bit_cast(bf16x4, vt[d][c][0]);
+        const bf16x4 hib = __builtin_bit_cast(bf16x4, vt[d][c][1]);
         bf16x8 vf;
-        const bf16x4 lob = __builtin_bit_cast(bf16x4, lo);
-        const bf16x4 hib = __builtin_bit_cast(bf16x4, hi);
         vf[0] = lob[0];
         vf[1] = lob[1];
         vf[2] = lob[2];
@@ -172,9 +275,10 @@ __global__ __launch_bounds__(64) void attn_kernel(
         vf[5] = hib[1];
         vf[6] = hib[2];
         vf[7] = hib[3];
-        oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[ss], oacc[d], 0, 0, 0);
+        oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[c], oacc[d], 0, 0, 0);
       }
     }
+#undef M3S_VT
   }
   if (qrow >= Sq) return;
   const float inv_l = 1.0f / l;
@@ -182,9 +286,11 @@ __global__ __launch_bounds__(64) void attn_kernel(
 #pragma unroll
   for (int d = 0; d < 2; d++)
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int dd = d * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-      O[dd] = f2bf(oacc[d][i] * inv_l);
+    for (int g4 = 0; g4 < 4; g4++) {
+      bf16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; j++) w[j] = f2bf(oacc[d][4 * g4 + j] * inv_l);
+      *reinterpret_cast<bf16x4*>(O + d * 32 + 8 * g4 + 4 * hh) = w;
     }
 }
 
@@ -199,6 +305,15 @@ extern "C" int m3s_vit_rope(void* d_t, int64_t ld, int64_t stride, const int64_t
   hipLaunchKernelGGL(rope2d_kernel, dim3(m3s_div_up(total, 256)), dim3(256), 0,
                      m3s_stream(stream), reinterpret_cast<bf16_t*>(d_t), ld, stride, d_pos,
                      stride_pos, (int)S, (int)heads, base, total);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_vit_rope_table(const int64_t* d_pos, int64_t tokens, float base,
+                                  float* d_table, void* stream) {
+  if (!d_pos || !d_table || tokens <= 0) return M3S_ERR_INVALID_ARG;
+  hipLaunchKernelGGL(rope_table_kernel, dim3(m3s_div_up(tokens * 32, 256)), dim3(256), 0,
+                     m3s_stream(stream), d_pos, tokens, base, d_table);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }
@@ -220,9 +335,11 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   (void)d_kpos;
   (void)stride_pos;
   (void)rope_base;
+  if (sk * ld_kv * 2 >= 0x7ffffff0) return M3S_ERR_TOO_LARGE;  // 31-bit buffer offsets
+  if (((uintptr_t)d_o) % 8 || ld_o % 4 || stride_o % 4) return M3S_ERR_INVALID_ARG;
   const float c_log2 = 0.125f * 1.4426950408889634f;  // head_dim^-0.5 * log2(e)
-  dim3 grid(m3s_div_up(sq, QT), (unsigned)heads, (unsigned)batch);
-  hipLaunchKernelGGL(attn_kernel, grid, dim3(64), 0, m3s_stream(stream),
+  dim3 grid(m3s_div_up(sq, AW * QT), (unsigned)heads, (unsigned)batch);
+  hipLaunchKernelGGL(attn_kernel, grid, dim3(AW * 64), 0, m3s_stream(stream),
                      reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,
                      reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v),
                      ld_kv, stride_kv, reinterpret_cast<bf16_t*>(d_o), ld_o, stride_o, (int)sq,

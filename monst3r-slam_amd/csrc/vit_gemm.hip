@@ -2,26 +2,38 @@
 //
 //   C[g] = epi(A[g] · B[g]^T)       A [M][K] (or implicit 3x3-conv rows of an NHWC image),
 //                                   B [N][K] weights (K contiguous: torch Linear layout)
-// Tiles (templated): BM x BN x BK with 256 threads = 4 waves laid out WM x WN; each wave
-// owns (BM/WM) x (BN/WN) = a grid of 32x32 v_mfma_f32_32x32x16_bf16 accumulators.
-// LDS: double buffer, rows padded by 16 B (conflict-free ds_read_b128 of the 32x32x16
-// fragments: consecutive rows land 4 banks apart).
-// Pipeline: global→register→LDS with prefetch distance 2 (two register sets): the loads
-// of K-tile t+2 are issued before tile t's MFMAs and written to LDS only after tile t+1's
-// MFMAs, so each load has two MFMA phases to land (the M = 768 transformer GEMMs run one
-// workgroup per CU and are latency-bound otherwise).  One barrier per K-tile.
-// Implicit conv: the staged rows' output pixels are decoded once; per K-tile the tap
-// (ky, kx) and channel offset are block-uniform (Cin % BK == 0).
-// Split-K (small tile grids): grid.z = batch x splits, f32 partials to a workspace, then a
-// reduce kernel applies the epilogue (deterministic, no atomics).
-// Epilogue: bias, GELU(erf), ReLU, f32/bf16 residual, f32/bf16 store, ConvTranspose(k=s)
-// scatter.  XCD-aware bijective tile order (cdna_hip_programming.md T1).
-#include <type_traits>
+//
+// Main loop (cdna_hip_programming.md §5 "Pipelining across barriers"):
+//  * operands go HBM → LDS with 16-B LDS-DMA buffer loads (buffer_load_dwordx4 … lds), a
+//    ring of STAGES K-tiles in one __shared__ array; tile t+STAGES-1 is issued right after
+//    the barrier that retires tile t, so STAGES-1 tiles are in flight during each MFMA
+//    phase; counted `s_waitcnt vmcnt(N)` + raw s_barrier (never __syncthreads, whose fence
+//    would drain the DMA queue).
+//  * out-of-range rows, K tails and conv zero padding are buffer out-of-bounds reads
+//    (voffset ≥ num_records → the hardware writes zeros): no branches around loads.
+//  * LDS image is lane-linear per wave instruction (what the DMA writes); bank conflicts of
+//    the ds_read_b128 fragment reads are removed by XOR-swizzling the 16-B chunk index with
+//    the row (applied to the per-lane GLOBAL address at load time and to the read address).
+//  * 4 waves, each a grid of 32x32 v_mfma_f32_32x32x16_bf16 accumulators.
+// Epilogue: accumulators → LDS f32 tile → row-contiguous 8-column vectors per thread:
+//   bias, GELU(erf), 2D RoPE (croco RoPE2D, via a per-token cos/sin table), f32/bf16
+//   residual, ReLU, f32/bf16 store, ConvTranspose(k=s) scatter — 16-B loads/stores.
+// Split-K (tile grids that cannot fill 256 CUs): grid.z = batch x splits, f32 partial tiles
+//   to a workspace, then a reduce kernel applies the same epilogue (fixed order, no atomics).
+// Implicit conv (MODE 1, MODE 2 = ReLU on A): per K-tile the tap (ky, kx) and channel
+//   offset are block-uniform (Cin % BK == 0); ReLU is applied to the A fragments in
+//   registers (v_pk_max_i16 on the bf16 bits).
+// XCD-aware bijective tile order (cdna_hip_programming.md T1).
+#include <stdlib.h>
 #include "vit_common.h"
 
 namespace {
 
 constexpr int NT = 256;
+constexpr uint32_t OOB = 0x80000000u;      // any voffset ≥ num_records reads as zero
+constexpr int32_t NUM_RECORDS = 0x7ffffff0;
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 struct Args {
   const bf16_t* A;
@@ -39,22 +51,15 @@ struct Args {
   int ct_s, ct_cout, ct_gw;
   int tiles_m, tiles_n;
   int splits;
-  float* ws;  // split-K partials [batch*splits][M][N]
+  int vec;                 // 8-wide vector epilogue allowed (alignment / N % 8 checked on host)
+  float* ws;               // split-K partials [batch*splits][M][N]
+  const float* rope_tab;   // [tokens][2 (y,x)][2 (cos,sin)][16]
+  int rope_cols, rope_tokens;
 };
 
-__device__ __forceinline__ uint4 relu8(uint4 v) {
-  uint32_t* w = reinterpret_cast<uint32_t*>(&v);
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    uint32_t x = w[i];
-    uint32_t lo = (x & 0x8000u) ? 0u : (x & 0xffffu);
-    uint32_t hi = (x & 0x80000000u) ? 0u : (x & 0xffff0000u);
-    w[i] = lo | hi;
-  }
-  return v;
-}
-
-// Shared epilogue for one element (m, n) of batch g.
+// ---------------------------------------------------------------------------------------
+// epilogue
+// ---------------------------------------------------------------------------------------
 struct Epi {
   const float* bias;
   const char* R;
@@ -62,6 +67,8 @@ struct Epi {
   int flags;
   int64_t ldc, ldr;
   int ct_s, ct_cout, ct_gw;
+  const float* rope_tab;
+  int rope_cols, rope_tokens;
 };
 
 __device__ __forceinline__ Epi make_epi(const Args& a, int g) {
@@ -77,27 +84,108 @@ __device__ __forceinline__ Epi make_epi(const Args& a, int g) {
   e.ct_s = a.ct_s;
   e.ct_cout = a.ct_cout;
   e.ct_gw = a.ct_gw;
+  e.rope_tab = a.rope_tab;
+  e.rope_cols = a.rope_cols;
+  e.rope_tokens = a.rope_tokens;
   return e;
 }
 
-__device__ __forceinline__ void epi_store(const Epi& e, float v, int m, int n) {
-  int co = n, ca = 0, cb = 0;
-  const bool convt = e.flags & M3S_EPI_CONVT;
-  if (convt) {
+// output element offset of (m, n) (ConvTranspose scatter: n = (a*s + b)*Cout + co)
+__device__ __forceinline__ int64_t out_offset(const Epi& e, int m, int n, int& co) {
+  if (e.flags & M3S_EPI_CONVT) {
     co = n % e.ct_cout;
     const int ab = n / e.ct_cout;
-    ca = ab / e.ct_s;
-    cb = ab - ca * e.ct_s;
-  }
-  if (e.bias) v += e.bias[co];
-  if (e.flags & M3S_EPI_GELU) v = gelu_erf(v);
-  int64_t off;
-  if (convt) {
+    const int ca = ab / e.ct_s, cb = ab - ca * e.ct_s;
     const int ti = m / e.ct_gw, tj = m - ti * e.ct_gw;
     const int64_t oy = (int64_t)ti * e.ct_s + ca, ox = (int64_t)tj * e.ct_s + cb;
-    off = (oy * ((int64_t)e.ct_gw * e.ct_s) + ox) * e.ct_cout + co;
+    return (oy * ((int64_t)e.ct_gw * e.ct_s) + ox) * e.ct_cout + co;
+  }
+  co = n;
+  return (int64_t)m * e.ldc + n;
+}
+
+// RoPE2D on an 8-column group [n, n+8) of one head (head dim 64 = [y | x] halves; in a
+// half, pairs (i, i+16)): v are the group's values, p the partner group's (n ^ 16).
+__device__ __forceinline__ void rope8(const Epi& e, float* v, const float* p, int m, int n) {
+  const int s = m % e.rope_tokens;
+  const int half = (n >> 5) & 1;
+  const int i0 = n & 15;
+  const float* t = e.rope_tab + ((int64_t)s * 2 + half) * 32;
+  const float4 c0 = *reinterpret_cast<const float4*>(t + i0);
+  const float4 c1 = *reinterpret_cast<const float4*>(t + i0 + 4);
+  const float4 s0 = *reinterpret_cast<const float4*>(t + 16 + i0);
+  const float4 s1 = *reinterpret_cast<const float4*>(t + 16 + i0 + 4);
+  const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float sg = (n & 16) ? 1.f : -1.f;  // lower: u c - v s; upper: v c + u s
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = v[i] * cs[i] + sg * p[i] * sn[i];
+}
+
+// 8 consecutive columns [n, n+8) of row m; p = partner columns (n ^ 16) for RoPE or null.
+__device__ __forceinline__ void epi_vec8(const Epi& e, float* v, float* p, int m, int n) {
+  int co;
+  const int64_t off = out_offset(e, m, n, co);
+  if (e.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(e.bias + co);
+    const float4 b1 = *reinterpret_cast<const float4*>(e.bias + co + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+    v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  if (e.flags & M3S_EPI_GELU) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = gelu_erf(v[i]);
+  }
+  if ((e.flags & M3S_EPI_ROPE) && n < e.rope_cols) {
+    const int pn = n ^ 16;
+    if (e.bias) {
+      const float4 b0 = *reinterpret_cast<const float4*>(e.bias + pn);
+      const float4 b1 = *reinterpret_cast<const float4*>(e.bias + pn + 4);
+      p[0] += b0.x; p[1] += b0.y; p[2] += b0.z; p[3] += b0.w;
+      p[4] += b1.x; p[5] += b1.y; p[6] += b1.z; p[7] += b1.w;
+    }
+    rope8(e, v, p, m, n);
+  }
+  if (e.flags & M3S_EPI_RES_F32) {
+    const float* r = reinterpret_cast<const float*>(e.R) + (int64_t)m * e.ldr + n;
+    const float4 r0 = *reinterpret_cast<const float4*>(r);
+    const float4 r1 = *reinterpret_cast<const float4*>(r + 4);
+    v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+    v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+  }
+  if (e.flags & M3S_EPI_RES_BF16) {
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>(
+        reinterpret_cast<const bf16_t*>(e.R) + (int64_t)m * e.ldr + n);
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] += bf2f(r[i]);
+  }
+  if (e.flags & M3S_EPI_RELU) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = fmaxf(v[i], 0.f);
+  }
+  if (e.flags & M3S_EPI_OUT_F32) {
+    float* c = reinterpret_cast<float*>(e.C) + off;
+    *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
   } else {
-    off = (int64_t)m * e.ldc + n;
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; i++) o[i] = f2bf(v[i]);
+    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16_t*>(e.C) + off) = o;
+  }
+}
+
+// one element (tails / unaligned shapes); p = partner value (RoPE) incl. its bias
+__device__ __forceinline__ void epi_one(const Epi& e, float v, float p, int m, int n) {
+  int co;
+  const int64_t off = out_offset(e, m, n, co);
+  if (e.bias) v += e.bias[co];
+  if (e.flags & M3S_EPI_GELU) v = gelu_erf(v);
+  if ((e.flags & M3S_EPI_ROPE) && n < e.rope_cols) {
+    if (e.bias) p += e.bias[n ^ 16];
+    const int s = m % e.rope_tokens, half = (n >> 5) & 1, i = n & 15;
+    const float* t = e.rope_tab + ((int64_t)s * 2 + half) * 32;
+    v = v * t[i] + ((n & 16) ? 1.f : -1.f) * p * t[16 + i];
   }
   if (e.flags & M3S_EPI_RES_F32) v += reinterpret_cast<const float*>(e.R)[(int64_t)m * e.ldr + n];
   if (e.flags & M3S_EPI_RES_BF16)
@@ -107,17 +195,57 @@ __device__ __forceinline__ void epi_store(const Epi& e, float v, int m, int n) {
   else reinterpret_cast<bf16_t*>(e.C)[off] = f2bf(v);
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int MODE, bool SPLIT>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(Args a) {
-  constexpr int LDS = BK + 8;                 // padded row (bf16 elements)
-  constexpr int CPR = BK / 8;                 // 16-B chunks per row
-  constexpr int A_CH = BM * CPR / NT;         // A chunks per thread per K-tile
-  constexpr int B_CH = BN * CPR / NT;
+// ---------------------------------------------------------------------------------------
+// main kernel
+// ---------------------------------------------------------------------------------------
+template <int BM, int BN, int BK, int STAGES>
+struct Cfg {
+  static constexpr int CPR = BK / 8;                 // 16-B chunks per row
+  static constexpr int RPB = 256 / (BK * 2);         // rows per 256-B LDS bank row
+  static constexpr int A_CH = BM * CPR / NT;         // DMA chunks per thread per K-tile
+  static constexpr int B_CH = BN * CPR / NT;
+  static constexpr int L = A_CH + B_CH;              // vmcnt units per K-tile
+  static constexpr int A_BYTES = BM * BK * 2;
+  static constexpr int ST_BYTES = (BM + BN) * BK * 2;
+  static constexpr int CST = BN + 4;                 // epilogue f32 row stride
+  static constexpr int EPI_BYTES = BM * CST * 4;
+  static constexpr int LDS_BYTES = STAGES * ST_BYTES > EPI_BYTES ? STAGES * ST_BYTES : EPI_BYTES;
+};
+
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (__attribute__((address_space(3))) void*)(lds), 16, voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void block_sync_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ bf16x8 relu_frag(bf16x8 x) {
+  // bf16 ReLU on the bit patterns: negative values are negative int16s (−0 → +0)
+  s16x2* w = reinterpret_cast<s16x2*>(&x);
+  const s16x2 z = {0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; i++) w[i] = __builtin_elementwise_max(w[i], z);
+  return x;
+}
+
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, bool SPLIT>
+__global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
+  using C = Cfg<BM, BN, BK, STAGES>;
   constexpr int TM = BM / WM / 32;            // 32x32 accumulators per wave (M)
   constexpr int TN = BN / WN / 32;
-  static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for 256 threads");
-  __shared__ __attribute__((aligned(16))) bf16_t As[2][BM][LDS];
-  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BN][LDS];
+  static_assert(C::A_CH >= 1 && C::B_CH >= 1, "tile too small for 256 threads");
+  static_assert((C::A_CH * NT) % C::CPR == 0 && 32 % (C::RPB * C::CPR) == 0, "swizzle");
+  static_assert(C::L * (STAGES - 2) <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
 
   const int nwg = a.tiles_m * a.tiles_n;
   const int orig = blockIdx.x;
@@ -130,87 +258,78 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args a) {
   const int zz = blockIdx.z;
   const int g = SPLIT ? zz / a.splits : zz;
   const int split = SPLIT ? zz - g * a.splits : 0;
-  const bf16_t* A = a.A + (int64_t)g * a.sA;
-  const bf16_t* B = a.B + (int64_t)g * a.sB;
   const int m0 = tm * BM;
   const int n0 = tn * BN;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wid = tid >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
-  const bool relu_in = (a.flags & M3S_PRO_RELU) != 0;
 
-  int a_row[A_CH], a_kc[A_CH];
-  int64_t a_base[A_CH];
-  int a_iy[A_CH], a_ix[A_CH];
-  bool a_ok[A_CH];
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(a.A + (int64_t)g * a.sA), (short)0, NUM_RECORDS, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(a.B + (int64_t)g * a.sB), (short)0, NUM_RECORDS, 0x00020000);
+
+  // per-thread DMA chunks: chunk q = i*NT + tid lands at LDS row q / CPR, slot q % CPR and
+  // carries logical K-chunk slot ^ swz(row)
+  uint32_t a_off[C::A_CH];
+  int a_kc[C::A_CH], a_iy[C::A_CH], a_ix[C::A_CH];
 #pragma unroll
-  for (int i = 0; i < A_CH; i++) {
-    const int c = tid + i * NT;
-    a_row[i] = c / CPR;
-    a_kc[i] = (c % CPR) * 8;
-    const int m = m0 + a_row[i];
-    a_ok[i] = m < a.M;
-    a_base[i] = 0;
-    a_iy[i] = 0;
-    a_ix[i] = 0;
+  for (int i = 0; i < C::A_CH; i++) {
+    const int q = i * NT + tid;
+    const int r = q / C::CPR, p = q % C::CPR;
+    const int kc = (p ^ ((r / C::RPB) % C::CPR)) * 8;
+    const int m = m0 + r;
+    a_kc[i] = kc;
     if (MODE == 0) {
-      a_base[i] = (int64_t)(a_ok[i] ? m : 0) * a.lda;
+      a_off[i] = m < a.M ? (uint32_t)(((int64_t)m * a.lda + kc) * 2) : OOB;
+      a_iy[i] = a_ix[i] = 0;
     } else {
-      const int mm = a_ok[i] ? m : 0;
-      const int oy = mm / a.Wout, ox = mm - oy * a.Wout;
-      a_iy[i] = oy * a.stride - 1;
+      const int oy = m / a.Wout, ox = m - oy * a.Wout;
+      a_iy[i] = m < a.M ? oy * a.stride - 1 : -(1 << 20);  // OOB rows never pass the bounds test
       a_ix[i] = ox * a.stride - 1;
+      a_off[i] = 0;
     }
   }
-  int b_row[B_CH], b_kc[B_CH];
-  bool b_ok[B_CH];
+  uint32_t b_off[C::B_CH];
+  int b_kc[C::B_CH];
 #pragma unroll
-  for (int i = 0; i < B_CH; i++) {
-    const int c = tid + i * NT;
-    b_row[i] = c / CPR;
-    b_kc[i] = (c % CPR) * 8;
-    b_ok[i] = (n0 + b_row[i]) < a.N;
+  for (int i = 0; i < C::B_CH; i++) {
+    const int q = i * NT + tid;
+    const int r = q / C::CPR, p = q % C::CPR;
+    const int kc = (p ^ ((r / C::RPB) % C::CPR)) * 8;
+    const int n = n0 + r;
+    b_kc[i] = kc;
+    b_off[i] = n < a.N ? (uint32_t)(((int64_t)n * a.ldb + kc) * 2) : OOB;
   }
 
-  uint4 ra[2][A_CH], rb[2][B_CH];
-  // register-set indices must be compile-time constants (a runtime index sends the
-  // arrays to scratch): the K loop below is unrolled by two with integral_constant sets
-  auto gload = [&](auto setc, int k0) {
-    constexpr int set = decltype(setc)::value;
+  auto issue = [&](int ktile, int stage) {
+    const int k0 = ktile * BK;
+    char* sb = lds + stage * C::ST_BYTES;
     if (MODE == 0) {
 #pragma unroll
-      for (int i = 0; i < A_CH; i++)
-        ra[set][i] = a_ok[i] ? *reinterpret_cast<const uint4*>(A + a_base[i] + k0 + a_kc[i])
-                             : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < C::A_CH; i++) {
+        const uint32_t vo = (k0 + a_kc[i] < a.K) ? a_off[i] + (uint32_t)k0 * 2 : OOB;
+        glds16(rA, sb + (i * NT + wid * 64) * 16, vo);
+      }
     } else {
       const int tap = k0 / a.Cin;  // block-uniform: Cin % BK == 0
       const int ci0 = k0 - tap * a.Cin;
       const int ky = tap / 3, kx = tap - ky * 3;
 #pragma unroll
-      for (int i = 0; i < A_CH; i++) {
+      for (int i = 0; i < C::A_CH; i++) {
         const int iy = a_iy[i] + ky, ix = a_ix[i] + kx;
-        const bool ok = a_ok[i] && iy >= 0 && iy < a.Hin && ix >= 0 && ix < a.Win;
-        ra[set][i] = ok ? *reinterpret_cast<const uint4*>(A + ((int64_t)iy * a.Win + ix) * a.Cin +
-                                                          ci0 + a_kc[i])
-                        : make_uint4(0, 0, 0, 0);
+        const bool ok = (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+        const uint32_t vo =
+            ok ? (uint32_t)((((int64_t)iy * a.Win + ix) * a.Cin + ci0 + a_kc[i]) * 2) : OOB;
+        glds16(rA, sb + (i * NT + wid * 64) * 16, vo);
       }
     }
 #pragma unroll
-    for (int i = 0; i < B_CH; i++)
-      rb[set][i] = b_ok[i] ? *reinterpret_cast<const uint4*>(
-                                 B + (int64_t)(n0 + b_row[i]) * a.ldb + k0 + b_kc[i])
-                           : make_uint4(0, 0, 0, 0);
-  };
-  auto lstore = [&](auto setc, int buf) {
-    constexpr int set = decltype(setc)::value;
-#pragma unroll
-    for (int i = 0; i < A_CH; i++)
-      *reinterpret_cast<uint4*>(&As[buf][a_row[i]][a_kc[i]]) = relu_in ? relu8(ra[set][i])
-                                                                        : ra[set][i];
-#pragma unroll
-    for (int i = 0; i < B_CH; i++)
-      *reinterpret_cast<uint4*>(&Bs[buf][b_row[i]][b_kc[i]]) = rb[set][i];
+    for (int i = 0; i < C::B_CH; i++) {
+      const uint32_t vo = (k0 + b_kc[i] < a.K) ? b_off[i] + (uint32_t)k0 * 2 : OOB;
+      glds16(rB, sb + C::A_BYTES + (i * NT + wid * 64) * 16, vo);
+    }
   };
 
   f32x16 acc[TM][TN];
@@ -222,8 +341,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args a) {
       for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
 
   const int fr = lane & 31;
-  const int fk = (lane >> 5) * 8;
-  int nk = a.K / BK;
+  const int fh = lane >> 5;
+  const int fsw = (fr / C::RPB) % C::CPR;     // row swizzle of this lane's fragment rows
+  int nk = (a.K + BK - 1) / BK;
   int kbase = 0;
   if (SPLIT) {
     const int per = (nk + a.splits - 1) / a.splits;
@@ -231,133 +351,207 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(Args a) {
     nk = min(per, nk - kbase);
     if (nk < 0) nk = 0;
   }
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  if (nk > 0) {
-    gload(I0{}, (kbase + 0) * BK);
-    if (nk > 1) gload(I1{}, (kbase + 1) * BK);
-    lstore(I0{}, 0);
-    __syncthreads();
-  }
-  auto step = [&](int kt, auto curc) {
-    constexpr int cur = decltype(curc)::value;
-    using Other = std::integral_constant<int, cur ^ 1>;
-    // prefetch tile kt+2 into register set `cur` (its tile kt is already in LDS)
-    if (kt + 2 < nk) gload(curc, (kbase + kt + 2) * BK);
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; s++)
+    if (s < nk) issue(kbase + s, s);
+
+  for (int kt = 0; kt < nk; kt++) {
+    // retire tile kt (leave the younger tiles in flight), then make it visible to all waves
+    const int ahead = min(nk - 1 - kt, STAGES - 2);
+    if (STAGES >= 4 && ahead >= 2) vm_wait<C::L * 2>();
+    else if (ahead >= 1) vm_wait<C::L>();
+    else vm_wait<0>();
+    block_sync_lds();
+    if (kt + STAGES - 1 < nk) issue(kbase + kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const char* sA = lds + (kt % STAGES) * C::ST_BYTES;
+    const char* sB = sA + C::A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < BK / 16; kk++) {
+      const int slot = ((kk * 2 + fh) ^ fsw) * 16;
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; i++)
+      for (int i = 0; i < TM; i++) {
         af[i] = *reinterpret_cast<const bf16x8*>(
-            &As[cur][wm * (BM / WM) + i * 32 + fr][kk * 16 + fk]);
+            sA + (wm * (BM / WM) + i * 32 + fr) * (BK * 2) + slot);
+        if (MODE == 2) af[i] = relu_frag(af[i]);
+      }
 #pragma unroll
       for (int j = 0; j < TN; j++)
         bfr[j] = *reinterpret_cast<const bf16x8*>(
-            &Bs[cur][wn * (BN / WN) + j * 32 + fr][kk * 16 + fk]);
+            sB + (wn * (BN / WN) + j * 32 + fr) * (BK * 2) + slot);
 #pragma unroll
       for (int i = 0; i < TM; i++)
 #pragma unroll
         for (int j = 0; j < TN; j++)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) lstore(Other{}, cur ^ 1);
-    __syncthreads();
-  };
-  for (int kt = 0; kt < nk; kt += 2) {
-    step(kt, I0{});
-    if (kt + 1 < nk) step(kt + 1, I1{});
   }
 
+  // ---- epilogue through LDS: f32 tile [BM][CST] ----
+  block_sync_lds();
+  float* cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < TM; i++)
+#pragma unroll
+    for (int j = 0; j < TN; j++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        cs[row * C::CST + wn * (BN / WN) + j * 32 + fr] = acc[i][j][r];
+      }
+  block_sync_lds();
+
+  constexpr int VPR = BN / 8;                 // 8-column vectors per row
+  constexpr int NV = BM * VPR / NT;           // vectors per thread
   if (SPLIT) {
     float* P = a.ws + (int64_t)zz * a.M * a.N;
-#pragma unroll
-    for (int j = 0; j < TN; j++) {
-      const int n = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
-      if (n >= a.N) continue;
-#pragma unroll
-      for (int i = 0; i < TM; i++)
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int m = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (m < a.M) P[(int64_t)m * a.N + n] = acc[i][j][r];
-        }
+#pragma unroll 4
+    for (int v = 0; v < NV; v++) {
+      const int idx = v * NT + tid;
+      const int row = idx / VPR, c = (idx % VPR) * 8;
+      const int m = m0 + row, n = n0 + c;
+      if (m >= a.M || n >= a.N) continue;
+      const float* src = cs + row * C::CST + c;
+      float* dst = P + (int64_t)m * a.N + n;
+      if (a.vec) {
+        *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+        *reinterpret_cast<float4*>(dst + 4) = *reinterpret_cast<const float4*>(src + 4);
+      } else {
+        for (int t = 0; t < 8 && n + t < a.N; t++) dst[t] = src[t];
+      }
     }
     return;
   }
   const Epi e = make_epi(a, g);
-#pragma unroll
-  for (int j = 0; j < TN; j++) {
-    const int n = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
-    if (n >= a.N) continue;
-#pragma unroll
-    for (int i = 0; i < TM; i++)
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int m = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < a.M) epi_store(e, acc[i][j][r], m, n);
+  const bool rope = a.flags & M3S_EPI_ROPE;
+#pragma unroll 2
+  for (int v = 0; v < NV; v++) {
+    const int idx = v * NT + tid;
+    const int row = idx / VPR, c = (idx % VPR) * 8;
+    const int m = m0 + row, n = n0 + c;
+    if (m >= a.M || n >= a.N) continue;
+    const float* src = cs + row * C::CST + c;
+    const float* psrc = cs + row * C::CST + (c ^ 16);
+    if (a.vec) {
+      float x[8], p[8];
+      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(src);
+      *reinterpret_cast<float4*>(x + 4) = *reinterpret_cast<const float4*>(src + 4);
+      if (rope) {
+        *reinterpret_cast<float4*>(p) = *reinterpret_cast<const float4*>(psrc);
+        *reinterpret_cast<float4*>(p + 4) = *reinterpret_cast<const float4*>(psrc + 4);
       }
+      epi_vec8(e, x, p, m, n);
+    } else {
+      for (int t = 0; t < 8 && n + t < a.N; t++) epi_one(e, src[t], rope ? psrc[t] : 0.f, m, n + t);
+    }
   }
 }
 
-// Sum the split-K partials (fixed order) and apply the epilogue; 4 columns per thread.
+// Sum the split-K partials (fixed order) and apply the epilogue; 8 columns per thread.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
-  const int64_t per_b = (int64_t)a.M * a.N;
-  const int64_t idx4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int vpr = (a.N + 7) / 8;
+  const int64_t vid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int g = blockIdx.y;
-  if (idx4 >= per_b) return;
+  if (vid >= (int64_t)a.M * vpr) return;
+  const int m = (int)(vid / vpr);
+  const int n = (int)(vid - (int64_t)m * vpr) * 8;
+  const int64_t per_b = (int64_t)a.M * a.N;
   const Epi e = make_epi(a, g);
-  const float* P = a.ws + (int64_t)g * a.splits * per_b;
-  float4 s = *reinterpret_cast<const float4*>(P + idx4);
-  for (int k = 1; k < a.splits; k++) {
-    const float4 t = *reinterpret_cast<const float4*>(P + k * per_b + idx4);
-    s.x += t.x;
-    s.y += t.y;
-    s.z += t.z;
-    s.w += t.w;
+  const float* P = a.ws + (int64_t)g * a.splits * per_b + (int64_t)m * a.N;
+  const bool rope = (a.flags & M3S_EPI_ROPE) && n < a.rope_cols;
+  float x[8], p[8];
+  if (a.vec) {
+#pragma unroll
+    for (int t = 0; t < 8; t++) x[t] = p[t] = 0.f;
+    for (int k = 0; k < a.splits; k++) {
+      const float* q = P + k * per_b;
+      const float4 u0 = *reinterpret_cast<const float4*>(q + n);
+      const float4 u1 = *reinterpret_cast<const float4*>(q + n + 4);
+      x[0] += u0.x; x[1] += u0.y; x[2] += u0.z; x[3] += u0.w;
+      x[4] += u1.x; x[5] += u1.y; x[6] += u1.z; x[7] += u1.w;
+      if (rope) {
+        const float4 w0 = *reinterpret_cast<const float4*>(q + (n ^ 16));
+        const float4 w1 = *reinterpret_cast<const float4*>(q + (n ^ 16) + 4);
+        p[0] += w0.x; p[1] += w0.y; p[2] += w0.z; p[3] += w0.w;
+        p[4] += w1.x; p[5] += w1.y; p[6] += w1.z; p[7] += w1.w;
+      }
+    }
+    epi_vec8(e, x, p, m, n);
+  } else {
+    for (int t = 0; t < 8 && n + t < a.N; t++) {
+      float s = 0.f, ps = 0.f;
+      for (int k = 0; k < a.splits; k++) {
+        s += P[k * per_b + n + t];
+        if (rope) ps += P[k * per_b + ((n + t) ^ 16)];
+      }
+      epi_one(e, s, ps, m, n + t);
+    }
   }
-  const int m = (int)(idx4 / a.N);
-  const int n = (int)(idx4 - (int64_t)m * a.N);
-  epi_store(e, s.x, m, n);
-  epi_store(e, s.y, m, n + 1);
-  epi_store(e, s.z, m, n + 2);
-  epi_store(e, s.w, m, n + 3);
 }
 
-template <int BM, int BN, int BK, int WM, int WN>
+// ---------------------------------------------------------------------------------------
+// tile configurations
+// ---------------------------------------------------------------------------------------
+enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3 };
+
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC>
 int launch(Args& a, int batch, hipStream_t s) {
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = (a.N + BN - 1) / BN;
   const bool split = a.splits > 1;
   dim3 grid((unsigned)(a.tiles_m * a.tiles_n), 1, (unsigned)(batch * (split ? a.splits : 1)));
   if (split) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, 0, true>), grid, dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true>), grid, dim3(NT), 0,
+                       s, a);
     M3S_LAUNCH_CHECK();
-    const int64_t per_b = (int64_t)a.M * a.N;
-    dim3 rg(m3s_div_up(per_b / 4, 256), (unsigned)batch);
-    hipLaunchKernelGGL(splitk_reduce_kernel, rg, dim3(256), 0, s, a);
+    const int64_t nv = (int64_t)a.M * ((a.N + 7) / 8);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(m3s_div_up(nv, 256), (unsigned)batch),
+                       dim3(256), 0, s, a);
   } else if (a.mode == 0) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, 0, false>), grid, dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, false>), grid, dim3(NT),
+                       0, s, a);
+  } else if (a.flags & M3S_PRO_RELU) {
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 2, false>), grid, dim3(NT),
+                       0, s, a);
   } else {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, 1, false>), grid, dim3(NT), 0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 1, false>), grid, dim3(NT),
+                       0, s, a);
   }
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }
+
+int forced_tile() {
+  const char* s = getenv("M3S_GEMM_TILE");  // tuning override (tools/gemm_bench.py)
+  return s ? atoi(s) : 0;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
 extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   if (!d || !d->A || !d->B || !d->C) return M3S_ERR_INVALID_ARG;
   if (d->M <= 0 || d->N <= 0 || d->K <= 0 || d->batch <= 0) return M3S_ERR_INVALID_ARG;
-  if (d->K % 32 != 0) return M3S_ERR_INVALID_ARG;
+  if (d->K % 8 != 0) return M3S_ERR_INVALID_ARG;
   if (d->mode == 1 && (d->Cin % 32 != 0 || d->K != 9 * d->Cin)) return M3S_ERR_INVALID_ARG;
   if ((d->flags & (M3S_EPI_RES_F32 | M3S_EPI_RES_BF16)) && !d->R) return M3S_ERR_INVALID_ARG;
   if ((d->flags & M3S_EPI_CONVT) && (d->ct_s <= 0 || d->ct_cout <= 0 || d->ct_gw <= 0))
     return M3S_ERR_INVALID_ARG;
-  if (((uintptr_t)d->A | (uintptr_t)d->B) % 16) return M3S_ERR_INVALID_ARG;
-  if (d->mode == 0 && (d->lda % 8 || d->ldb % 8)) return M3S_ERR_INVALID_ARG;
+  if ((d->flags & M3S_EPI_ROPE) &&
+      (!d->rope_table || d->rope_tokens <= 0 || (d->flags & M3S_EPI_CONVT) ||
+       d->rope_cols % 64 != 0 || !aligned16(d->rope_table)))
+    return M3S_ERR_INVALID_ARG;
+  if (!aligned16(d->A) || !aligned16(d->B)) return M3S_ERR_INVALID_ARG;
+  if ((d->mode == 0 && d->lda % 8) || d->ldb % 8 || d->strideA % 8 || d->strideB % 8)
+    return M3S_ERR_INVALID_ARG;
   if (d->batch > 65535) return M3S_ERR_TOO_LARGE;
+  // buffer addressing: each operand's per-batch span must fit a 31-bit byte offset
+  const int64_t spanA = d->mode == 0 ? ((int64_t)(d->M - 1) * d->lda + d->K) * 2
+                                     : (int64_t)d->Hin * d->Win * d->Cin * 2;
+  const int64_t spanB = ((int64_t)(d->N - 1) * d->ldb + d->K) * 2;
+  if (spanA >= NUM_RECORDS || spanB >= NUM_RECORDS) return M3S_ERR_TOO_LARGE;
   Args a;
   a.A = reinterpret_cast<const bf16_t*>(d->A);
   a.lda = d->lda;
@@ -389,25 +583,41 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   a.ct_gw = d->ct_gw;
   a.splits = 1;
   a.ws = reinterpret_cast<float*>(d->workspace);
+  a.rope_tab = d->rope_table;
+  a.rope_cols = d->rope_cols;
+  a.rope_tokens = d->rope_tokens;
+  const bool out32 = d->flags & M3S_EPI_OUT_F32;
+  const bool has_bias = d->bias && (d->flags & M3S_EPI_BIAS);
+  a.vec = d->N % 8 == 0 && d->ldc % 8 == 0 && d->strideC % 8 == 0 && aligned16(d->C) &&
+          (!(d->flags & M3S_EPI_CONVT) || d->ct_cout % 8 == 0) &&
+          (!has_bias || (aligned16(d->bias) && d->strideBias % 4 == 0)) &&
+          (!d->R || (d->ldr % 8 == 0 && d->strideR % 8 == 0 && aligned16(d->R)));
+  (void)out32;
+  if ((d->flags & M3S_EPI_ROPE) && !a.vec) return M3S_ERR_INVALID_ARG;
   hipStream_t s = m3s_stream(stream);
-  const bool k64 = (d->K % 64 == 0) && (d->mode == 0 || d->Cin % 64 == 0);
+
+  // Tile choice (measured on the pair shapes, tools/gemm_tune.py): convs and short-K
+  // GEMMs run 64x128 tiles at 2 workgroups/CU; long-K GEMMs 128x128 tiles, K split across
+  // workgroups while the grid stays within one wave of 256 CUs.
+  const bool conv = d->mode == 1;
   const int64_t tiles128 = (int64_t)((d->M + 127) / 128) * ((d->N + 127) / 128) * d->batch;
-  const bool small_grid = tiles128 < 192 && d->M <= 1024;
-  if (small_grid && k64) {
-    // 64x128 tiles; split K when the grid still cannot fill the 256 CUs
-    const int64_t tiles = (int64_t)((d->M + 63) / 64) * ((d->N + 127) / 128) * d->batch;
-    int splits = d->split_k;
-    if (splits <= 0) {
-      splits = 1;
-      while (tiles * splits < 384 && (d->K / 64) / (splits * 2) >= 8) splits *= 2;
-    }
-    const bool can_split = d->mode == 0 && !(d->flags & M3S_EPI_CONVT) && d->N % 4 == 0 &&
-                           d->workspace &&
-                           (int64_t)splits * d->batch * d->M * d->N * 4 <= d->workspace_bytes;
-    if (splits > 1 && can_split) a.splits = splits;
-    return launch<64, 128, 64, 2, 2>(a, d->batch, s);
+  const int nk = (d->K + 63) / 64;
+  int cfg = forced_tile();
+  if (cfg == 0) cfg = conv ? T64 : (nk >= 32 ? T128 : T64);
+  if (conv && d->Cin % 64 != 0) cfg = T128K32;  // tap-uniform K-tiles need Cin % BK == 0
+  if (!conv && cfg == T128K32) cfg = T128;
+  int splits = d->split_k;
+  if (splits <= 0) {
+    splits = 1;
+    if (cfg == T128)
+      while (tiles128 * splits * 2 <= 256 && nk / (splits * 2) >= 8) splits *= 2;
   }
-  if (small_grid) return launch<64, 128, 32, 2, 2>(a, d->batch, s);
-  if (k64) return launch<128, 128, 64, 2, 2>(a, d->batch, s);
-  return launch<128, 128, 32, 2, 2>(a, d->batch, s);
+  const bool can_split = !conv && !(d->flags & M3S_EPI_CONVT) && d->workspace &&
+                         (int64_t)splits * d->batch * d->M * d->N * 4 <= d->workspace_bytes;
+  if (splits > 1 && can_split) a.splits = splits;
+  switch (cfg) {
+    case T128: return launch<128, 128, 64, 2, 2, 3, 1>(a, d->batch, s);
+    case T128K32: return launch<128, 128, 32, 2, 2, 4, 2>(a, d->batch, s);
+    default: return launch<64, 128, 64, 2, 2, 3, 2>(a, d->batch, s);
+  }
 }

@@ -49,6 +49,7 @@ SIGNATURES = {
     "m3s_vit_rope": (_I, [_P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "m3s_vit_attention": (_I, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _I64, _I64,
                                _I64, _I64, _I64, _I64, _F, _P]),
+    "m3s_vit_rope_table": (_I, [_P, _I64, _F, _P, _P]),
     "m3s_vit_patchify": (_I, [_P, _P, _I64, _I64, _I64, _P]),
     "m3s_vit_upsample2x": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "m3s_vit_dpt_out": (_I, [_P, _P, _P, _P, _P, _I64, _F, _I64, _I64, _I64, _P]),
@@ -68,11 +69,13 @@ class GemmDesc(ctypes.Structure):
                 ("Hin", ctypes.c_int32), ("Win", ctypes.c_int32), ("Cin", ctypes.c_int32),
                 ("Hout", ctypes.c_int32), ("Wout", ctypes.c_int32), ("stride", ctypes.c_int32),
                 ("ct_s", ctypes.c_int32), ("ct_cout", ctypes.c_int32), ("ct_gw", ctypes.c_int32),
-                ("workspace", _P), ("workspace_bytes", _I64), ("split_k", ctypes.c_int32)]
+                ("workspace", _P), ("workspace_bytes", _I64), ("split_k", ctypes.c_int32),
+                ("rope_table", _P), ("rope_cols", ctypes.c_int32),
+                ("rope_tokens", ctypes.c_int32)]
 
 
-EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT = (
-    1, 2, 4, 8, 16, 32, 64, 128)
+(EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT,
+ EPI_ROPE) = (1, 2, 4, 8, 16, 32, 64, 128, 256)
 
 _lib = None
 

@@ -51,7 +51,8 @@ class Ops:
         return _lib.stream(self.dev)
 
     def gemm(self, A, B, C, M, N, K, batch=1, *, lda=None, ldb=None, ldc=None, sA=0, sB=0,
-             sC=0, bias=None, sBias=0, R=None, ldr=None, sR=0, flags=0, conv=None, convt=None):
+             sC=0, bias=None, sBias=0, R=None, ldr=None, sR=0, flags=0, conv=None, convt=None,
+             rope=None, split_k=0):
         d = _lib.GemmDesc()
         d.A, d.lda, d.strideA = _p(A), lda if lda is not None else K, sA
         d.B, d.ldb, d.strideB = _p(B), ldb if ldb is not None else K, sB
@@ -59,7 +60,7 @@ class Ops:
         d.bias, d.strideBias = _p(bias), sBias
         d.R, d.ldr, d.strideR = _p(R), ldr if ldr is not None else N, sR
         d.M, d.N, d.K, d.batch, d.flags = M, N, K, batch, flags
-        d.workspace, d.workspace_bytes, d.split_k = _p(self.ws), self.ws.numel(), 0
+        d.workspace, d.workspace_bytes, d.split_k = _p(self.ws), self.ws.numel(), split_k
         if bias is not None:
             d.flags |= _lib.EPI_BIAS
         if conv is not None:
@@ -68,6 +69,9 @@ class Ops:
         if convt is not None:
             d.flags |= _lib.EPI_CONVT
             d.ct_s, d.ct_cout, d.ct_gw = convt
+        if rope is not None:  # (cos/sin table, rotated columns, tokens per image)
+            d.flags |= _lib.EPI_ROPE
+            d.rope_table, d.rope_cols, d.rope_tokens = _p(rope[0]), rope[1], rope[2]
         if self.probe is not None:
             st = torch.cuda.current_stream(self.dev)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -86,6 +90,13 @@ class Ops:
     def rope(self, t, ld, stride, pos, stride_pos, batch, S, heads, base):
         _lib.check(self.lib.m3s_vit_rope(_p(t), ld, stride, _p(pos), stride_pos, batch, S, heads,
                                          float(base), self._s()), "vit_rope")
+
+    def rope_table(self, pos, base):
+        """pos int64 [S,2] → f32 [S,2,2,16] cos/sin table for the GEMM-epilogue RoPE."""
+        tab = torch.empty((pos.shape[0], 2, 2, 16), dtype=F32, device=self.dev)
+        _lib.check(self.lib.m3s_vit_rope_table(_p(pos), pos.shape[0], float(base), _p(tab),
+                                               self._s()), "vit_rope_table")
+        return tab
 
     def attn(self, q, ldq, sq_b, k, v, ldkv, skv_b, o, ldo, so_b, batch, heads, sq, sk):
         _lib.check(self.lib.m3s_vit_attention(_p(q), ldq, sq_b, _p(k), _p(v), ldkv, skv_b, None,
@@ -254,6 +265,14 @@ class PairModel:
             self._bufs[key] = t
         return t
 
+    def rope_tab(self, gh, gw):
+        key = ("rope", gh, gw)
+        t = self._bufs.get(key)
+        if t is None:
+            t = self.ops.rope_table(self.positions(1, gh, gw)[0].contiguous(), self.a.rope_base)
+            self._bufs[key] = t
+        return t
+
     # ---- encoder: PatchEmbed + 24 blocks + enc_norm (batch of B images as M = B*S) ----
     def encode(self, img, out=None):
         """img f32 [B,3,H,W] → feat bf16 [B,S,E], pos int64 [B,S,2]."""
@@ -273,12 +292,12 @@ class PairModel:
         att = self._buf("enc_att", (M, E), BF16)
         hid = self._buf("enc_hid", (M, a.mlp_ratio * E), BF16)
         pos = self.positions(B, gh, gw)
+        rt = self.rope_tab(gh, gw)
         P = W.enc
         for i in range(a.enc_depth):
             o.ln(x, P["ln1_g"][i], P["ln1_b"][i], xn, M, E)
-            o.gemm(xn, P["qkv_w"][i], qkv, M, 3 * E, E, bias=P["qkv_b"][i])
-            o.rope(qkv, 3 * E, S * 3 * E, pos, S * 2, B, S, a.enc_heads, a.rope_base)
-            o.rope(qkv[:, E:], 3 * E, S * 3 * E, pos, S * 2, B, S, a.enc_heads, a.rope_base)
+            # qkv projection with RoPE2D on q and k fused into the epilogue
+            o.gemm(xn, P["qkv_w"][i], qkv, M, 3 * E, E, bias=P["qkv_b"][i], rope=(rt, 2 * E, S))
             o.attn(qkv, 3 * E, S * 3 * E, qkv[:, E:], qkv[:, 2 * E:], 3 * E, S * 3 * E, att, E,
                    S * E, B, a.enc_heads, S, S)
             o.gemm(att, P["proj_w"][i], x, M, E, E, bias=P["proj_b"][i], R=x,
@@ -313,6 +332,7 @@ class PairModel:
         att = self._buf("dec_att", (Z, S, D), BF16)
         hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), BF16)
         hooks = {"h0": h0}
+        rt = self.rope_tab(gh, gw)
         hk = set(a.hooks[1:3])
         R32 = _lib.EPI_OUT_F32 | _lib.EPI_RES_F32
         for i in range(a.dec_depth):
@@ -322,9 +342,7 @@ class PairModel:
             # self-attention
             o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D)
             o.gemm(xn, P["qkv_w"], qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
-                   bias=P["qkv_b"], sBias=3 * D)
-            o.rope(qkv, 3 * D, S * 3 * D, pos, 0, Z, S, a.dec_heads, a.rope_base)
-            o.rope(qkv[:, :, D:], 3 * D, S * 3 * D, pos, 0, Z, S, a.dec_heads, a.rope_base)
+                   bias=P["qkv_b"], sBias=3 * D, rope=(rt, 2 * D, S))
             o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,
                    D, S * D, Z, a.dec_heads, S, S)
             o.gemm(att, P["proj_w"], x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["proj_b"],
@@ -332,11 +350,9 @@ class PairModel:
             # cross-attention: q from norm2(x), k/v from y_
             o.ln(x, P["ln2_g"], P["ln2_b"], xn, S, D, Z, S * D, S * D, D)
             o.gemm(xn, P["q_w"], q, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["q_b"],
-                   sBias=D)
+                   sBias=D, rope=(rt, D, S))
             o.gemm(yn, P["kv_w"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D, sC=S * 2 * D,
-                   bias=P["kv_b"], sBias=2 * D)
-            o.rope(q, D, S * D, pos, 0, Z, S, a.dec_heads, a.rope_base)
-            o.rope(kv, 2 * D, S * 2 * D, pos, 0, Z, S, a.dec_heads, a.rope_base)
+                   bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S))
             o.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, att, D, S * D, Z, a.dec_heads,
                    S, S)
             o.gemm(att, P["cproj_w"], x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D,

@@ -53,6 +53,29 @@ def test_gemm_residual_f32(ops, dev):
     assert _rel(x, ref) < 1e-3  # f32 out: only the f32-accumulation order differs
 
 
+@pytest.mark.parametrize("split_k", [0, 1, 2, 4])
+def test_gemm_rope_epilogue(ops, dev, split_k):
+    """qkv projection with RoPE2D fused into the epilogue (applied to f32 acc + bias) vs
+    torch fp32 GEMM followed by the reference RoPE2D formula (oracle/vit_ref.py)."""
+    from oracle import vit_ref as V
+    g = torch.Generator(device=dev).manual_seed(7)
+    B, gh, gw, heads = 2, 24, 32, 4
+    S, C, K = gh * gw, heads * 64, 256
+    A = torch.randn(B * S, K, device=dev, generator=g).bfloat16()
+    W = (torch.randn(3 * C, K, device=dev, generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(3 * C, device=dev, generator=g)
+    out = torch.empty(B * S, 3 * C, device=dev, dtype=torch.bfloat16)
+    pos = V.positions(1, gh, gw, dev)[0].contiguous()
+    tab = ops.rope_table(pos, 100.0)
+    ops.gemm(A, W, out, B * S, 3 * C, K, bias=bias, rope=(tab, 2 * C, S), split_k=split_k)
+    y = (A.float() @ W.float().t() + bias).reshape(B, S, 3, heads, 64)
+    posb = V.positions(B, gh, gw, dev)
+    ref = y.clone()
+    for j in (0, 1):  # q, k rotated; v untouched
+        ref[:, :, j] = V.rope2d(y[:, :, j].transpose(1, 2), posb, 100.0).transpose(1, 2)
+    assert _rel(out, ref.reshape(B * S, 3 * C)) < 1e-2
+
+
 @pytest.mark.parametrize("H,W,cin,cout,stride,relu_in,res", [
     (24, 32, 256, 256, 1, True, True), (12, 16, 768, 768, 2, False, False),
     (96, 128, 96, 256, 1, False, False), (7, 9, 64, 32, 1, True, False)])

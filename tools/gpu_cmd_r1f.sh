@@ -1,0 +1,8 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/prof
+timeout -k 10 600 python -m pytest tests -m gpu -x -q -rf > gpurun_out/pytest_gpu_r1f.log 2>&1 && \
+timeout -k 10 600 python bench.py --steps 20 --warmup 2 --no-cpu-baseline > gpurun_out/bench_r1f.log 2>&1 && \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/trace_f -o bench --output-format csv \
+    -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof_trace_r1f.log 2>&1
+echo "exit=$?"
