@@ -176,7 +176,8 @@ enum {
   M3S_EPI_OUT_F32 = 32,   /* store f32 (default bf16)                          */
   M3S_PRO_RELU = 64,      /* ReLU applied to A while loading (conv prologue)   */
   M3S_EPI_CONVT = 128,    /* scatter rows/cols as ConvTranspose(k=s, stride=s) */
-  M3S_EPI_ROPE = 256      /* 2D RoPE on columns < rope_cols (head dim 64), after bias */
+  M3S_EPI_ROPE = 256      /* 2D RoPE on columns < rope_cols (head dim 64), after bias;
+                             not combined with a residual or CONVT                   */
 };
 
 typedef struct {

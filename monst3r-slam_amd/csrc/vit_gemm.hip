@@ -219,7 +219,12 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  // the builtin (not inline asm) so the compiler's own wait-count tracking sees the DMA
+  // retired — otherwise it later waits vmcnt(0) before every ds_read of the epilogue,
+  // i.e. behind each preceding global store.  gfx9 encoding: vmcnt[3:0] | vmcnt[5:4]<<14,
+  // expcnt[6:4] = 7, lgkmcnt[11:8] = 15 (no wait on those).
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
 }
 
 __device__ __forceinline__ void block_sync_lds() {
@@ -237,8 +242,21 @@ __device__ __forceinline__ bf16x8 relu_frag(bf16x8 x) {
   return x;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, bool SPLIT>
+// Optional in-kernel timeline (build with -DM3S_GEMM_STAMPS, tools/gemm_stamps.py): wave 0
+// of each workgroup accumulates s_memtime deltas per phase into g_m3s_stamps[block][8].
+#ifdef M3S_GEMM_STAMPS
+__device__ long long* g_m3s_stamps;
+#define M3S_T(v) long long v = (long long)__builtin_amdgcn_s_memtime()
+#else
+#define M3S_T(v)
+#endif
+
+// EPI >= 0: the epilogue flag set, fixed at compile time (straight-line epilogue code, and
+// the 8-wide vector path assumed); EPI < 0: flags read at run time.
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, bool SPLIT,
+          int EPI>
 __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
+  M3S_T(t_start);
   using C = Cfg<BM, BN, BK, STAGES>;
   constexpr int TM = BM / WM / 32;            // 32x32 accumulators per wave (M)
   constexpr int TN = BN / WN / 32;
@@ -303,33 +321,40 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
     b_off[i] = n < a.N ? (uint32_t)(((int64_t)n * a.ldb + kc) * 2) : OOB;
   }
 
-  auto issue = [&](int ktile, int stage) {
-    const int k0 = ktile * BK;
-    char* sb = lds + stage * C::ST_BYTES;
-    if (MODE == 0) {
-#pragma unroll
-      for (int i = 0; i < C::A_CH; i++) {
-        const uint32_t vo = (k0 + a_kc[i] < a.K) ? a_off[i] + (uint32_t)k0 * 2 : OOB;
-        glds16(rA, sb + (i * NT + wid * 64) * 16, vo);
-      }
-    } else {
-      const int tap = k0 / a.Cin;  // block-uniform: Cin % BK == 0
-      const int ci0 = k0 - tap * a.Cin;
-      const int ky = tap / 3, kx = tap - ky * 3;
-#pragma unroll
-      for (int i = 0; i < C::A_CH; i++) {
-        const int iy = a_iy[i] + ky, ix = a_ix[i] + kx;
+  // One DMA chunk j (< A_CH: A, else B) of K-tile k0 into stage buffer sb.  The conv tap
+  // (ky, kx) / channel offset ci0 are block-uniform per K-tile.
+  auto issue_chunk = [&](int j, int k0, char* sb, int ky, int kx, int ci0) {
+    if (j < C::A_CH) {
+      uint32_t vo;
+      if (MODE == 0) {
+        vo = (k0 + a_kc[j] < a.K) ? a_off[j] + (uint32_t)k0 * 2 : OOB;
+      } else {
+        const int iy = a_iy[j] + ky, ix = a_ix[j] + kx;
         const bool ok = (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-        const uint32_t vo =
-            ok ? (uint32_t)((((int64_t)iy * a.Win + ix) * a.Cin + ci0 + a_kc[i]) * 2) : OOB;
-        glds16(rA, sb + (i * NT + wid * 64) * 16, vo);
+        vo = ok ? (uint32_t)((((int64_t)iy * a.Win + ix) * a.Cin + ci0 + a_kc[j]) * 2) : OOB;
       }
-    }
-#pragma unroll
-    for (int i = 0; i < C::B_CH; i++) {
+      glds16(rA, sb + (j * NT + wid * 64) * 16, vo);
+    } else {
+      const int i = j - C::A_CH;
       const uint32_t vo = (k0 + b_kc[i] < a.K) ? b_off[i] + (uint32_t)k0 * 2 : OOB;
       glds16(rB, sb + C::A_BYTES + (i * NT + wid * 64) * 16, vo);
     }
+  };
+  auto tap_of = [&](int k0, int& ky, int& kx, int& ci0) {
+    ky = kx = ci0 = 0;
+    if (MODE != 0) {
+      const int tap = k0 / a.Cin;  // Cin % BK == 0
+      ci0 = k0 - tap * a.Cin;
+      ky = tap / 3;
+      kx = tap - ky * 3;
+    }
+  };
+  auto issue = [&](int ktile, int stage) {
+    const int k0 = ktile * BK;
+    int ky, kx, ci0;
+    tap_of(k0, ky, kx, ci0);
+#pragma unroll
+    for (int j = 0; j < C::L; j++) issue_chunk(j, k0, lds + stage * C::ST_BYTES, ky, kx, ci0);
   };
 
   f32x16 acc[TM][TN];
@@ -355,15 +380,28 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
 #pragma unroll
   for (int s = 0; s < STAGES - 1; s++)
     if (s < nk) issue(kbase + s, s);
+  M3S_T(t_pro);
+#ifdef M3S_GEMM_STAMPS
+  long long s_wait = 0, s_bar = 0, s_comp = 0;
+#endif
 
   for (int kt = 0; kt < nk; kt++) {
+    M3S_T(t0);
     // retire tile kt (leave the younger tiles in flight), then make it visible to all waves
     const int ahead = min(nk - 1 - kt, STAGES - 2);
     if (STAGES >= 4 && ahead >= 2) vm_wait<C::L * 2>();
     else if (ahead >= 1) vm_wait<C::L>();
     else vm_wait<0>();
+    M3S_T(t1);
     block_sync_lds();
-    if (kt + STAGES - 1 < nk) issue(kbase + kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    M3S_T(t2);
+    // the DMA of tile kt+STAGES-1 is spread over the MFMA phases of this tile so its issue
+    // cost overlaps MFMA execution
+    const bool pre = kt + STAGES - 1 < nk;
+    const int pk0 = (kbase + kt + STAGES - 1) * BK;
+    char* psb = lds + ((kt + STAGES - 1) % STAGES) * C::ST_BYTES;
+    int pky, pkx, pci0;
+    tap_of(pk0, pky, pkx, pci0);
     const char* sA = lds + (kt % STAGES) * C::ST_BYTES;
     const char* sB = sA + C::A_BYTES;
 #pragma unroll
@@ -380,16 +418,88 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
       for (int j = 0; j < TN; j++)
         bfr[j] = *reinterpret_cast<const bf16x8*>(
             sB + (wn * (BN / WN) + j * 32 + fr) * (BK * 2) + slot);
+      if (pre) {
+#pragma unroll
+        for (int j = 0; j < C::L; j++)
+          if (j * (BK / 16) / C::L == kk) issue_chunk(j, pk0, psb, pky, pkx, pci0);
+      }
 #pragma unroll
       for (int i = 0; i < TM; i++)
 #pragma unroll
         for (int j = 0; j < TN; j++)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+#ifdef M3S_GEMM_STAMPS
+    M3S_T(t3);
+    s_wait += t1 - t0;
+    s_bar += t2 - t1;
+    s_comp += t3 - t2;
+#endif
   }
+  M3S_T(t_loop);
 
   // ---- epilogue through LDS: f32 tile [BM][CST] ----
+  constexpr int VPR = BN / 8;                 // 8-column vectors per row
+  constexpr int NV = BM * VPR / NT;           // vectors per thread
+  constexpr int RSTEP = NT / VPR;             // rows between one thread's vectors
+  static_assert(NT % VPR == 0, "epilogue layout");
+  // Vector path: a thread owns columns [n, n+8) of rows r0 + v*RSTEP.  Its bias and, per
+  // group of EG vectors, the residual (or RoPE cos/sin) operands are loaded ahead of use —
+  // the first group before the LDS round trip — so their latency is overlapped.
+  constexpr int EG = NV < 4 ? NV : 4;
+  const int ec = (tid % VPR) * 8, er0 = tid / VPR;
+  const int en = n0 + ec;
+  const int fl = EPI >= 0 ? EPI : a.flags;
+  const bool vec = EPI >= 0 ? true : (a.vec != 0);
+  const bool vec_path = !SPLIT && vec && en < a.N;
+  float e_b[8], e_pb[8], e_x[EG][16];
+  Epi e = make_epi(a, g);
+  e.flags = fl;
+  const bool e_rope = (fl & M3S_EPI_ROPE) && en < a.rope_cols;
+  auto e_prefetch = [&](int v0) {
+#pragma unroll
+    for (int u = 0; u < EG; u++) {
+      const int m = min(m0 + er0 + (v0 + u) * RSTEP, a.M - 1);  // rows ≥ M are not stored
+#pragma unroll
+      for (int t = 0; t < 16; t++) e_x[u][t] = 0.f;
+      if (fl & M3S_EPI_RES_F32) {
+        const float* r = reinterpret_cast<const float*>(e.R) + (int64_t)m * e.ldr + en;
+        *reinterpret_cast<float4*>(&e_x[u][0]) = *reinterpret_cast<const float4*>(r);
+        *reinterpret_cast<float4*>(&e_x[u][4]) = *reinterpret_cast<const float4*>(r + 4);
+      } else if (fl & M3S_EPI_RES_BF16) {
+        const bf16x8 r = *reinterpret_cast<const bf16x8*>(
+            reinterpret_cast<const bf16_t*>(e.R) + (int64_t)m * e.ldr + en);
+#pragma unroll
+        for (int t = 0; t < 8; t++) e_x[u][t] = bf2f(r[t]);
+      } else if (e_rope) {  // RoPE GEMMs carry no residual: cos → [0, 8), sin → [8, 16)
+        const float* tb = e.rope_tab +
+                          ((int64_t)(m % e.rope_tokens) * 2 + ((en >> 5) & 1)) * 32 + (en & 15);
+        *reinterpret_cast<float4*>(&e_x[u][0]) = *reinterpret_cast<const float4*>(tb);
+        *reinterpret_cast<float4*>(&e_x[u][4]) = *reinterpret_cast<const float4*>(tb + 4);
+        *reinterpret_cast<float4*>(&e_x[u][8]) = *reinterpret_cast<const float4*>(tb + 16);
+        *reinterpret_cast<float4*>(&e_x[u][12]) = *reinterpret_cast<const float4*>(tb + 20);
+      }
+    }
+  };
+  if (vec_path) {
+    int co;
+    (void)out_offset(e, m0, en, co);
+#pragma unroll
+    for (int t = 0; t < 8; t++) e_b[t] = e_pb[t] = 0.f;
+    if (e.bias) {
+      *reinterpret_cast<float4*>(&e_b[0]) = *reinterpret_cast<const float4*>(e.bias + co);
+      *reinterpret_cast<float4*>(&e_b[4]) = *reinterpret_cast<const float4*>(e.bias + co + 4);
+      if (e_rope) {
+        *reinterpret_cast<float4*>(&e_pb[0]) = *reinterpret_cast<const float4*>(e.bias + (en ^ 16));
+        *reinterpret_cast<float4*>(&e_pb[4]) =
+            *reinterpret_cast<const float4*>(e.bias + (en ^ 16) + 4);
+      }
+    }
+    e_prefetch(0);
+  }
+  M3S_T(t_e0);
   block_sync_lds();
+  M3S_T(t_e1);
   float* cs = reinterpret_cast<float*>(lds);
 #pragma unroll
   for (int i = 0; i < TM; i++)
@@ -401,9 +511,8 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
         cs[row * C::CST + wn * (BN / WN) + j * 32 + fr] = acc[i][j][r];
       }
   block_sync_lds();
+  M3S_T(t_e2);
 
-  constexpr int VPR = BN / 8;                 // 8-column vectors per row
-  constexpr int NV = BM * VPR / NT;           // vectors per thread
   if (SPLIT) {
     float* P = a.ws + (int64_t)zz * a.M * a.N;
 #pragma unroll 4
@@ -414,38 +523,124 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
       if (m >= a.M || n >= a.N) continue;
       const float* src = cs + row * C::CST + c;
       float* dst = P + (int64_t)m * a.N + n;
-      if (a.vec) {
+      if (vec) {
         *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
         *reinterpret_cast<float4*>(dst + 4) = *reinterpret_cast<const float4*>(src + 4);
       } else {
         for (int t = 0; t < 8 && n + t < a.N; t++) dst[t] = src[t];
       }
     }
+#ifdef M3S_GEMM_STAMPS
+    if (tid == 0) {
+      M3S_T(t_end);
+      long long* o = g_m3s_stamps + ((int64_t)blockIdx.z * gridDim.x + blockIdx.x) * 12;
+      o[8] = t_e0 - t_loop;
+      o[9] = t_e1 - t_e0;
+      o[10] = t_e2 - t_e1;
+      o[11] = t_end - t_e2;
+      o[0] = t_pro - t_start;
+      o[1] = s_wait;
+      o[2] = s_bar;
+      o[3] = s_comp;
+      o[4] = t_end - t_loop;
+      o[5] = nk;
+      o[6] = t_end - t_start;
+      o[7] = t_start;
+    }
+#endif
     return;
   }
-  const Epi e = make_epi(a, g);
-  const bool rope = a.flags & M3S_EPI_ROPE;
-#pragma unroll 2
-  for (int v = 0; v < NV; v++) {
-    const int idx = v * NT + tid;
-    const int row = idx / VPR, c = (idx % VPR) * 8;
-    const int m = m0 + row, n = n0 + c;
-    if (m >= a.M || n >= a.N) continue;
-    const float* src = cs + row * C::CST + c;
-    const float* psrc = cs + row * C::CST + (c ^ 16);
-    if (a.vec) {
-      float x[8], p[8];
-      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(src);
-      *reinterpret_cast<float4*>(x + 4) = *reinterpret_cast<const float4*>(src + 4);
-      if (rope) {
-        *reinterpret_cast<float4*>(p) = *reinterpret_cast<const float4*>(psrc);
-        *reinterpret_cast<float4*>(p + 4) = *reinterpret_cast<const float4*>(psrc + 4);
+  if (vec_path) {
+    const float sg = (en & 16) ? 1.f : -1.f;
+    const bool has_res = fl & (M3S_EPI_RES_F32 | M3S_EPI_RES_BF16);
+    const bool rope_now = e_rope && !has_res;
+    // per group: all LDS reads first, then the math and the global stores (a ds_read issued
+    // after a global store waits for that store: the compiler cannot prove it does not
+    // alias the LDS-DMA ring — one such wait per group instead of one per vector)
+#pragma unroll
+    for (int v0 = 0; v0 < NV; v0 += EG) {
+      if (v0 > 0) e_prefetch(v0);
+      float xv[EG][8], pv[EG][8];
+#pragma unroll
+      for (int u = 0; u < EG; u++) {
+        const int row = er0 + (v0 + u) * RSTEP;
+        const float* src = cs + row * C::CST + ec;
+        *reinterpret_cast<float4*>(&xv[u][0]) = *reinterpret_cast<const float4*>(src);
+        *reinterpret_cast<float4*>(&xv[u][4]) = *reinterpret_cast<const float4*>(src + 4);
+        if (rope_now) {
+          const float* psrc = cs + row * C::CST + (ec ^ 16);
+          *reinterpret_cast<float4*>(&pv[u][0]) = *reinterpret_cast<const float4*>(psrc);
+          *reinterpret_cast<float4*>(&pv[u][4]) = *reinterpret_cast<const float4*>(psrc + 4);
+        }
       }
-      epi_vec8(e, x, p, m, n);
-    } else {
+#pragma unroll
+      for (int u = 0; u < EG; u++) {
+        const int m = m0 + er0 + (v0 + u) * RSTEP;
+        if (m >= a.M) continue;
+        float* x = xv[u];
+#pragma unroll
+        for (int t = 0; t < 8; t++) x[t] += e_b[t];
+        if (fl & M3S_EPI_GELU) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) x[t] = gelu_erf(x[t]);
+        }
+        if (rope_now) {
+#pragma unroll
+          for (int t = 0; t < 8; t++)
+            x[t] = x[t] * e_x[u][t] + sg * (pv[u][t] + e_pb[t]) * e_x[u][8 + t];
+        }
+        if (has_res) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) x[t] += e_x[u][t];
+        }
+        if (fl & M3S_EPI_RELU) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) x[t] = fmaxf(x[t], 0.f);
+        }
+        int co;
+        const int64_t off = out_offset(e, m, en, co);
+        if (fl & M3S_EPI_OUT_F32) {
+          float* cp = reinterpret_cast<float*>(e.C) + off;
+          *reinterpret_cast<float4*>(cp) = make_float4(x[0], x[1], x[2], x[3]);
+          *reinterpret_cast<float4*>(cp + 4) = make_float4(x[4], x[5], x[6], x[7]);
+        } else {
+          bf16x8 o;
+#pragma unroll
+          for (int t = 0; t < 8; t++) o[t] = f2bf(x[t]);
+          *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16_t*>(e.C) + off) = o;
+        }
+      }
+    }
+  } else if (!vec) {
+    const bool rope = fl & M3S_EPI_ROPE;
+    for (int v = 0; v < NV; v++) {
+      const int idx = v * NT + tid;
+      const int row = idx / VPR, c = (idx % VPR) * 8;
+      const int m = m0 + row, n = n0 + c;
+      if (m >= a.M || n >= a.N) continue;
+      const float* src = cs + row * C::CST + c;
+      const float* psrc = cs + row * C::CST + (c ^ 16);
       for (int t = 0; t < 8 && n + t < a.N; t++) epi_one(e, src[t], rope ? psrc[t] : 0.f, m, n + t);
     }
   }
+#ifdef M3S_GEMM_STAMPS
+  if (tid == 0) {
+    M3S_T(t_end);
+    long long* o = g_m3s_stamps + ((int64_t)blockIdx.z * gridDim.x + blockIdx.x) * 12;
+      o[8] = t_e0 - t_loop;
+      o[9] = t_e1 - t_e0;
+      o[10] = t_e2 - t_e1;
+      o[11] = t_end - t_e2;
+    o[0] = t_pro - t_start;
+    o[1] = s_wait;
+    o[2] = s_bar;
+    o[3] = s_comp;
+    o[4] = t_end - t_loop;
+    o[5] = nk;
+    o[6] = t_end - t_start;
+    o[7] = t_start;
+  }
+#endif
 }
 
 // Sum the split-K partials (fixed order) and apply the epilogue; 8 columns per thread.
@@ -493,7 +688,48 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
 // ---------------------------------------------------------------------------------------
 // tile configurations
 // ---------------------------------------------------------------------------------------
-enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3 };
+enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6 };
+
+// Epilogue flag sets compiled as straight-line variants (8-wide vector path), per mode:
+//   GEMM: bf16 out, +RoPE, +GELU, f32 residual → f32, f32 out;  conv: bf16 out, +bf16
+//   residual, +ReLU.  Any other combination (or an unaligned shape) runs the generic
+//   run-time-flag epilogue.  Each set exists with and without bias.
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, int E>
+bool try_epi(Args& a, dim3 grid, hipStream_t s, int key) {
+  if (key == E) {
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, E>), grid,
+                       dim3(NT), 0, s, a);
+    return true;
+  }
+  if (key == (E | M3S_EPI_BIAS)) {
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, E | M3S_EPI_BIAS>),
+                       grid, dim3(NT), 0, s, a);
+    return true;
+  }
+  return false;
+}
+
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE>
+void launch_main(Args& a, dim3 grid, hipStream_t s) {
+  const int key = (a.flags & ~(M3S_PRO_RELU | (a.bias ? 0 : M3S_EPI_BIAS)));
+  if (a.vec) {
+    if (MODE == 0) {
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0>(a, grid, s, key)) return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_ROPE>(a, grid, s, key)) return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_GELU>(a, grid, s, key)) return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32>(
+              a, grid, s, key))
+        return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_OUT_F32>(a, grid, s, key)) return;
+    } else {
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0>(a, grid, s, key)) return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RES_BF16>(a, grid, s, key)) return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RELU>(a, grid, s, key)) return;
+    }
+  }
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, -1>), grid,
+                     dim3(NT), 0, s, a);
+}
 
 template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC>
 int launch(Args& a, int batch, hipStream_t s) {
@@ -502,21 +738,18 @@ int launch(Args& a, int batch, hipStream_t s) {
   const bool split = a.splits > 1;
   dim3 grid((unsigned)(a.tiles_m * a.tiles_n), 1, (unsigned)(batch * (split ? a.splits : 1)));
   if (split) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true>), grid, dim3(NT), 0,
-                       s, a);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true, -1>), grid, dim3(NT),
+                       0, s, a);
     M3S_LAUNCH_CHECK();
     const int64_t nv = (int64_t)a.M * ((a.N + 7) / 8);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(m3s_div_up(nv, 256), (unsigned)batch),
                        dim3(256), 0, s, a);
   } else if (a.mode == 0) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, false>), grid, dim3(NT),
-                       0, s, a);
+    launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 0>(a, grid, s);
   } else if (a.flags & M3S_PRO_RELU) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 2, false>), grid, dim3(NT),
-                       0, s, a);
+    launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 2>(a, grid, s);
   } else {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 1, false>), grid, dim3(NT),
-                       0, s, a);
+    launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 1>(a, grid, s);
   }
   M3S_LAUNCH_CHECK();
   return M3S_OK;
@@ -531,6 +764,12 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
+#ifdef M3S_GEMM_STAMPS
+extern "C" int m3s_debug_set_stamps(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_m3s_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -2;
+}
+#endif
+
 extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   if (!d || !d->A || !d->B || !d->C) return M3S_ERR_INVALID_ARG;
   if (d->M <= 0 || d->N <= 0 || d->K <= 0 || d->batch <= 0) return M3S_ERR_INVALID_ARG;
@@ -540,7 +779,8 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   if ((d->flags & M3S_EPI_CONVT) && (d->ct_s <= 0 || d->ct_cout <= 0 || d->ct_gw <= 0))
     return M3S_ERR_INVALID_ARG;
   if ((d->flags & M3S_EPI_ROPE) &&
-      (!d->rope_table || d->rope_tokens <= 0 || (d->flags & M3S_EPI_CONVT) ||
+      (!d->rope_table || d->rope_tokens <= 0 ||
+       (d->flags & (M3S_EPI_CONVT | M3S_EPI_RES_F32 | M3S_EPI_RES_BF16)) ||
        d->rope_cols % 64 != 0 || !aligned16(d->rope_table)))
     return M3S_ERR_INVALID_ARG;
   if (!aligned16(d->A) || !aligned16(d->B)) return M3S_ERR_INVALID_ARG;
@@ -596,16 +836,24 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   if ((d->flags & M3S_EPI_ROPE) && !a.vec) return M3S_ERR_INVALID_ARG;
   hipStream_t s = m3s_stream(stream);
 
-  // Tile choice (measured on the pair shapes, tools/gemm_tune.py): convs and short-K
-  // GEMMs run 64x128 tiles at 2 workgroups/CU; long-K GEMMs 128x128 tiles, K split across
-  // workgroups while the grid stays within one wave of 256 CUs.
+  // Tile choice (measured on the pair shapes, tools/gemm_tune.py): 128x128 tiles (one
+  // workgroup per CU, K split while the grid stays within one wave of 256 CUs) unless the
+  // grid is tiny, K is short, or a large grid with short K favours 64x128 at 2/CU; convs
+  // 64x128, or 256x128 once the grid has several waves of workgroups.
   const bool conv = d->mode == 1;
   const int64_t tiles128 = (int64_t)((d->M + 127) / 128) * ((d->N + 127) / 128) * d->batch;
   const int nk = (d->K + 63) / 64;
   int cfg = forced_tile();
-  if (cfg == 0) cfg = conv ? T64 : (nk >= 32 ? T128 : T64);
+  if (cfg == 0) {
+    if (conv) cfg = tiles128 >= 1536 ? T256 : T64;
+    else if (nk >= 32) cfg = T128;
+    else if (tiles128 < 64 || nk < 8 || (tiles128 > 512 && nk < 16)) cfg = T64;
+    else cfg = T128;
+  }
+  if (cfg != T128 && cfg != T64 && cfg != T128K32 && cfg != T256) cfg = T128;
   if (conv && d->Cin % 64 != 0) cfg = T128K32;  // tap-uniform K-tiles need Cin % BK == 0
   if (!conv && cfg == T128K32) cfg = T128;
+  if (conv && d->Cin % 64 == 0 && cfg == T128K32) cfg = T128;
   int splits = d->split_k;
   if (splits <= 0) {
     splits = 1;
@@ -618,6 +866,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   switch (cfg) {
     case T128: return launch<128, 128, 64, 2, 2, 3, 1>(a, d->batch, s);
     case T128K32: return launch<128, 128, 32, 2, 2, 4, 2>(a, d->batch, s);
+    case T256: return launch<256, 128, 64, 2, 2, 3, 1>(a, d->batch, s);
     default: return launch<64, 128, 64, 2, 2, 3, 2>(a, d->batch, s);
   }
 }
