@@ -195,6 +195,8 @@ typedef struct {
   int32_t split_k;                         /* 0 = auto (uses workspace if it pays)  */
   const float* rope_table;                 /* ROPE: m3s_vit_rope_table output        */
   int32_t rope_cols, rope_tokens;          /* ROPE: rotated columns; row m → token m % rope_tokens */
+  int32_t weight_mod;                      /* >0: batch g reads B / bias of batch g % weight_mod
+                                              (P problem groups sharing one weight stack) */
 } m3s_gemm_desc;
 
 /* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 8 == 0; conv: Cin % 32 == 0.
@@ -212,12 +214,13 @@ int m3s_vit_rope_table(const int64_t* d_pos, int64_t tokens, float base, float* 
 
 /* LayerNorm over the last dim (eps), x f32/bf16 [rows][dim] → y bf16 or f32
  * (x_is_bf16 / y_is_f32 flags); batch strides in elements.  dim ≤ 4096, dim % 4 == 0.
+ * param_mod > 0: batch b uses gamma/beta of batch b % param_mod.
  * Batch b of y normalises batch (b ^ x_batch_xor) of x: with x_batch_xor = 1 the
  * decoder's norm_y(other side) (croco/blocks.py:187) runs for both sides in one launch. */
 int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_gamma,
                       const float* d_beta, void* d_y, int y_is_f32, int64_t rows, int64_t dim,
                       float eps, int64_t batch, int64_t stride_x, int64_t stride_y,
-                      int64_t stride_param, int x_batch_xor, void* stream);
+                      int64_t stride_param, int64_t param_mod, int x_batch_xor, void* stream);
 
 /* In-place 2-D RoPE (curope kernels.cu:17-82; pos_embed.py:106-158) on a bf16 view
  * t [B][S] rows of ld (head h at column h*64): dims [0,32) rotate by pos y, [32,64) by
@@ -250,10 +253,11 @@ int m3s_vit_upsample2x(const void* d_in, void* d_out, const void* d_add, int64_t
 /* DPT regression head tail, fused: t = relu(conv3x3 output) [B][P][128] bf16 is reduced
  * by the final 1x1 conv (128 → 4, per-head W4 f32 [B][4][128], b4 [B][4]) and post-processed
  * (d3r/heads/postprocess.py:10-58): pts3d = xyz/max(|xyz|,1e-8) * expm1(|xyz|),
- * conf = conf_min + exp(c).  pts3d f32 [P][3], conf f32 [P]. */
+ * conf = conf_min + exp(c).  pts3d f32 [P][3], conf f32 [P].
+ * param_mod > 0: batch b uses W4/b4 of head b % param_mod. */
 int m3s_vit_dpt_out(const void* d_t, const float* d_w4, const float* d_b4, float* d_pts3d,
                     float* d_conf, int64_t pixels, float conf_min, int64_t batch,
-                    int64_t stride_t, int64_t stride_out, void* stream);
+                    int64_t stride_t, int64_t stride_out, int64_t param_mod, void* stream);
 
 /* MASt3R local-feature tail (catmlp_dpt_head.py:25-39,84-96): feats bf16 or f32
  * [B][S][25*256] (fc2 output, per token) → pixel_shuffle(16) → desc = normalise(ch 0..23)
@@ -262,6 +266,25 @@ int m3s_vit_dpt_out(const void* d_t, const float* d_w4, const float* d_b4, float
 int m3s_vit_local_features(const float* d_feats, float* d_desc, uint16_t* d_desc_f16,
                            float* d_desc_conf, int64_t batch, int64_t h, int64_t w,
                            void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Dynamic-mask arithmetic (MonST3R dynamic-object filtering).
+ * ------------------------------------------------------------------------- */
+
+/* Error map + threshold of get_dynamic_mask (mast3r_slam/monst3r_utils.py:625-637):
+ * err = |flow - ego_flow[:2]| per pixel, norm = (err - min)/(max - min) (0 if max == min),
+ * mask = norm > threshold.  flow, ego_flow f32 [2][n] (channel-major, n = H*W; only the
+ * first 2 ego channels are read) → mask u8 [n].  workspace: (n + 64) floats (device). */
+int m3s_flow_error_mask(const float* d_flow, const float* d_ego_flow, int64_t n,
+                        float threshold, uint8_t* d_mask, float* d_workspace, void* stream);
+
+/* apply_dynamic_mask_to_pointmaps (monst3r_utils.py:300-341), in place: where mask[p]
+ * (u8 [hw], shared by the batch) C[b][p] = value, Q[b][p] = value (Q optional) and
+ * D[b][p][:] = 0 (D optional, f32 or f16 [b][hw][fdim]).  The reference zeroes D whenever
+ * it is given, whatever zero_descriptors says (:333-335); the flag is accepted and ignored. */
+int m3s_apply_dynamic_mask(const uint8_t* d_mask, float* d_C, float* d_Q, void* d_D,
+                           int D_is_f16, int64_t batch, int64_t hw, int64_t fdim,
+                           float value, int zero_descriptors, void* stream);
 
 #ifdef __cplusplus
 }

@@ -55,6 +55,7 @@ struct Args {
   float* ws;               // split-K partials [batch*splits][M][N]
   const float* rope_tab;   // [tokens][2 (y,x)][2 (cos,sin)][16]
   int rope_cols, rope_tokens;
+  int wmod;                // > 0: weights / bias of batch g % wmod
 };
 
 // ---------------------------------------------------------------------------------------
@@ -75,7 +76,8 @@ __device__ __forceinline__ Epi make_epi(const Args& a, int g) {
   Epi e;
   const bool out32 = a.flags & M3S_EPI_OUT_F32;
   const bool res32 = a.flags & M3S_EPI_RES_F32;
-  e.bias = (a.bias && (a.flags & M3S_EPI_BIAS)) ? a.bias + (int64_t)g * a.sBias : nullptr;
+  const int64_t gw = a.wmod > 0 ? g % a.wmod : g;
+  e.bias = (a.bias && (a.flags & M3S_EPI_BIAS)) ? a.bias + gw * a.sBias : nullptr;
   e.R = a.R ? reinterpret_cast<const char*>(a.R) + (int64_t)g * a.sR * (res32 ? 4 : 2) : nullptr;
   e.C = reinterpret_cast<char*>(a.C) + (int64_t)g * a.sC * (out32 ? 4 : 2);
   e.flags = a.flags;
@@ -286,7 +288,8 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>(a.A + (int64_t)g * a.sA), (short)0, NUM_RECORDS, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(a.B + (int64_t)g * a.sB), (short)0, NUM_RECORDS, 0x00020000);
+      const_cast<bf16_t*>(a.B + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sB), (short)0,
+      NUM_RECORDS, 0x00020000);
 
   // per-thread DMA chunks: chunk q = i*NT + tid lands at LDS row q / CPR, slot q % CPR and
   // carries logical K-chunk slot ^ swz(row)
@@ -826,6 +829,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   a.rope_tab = d->rope_table;
   a.rope_cols = d->rope_cols;
   a.rope_tokens = d->rope_tokens;
+  a.wmod = d->weight_mod > 0 ? d->weight_mod : 0;
   const bool out32 = d->flags & M3S_EPI_OUT_F32;
   const bool has_bias = d->bias && (d->flags & M3S_EPI_BIAS);
   a.vec = d->N % 8 == 0 && d->ldc % 8 == 0 && d->strideC % 8 == 0 && aligned16(d->C) &&

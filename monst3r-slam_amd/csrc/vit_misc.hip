@@ -13,13 +13,15 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
                                                         const float* __restrict__ beta,
                                                         void* __restrict__ y, int64_t rows,
                                                         int dim, float eps, int64_t sx,
-                                                        int64_t sy, int64_t sp, int xxor) {
+                                                        int64_t sy, int64_t sp, int64_t pmod,
+                                                        int xxor) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t b = blockIdx.y;
   if (row >= rows) return;
-  const float* g = gamma + b * sp;
-  const float* be = beta + b * sp;
+  const int64_t pb = pmod > 0 ? b % pmod : b;
+  const float* g = gamma + pb * sp;
+  const float* be = beta + pb * sp;
   constexpr int MAXV = 16;  // dim <= 64 * 4 * 16 = 4096
   float v[MAXV][4];
   const int nvec = dim / 4;
@@ -161,11 +163,13 @@ __global__ __launch_bounds__(256) void dpt_out_kernel(const bf16_t* __restrict__
                                                       const float* __restrict__ b4,
                                                       float* __restrict__ pts3d,
                                                       float* __restrict__ conf, int64_t pixels,
-                                                      float conf_min, int64_t st, int64_t so) {
+                                                      float conf_min, int64_t st, int64_t so,
+                                                      int64_t pmod) {
   __shared__ float sw[4 * 128];
   const int64_t b = blockIdx.y;
-  w4 += b * 512;  // per-head weights: w4 [B][4][128], b4 [B][4]
-  b4 += b * 4;
+  const int64_t pb = pmod > 0 ? b % pmod : b;
+  w4 += pb * 512;  // per-head weights: w4 [B][4][128], b4 [B][4]
+  b4 += pb * 4;
   for (int i = threadIdx.x; i < 512; i += 256) sw[i] = w4[i];
   __syncthreads();
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -231,24 +235,28 @@ __global__ __launch_bounds__(256) void local_feat_kernel(const float* __restrict
 extern "C" int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_gamma,
                                  const float* d_beta, void* d_y, int y_is_f32, int64_t rows,
                                  int64_t dim, float eps, int64_t batch, int64_t stride_x,
-                                 int64_t stride_y, int64_t stride_param, int x_batch_xor,
-                                 void* stream) {
+                                 int64_t stride_y, int64_t stride_param, int64_t param_mod,
+                                 int x_batch_xor, void* stream) {
   if (!d_x || !d_gamma || !d_beta || !d_y || rows <= 0 || batch <= 0) return M3S_ERR_INVALID_ARG;
   if (dim % 4 || dim > 4096 || dim <= 0) return M3S_ERR_INVALID_ARG;
   dim3 grid(m3s_div_up(rows, 4), (unsigned)batch);
   hipStream_t s = m3s_stream(stream);
   if (x_is_bf16 && !y_is_f32)
     hipLaunchKernelGGL((layernorm_kernel<true, false>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, x_batch_xor);
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,
+                       x_batch_xor);
   else if (x_is_bf16 && y_is_f32)
     hipLaunchKernelGGL((layernorm_kernel<true, true>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, x_batch_xor);
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,
+                       x_batch_xor);
   else if (!x_is_bf16 && !y_is_f32)
     hipLaunchKernelGGL((layernorm_kernel<false, false>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, x_batch_xor);
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,
+                       x_batch_xor);
   else
     hipLaunchKernelGGL((layernorm_kernel<false, true>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, x_batch_xor);
+                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,
+                       x_batch_xor);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }
@@ -282,13 +290,13 @@ extern "C" int m3s_vit_upsample2x(const void* d_in, void* d_out, const void* d_a
 extern "C" int m3s_vit_dpt_out(const void* d_t, const float* d_w4, const float* d_b4,
                                float* d_pts3d, float* d_conf, int64_t pixels, float conf_min,
                                int64_t batch, int64_t stride_t, int64_t stride_out,
-                               void* stream) {
+                               int64_t param_mod, void* stream) {
   if (!d_t || !d_w4 || !d_b4 || !d_pts3d || !d_conf || pixels <= 0 || batch <= 0)
     return M3S_ERR_INVALID_ARG;
   dim3 grid(m3s_div_up(pixels, 256), (unsigned)batch);
   hipLaunchKernelGGL(dpt_out_kernel, grid, dim3(256), 0, m3s_stream(stream),
                      reinterpret_cast<const bf16_t*>(d_t), d_w4, d_b4, d_pts3d, d_conf, pixels,
-                     conf_min, stride_t, stride_out);
+                     conf_min, stride_t, stride_out, param_mod);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }

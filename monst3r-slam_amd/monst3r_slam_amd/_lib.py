@@ -44,16 +44,18 @@ SIGNATURES = {
     "m3s_track_calib": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _F, _F, _F, _F,
                              _I, _F, _F, _P, _P, _P, _P, _P]),
     "m3s_vit_gemm": (_I, [_P, _P]),
-    "m3s_vit_layernorm": (_I, [_P, _I, _P, _P, _P, _I, _I64, _I64, _F, _I64, _I64, _I64, _I64, _I,
-                               _P]),
+    "m3s_vit_layernorm": (_I, [_P, _I, _P, _P, _P, _I, _I64, _I64, _F, _I64, _I64, _I64, _I64,
+                               _I64, _I, _P]),
     "m3s_vit_rope": (_I, [_P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "m3s_vit_attention": (_I, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _I64, _I64,
                                _I64, _I64, _I64, _I64, _F, _P]),
     "m3s_vit_rope_table": (_I, [_P, _I64, _F, _P, _P]),
     "m3s_vit_patchify": (_I, [_P, _P, _I64, _I64, _I64, _P]),
     "m3s_vit_upsample2x": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
-    "m3s_vit_dpt_out": (_I, [_P, _P, _P, _P, _P, _I64, _F, _I64, _I64, _I64, _P]),
+    "m3s_vit_dpt_out": (_I, [_P, _P, _P, _P, _P, _I64, _F, _I64, _I64, _I64, _I64, _P]),
     "m3s_vit_local_features": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P]),
+    "m3s_flow_error_mask": (_I, [_P, _P, _I64, _F, _P, _P, _P]),
+    "m3s_apply_dynamic_mask": (_I, [_P, _P, _P, _P, _I, _I64, _I64, _I64, _F, _I, _P]),
 }
 
 
@@ -71,7 +73,7 @@ class GemmDesc(ctypes.Structure):
                 ("ct_s", ctypes.c_int32), ("ct_cout", ctypes.c_int32), ("ct_gw", ctypes.c_int32),
                 ("workspace", _P), ("workspace_bytes", _I64), ("split_k", ctypes.c_int32),
                 ("rope_table", _P), ("rope_cols", ctypes.c_int32),
-                ("rope_tokens", ctypes.c_int32)]
+                ("rope_tokens", ctypes.c_int32), ("weight_mod", ctypes.c_int32)]
 
 
 (EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT,

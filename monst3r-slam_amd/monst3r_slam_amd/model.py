@@ -52,7 +52,7 @@ class Ops:
 
     def gemm(self, A, B, C, M, N, K, batch=1, *, lda=None, ldb=None, ldc=None, sA=0, sB=0,
              sC=0, bias=None, sBias=0, R=None, ldr=None, sR=0, flags=0, conv=None, convt=None,
-             rope=None, split_k=0):
+             rope=None, split_k=0, wmod=0):
         d = _lib.GemmDesc()
         d.A, d.lda, d.strideA = _p(A), lda if lda is not None else K, sA
         d.B, d.ldb, d.strideB = _p(B), ldb if ldb is not None else K, sB
@@ -61,6 +61,7 @@ class Ops:
         d.R, d.ldr, d.strideR = _p(R), ldr if ldr is not None else N, sR
         d.M, d.N, d.K, d.batch, d.flags = M, N, K, batch, flags
         d.workspace, d.workspace_bytes, d.split_k = _p(self.ws), self.ws.numel(), split_k
+        d.weight_mod = wmod
         if bias is not None:
             d.flags |= _lib.EPI_BIAS
         if conv is not None:
@@ -82,10 +83,10 @@ class Ops:
             return
         _lib.check(self.lib.m3s_vit_gemm(ctypes.byref(d), self._s()), "vit_gemm")
 
-    def ln(self, x, g, b, y, rows, dim, batch=1, sx=0, sy=0, sp=0, y_f32=False, xor=0):
+    def ln(self, x, g, b, y, rows, dim, batch=1, sx=0, sy=0, sp=0, y_f32=False, xor=0, pmod=0):
         _lib.check(self.lib.m3s_vit_layernorm(
             _p(x), int(x.dtype == BF16), _p(g), _p(b), _p(y), int(y_f32), rows, dim, LN_EPS,
-            batch, sx, sy, sp, xor, self._s()), "vit_layernorm")
+            batch, sx, sy, sp, pmod, xor, self._s()), "vit_layernorm")
 
     def rope(self, t, ld, stride, pos, stride_pos, batch, S, heads, base):
         _lib.check(self.lib.m3s_vit_rope(_p(t), ld, stride, _p(pos), stride_pos, batch, S, heads,
@@ -110,9 +111,10 @@ class Ops:
         _lib.check(self.lib.m3s_vit_upsample2x(_p(x), _p(out), _p(add), b, h, w, c,
                                                oh or 2 * h, ow or 2 * w, self._s()), "upsample2x")
 
-    def dpt_out(self, t, w4, b4, pts, conf, pixels, conf_min, batch, st, so):
+    def dpt_out(self, t, w4, b4, pts, conf, pixels, conf_min, batch, st, so, pmod=0):
         _lib.check(self.lib.m3s_vit_dpt_out(_p(t), _p(w4), _p(b4), _p(pts), _p(conf), pixels,
-                                            float(conf_min), batch, st, so, self._s()), "dpt_out")
+                                            float(conf_min), batch, st, so, pmod, self._s()),
+                   "dpt_out")
 
     def local_features(self, feats, desc, desc16, dconf, b, h, w):
         _lib.check(self.lib.m3s_vit_local_features(_p(feats), _p(desc), _p(desc16), _p(dconf), b,
@@ -249,10 +251,13 @@ class PairModel:
 
     # ---- buffers ----
     def _buf(self, key, shape, dtype):
-        t = self._bufs.get(key)
-        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+        """Persistent scratch per (name, shape, dtype): a buffer is never freed or
+        reallocated, so HIP graphs captured over it stay valid when other batch sizes run."""
+        k = (key, tuple(shape), dtype)
+        t = self._bufs.get(k)
+        if t is None:
             t = torch.empty(shape, dtype=dtype, device=self.dev)
-            self._bufs[key] = t
+            self._bufs[k] = t
         return t
 
     def positions(self, b, gh, gw):
@@ -315,15 +320,25 @@ class PairModel:
     def decode(self, feat_i, feat_j, pos, gh, gw):
         """feat_i/feat_j bf16 [S,E] (frame i = side 1, keyframe j = side 2).
         Returns hooks dict: h0 bf16 [4,S,E], h6/h9/h12 bf16 [4,S,D] (h12 = dec_norm)."""
+        S, E = gh * gw, self.a.enc_dim
+        return self.decode_multi(feat_i.reshape(1, S, E), feat_j.reshape(1, S, E), gh, gw)
+
+    def decode_multi(self, feat1, feat2, gh, gw):
+        """G directed pairs at once: feat1/feat2 bf16 [G,S,E] are the first / second view of
+        each pair (d3r/model.py:171-190 `_decoder(f1, pos1, f2, pos2)`), decoded by BOTH
+        models.  Problems z = (g*2 + model)*2 + side; every launch covers all 4G of them and
+        reads the weight stack of z % 4 (weight_mod).  Returns hooks [4G,S,*]."""
         o, a, W = self.ops, self.a, self.w
         S, E, D = gh * gw, a.enc_dim, a.dec_dim
-        Z = 4
+        G = feat1.shape[0]
+        Z = 4 * G
         h0 = self._buf("h0", (Z, S, E), BF16)
-        h0[0::2].copy_(feat_i.reshape(1, S, E).expand(2, S, E))
-        h0[1::2].copy_(feat_j.reshape(1, S, E).expand(2, S, E))
+        hv = h0.view(G, 2, 2, S, E)
+        hv[:, :, 0].copy_(feat1.reshape(G, 1, S, E).expand(G, 2, S, E))
+        hv[:, :, 1].copy_(feat2.reshape(G, 1, S, E).expand(G, 2, S, E))
         x = self._buf("dec_x", (Z, S, D), F32)
         o.gemm(h0, W.dec_embed_w, x, S, D, E, Z, sA=S * E, sB=D * E, sC=S * D,
-               bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32)
+               bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32, wmod=4)
         xn = self._buf("dec_xn", (Z, S, D), BF16)
         yn = self._buf("dec_yn", (Z, S, D), BF16)
         qkv = self._buf("dec_qkv", (Z, S, 3 * D), BF16)
@@ -338,37 +353,39 @@ class PairModel:
         for i in range(a.dec_depth):
             P = W.dec[i]
             # y_ = norm_y(previous output of the other side) — before this layer updates x
-            o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1)
+            o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1, pmod=4)
             # self-attention
-            o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D)
+            o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
             o.gemm(xn, P["qkv_w"], qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
-                   bias=P["qkv_b"], sBias=3 * D, rope=(rt, 2 * D, S))
+                   bias=P["qkv_b"], sBias=3 * D, rope=(rt, 2 * D, S), wmod=4)
             o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,
                    D, S * D, Z, a.dec_heads, S, S)
             o.gemm(att, P["proj_w"], x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["proj_b"],
-                   sBias=D, R=x, sR=S * D, flags=R32)
+                   sBias=D, R=x, sR=S * D, flags=R32, wmod=4)
             # cross-attention: q from norm2(x), k/v from y_
-            o.ln(x, P["ln2_g"], P["ln2_b"], xn, S, D, Z, S * D, S * D, D)
+            o.ln(x, P["ln2_g"], P["ln2_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
             o.gemm(xn, P["q_w"], q, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["q_b"],
-                   sBias=D, rope=(rt, D, S))
+                   sBias=D, rope=(rt, D, S), wmod=4)
             o.gemm(yn, P["kv_w"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D, sC=S * 2 * D,
-                   bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S))
+                   bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4)
             o.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, att, D, S * D, Z, a.dec_heads,
                    S, S)
             o.gemm(att, P["cproj_w"], x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D,
-                   bias=P["cproj_b"], sBias=D, R=x, sR=S * D, flags=R32)
+                   bias=P["cproj_b"], sBias=D, R=x, sR=S * D, flags=R32, wmod=4)
             # MLP
-            o.ln(x, P["ln3_g"], P["ln3_b"], xn, S, D, Z, S * D, S * D, D)
+            o.ln(x, P["ln3_g"], P["ln3_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
             o.gemm(xn, P["fc1_w"], hid, S, a.mlp_ratio * D, D, Z, sA=S * D,
                    sB=a.mlp_ratio * D * D, sC=S * a.mlp_ratio * D, bias=P["fc1_b"],
-                   sBias=a.mlp_ratio * D, flags=_lib.EPI_GELU)
+                   sBias=a.mlp_ratio * D, flags=_lib.EPI_GELU, wmod=4)
             o.gemm(hid, P["fc2_w"], x, S, D, a.mlp_ratio * D, Z, sA=S * a.mlp_ratio * D,
                    sB=a.mlp_ratio * D * D, sC=S * D, bias=P["fc2_b"], sBias=D, R=x, sR=S * D,
-                   flags=R32)
+                   flags=R32, wmod=4)
             if (i + 1) in hk:
-                hooks[f"h{i + 1}"] = x.to(BF16)
+                hb = self._buf(f"h{i + 1}", (Z, S, D), BF16)
+                hb.copy_(x)
+                hooks[f"h{i + 1}"] = hb
         h12 = self._buf("h12", (Z, S, D), BF16)
-        o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D)
+        o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=4)
         hooks["h12"] = h12
         return hooks
 
@@ -381,7 +398,8 @@ class PairModel:
         o.gemm(x, H[wkey], out, hout * wout, cout, 9 * cin, b, sA=hin * win * cin,
                sB=cout * 9 * cin, sC=hout * wout * cout,
                bias=H[bias_key] if bias_key else None, sBias=cout, R=R,
-               sR=hout * wout * cout, flags=flags, conv=(hin, win, cin, hout, wout, stride))
+               sR=hout * wout * cout, flags=flags, conv=(hin, win, cin, hout, wout, stride),
+               wmod=4)
         return hout, wout
 
     def _rcu(self, x, k, u, b, h, w, out, addend_res=None):
@@ -410,39 +428,41 @@ class PairModel:
         self._rcu(s1, k, 2, b, h, w, s2)
         oc = self._buf(("fus_oc", h, w), (b, h, w, F), BF16)
         o.gemm(s2, H[f"r{k}_out_w"], oc, h * w, F, F, b, sA=h * w * F, sB=F * F, sC=h * w * F,
-               bias=H[f"r{k}_out_b"], sBias=F)
+               bias=H[f"r{k}_out_b"], sBias=F, wmod=4)
         oh, ow = next_hw
         o.up2(oc, out, b, h, w, F, oh, ow, add=next_skip)
 
     def heads(self, hooks, gh, gw, H, W):
-        """Four DPT heads (z = model*2 + side) + MASt3R local features.
-        Returns pts3d f32 [4,H,W,3], conf f32 [4,H,W], desc16 f16 [2,H,W,24],
-        desc f32 [2,H,W,24], desc_conf f32 [2,H,W] (the latter three for z = 2, 3)."""
+        """DPT heads of all 4G problems (z = (g*2 + model)*2 + side, head weights z % 4) +
+        MASt3R local features of the model-1 problems.
+        Returns pts3d f32 [4G,H,W,3], conf f32 [4G,H,W], desc16 f16 [2G,H,W,24],
+        desc f32 [2G,H,W,24], desc_conf f32 [2G,H,W] (the latter three: (g, side) of model 1)."""
         o, a, Hw = self.ops, self.a, self.w.h
-        Z = 4
+        Z = hooks["h0"].shape[0]
+        G = Z // 4
         S, E, D = gh * gw, a.enc_dim, a.dec_dim
         Ld = a.layer_dims
         F = a.feature_dim
         # act_postprocess
         t0 = self._buf("ap_t0", (Z, S, Ld[0]), BF16)
         o.gemm(hooks["h0"], Hw["ap0_w"], t0, S, Ld[0], E, Z, sA=S * E, sB=Ld[0] * E,
-               sC=S * Ld[0], bias=Hw["ap0_b"], sBias=Ld[0])
+               sC=S * Ld[0], bias=Hw["ap0_b"], sBias=Ld[0], wmod=4)
         L0 = self._buf("ap_L0", (Z, 4 * gh, 4 * gw, Ld[0]), BF16)
         o.gemm(t0, Hw["ap0t_w"], L0, S, 16 * Ld[0], Ld[0], Z, sA=S * Ld[0],
                sB=16 * Ld[0] * Ld[0], sC=16 * S * Ld[0], bias=Hw["ap0t_b"], sBias=Ld[0],
-               convt=(4, Ld[0], gw))
+               convt=(4, Ld[0], gw), wmod=4)
         t1 = self._buf("ap_t1", (Z, S, Ld[1]), BF16)
         o.gemm(hooks["h6"], Hw["ap1_w"], t1, S, Ld[1], D, Z, sA=S * D, sB=Ld[1] * D,
-               sC=S * Ld[1], bias=Hw["ap1_b"], sBias=Ld[1])
+               sC=S * Ld[1], bias=Hw["ap1_b"], sBias=Ld[1], wmod=4)
         L1 = self._buf("ap_L1", (Z, 2 * gh, 2 * gw, Ld[1]), BF16)
         o.gemm(t1, Hw["ap1t_w"], L1, S, 4 * Ld[1], Ld[1], Z, sA=S * Ld[1], sB=4 * Ld[1] * Ld[1],
-               sC=4 * S * Ld[1], bias=Hw["ap1t_b"], sBias=Ld[1], convt=(2, Ld[1], gw))
+               sC=4 * S * Ld[1], bias=Hw["ap1t_b"], sBias=Ld[1], convt=(2, Ld[1], gw), wmod=4)
         L2 = self._buf("ap_L2", (Z, gh, gw, Ld[2]), BF16)
         o.gemm(hooks["h9"], Hw["ap2_w"], L2, S, Ld[2], D, Z, sA=S * D, sB=Ld[2] * D,
-               sC=S * Ld[2], bias=Hw["ap2_b"], sBias=Ld[2])
+               sC=S * Ld[2], bias=Hw["ap2_b"], sBias=Ld[2], wmod=4)
         t3 = self._buf("ap_t3", (Z, gh, gw, Ld[3]), BF16)
         o.gemm(hooks["h12"], Hw["ap3_w"], t3, S, Ld[3], D, Z, sA=S * D, sB=Ld[3] * D,
-               sC=S * Ld[3], bias=Hw["ap3_b"], sBias=Ld[3])
+               sC=S * Ld[3], bias=Hw["ap3_b"], sBias=Ld[3], wmod=4)
         g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
         L3 = self._buf("ap_L3", (Z, g3h, g3w, Ld[3]), BF16)
         self._conv3(t3, "ap3c_w", L3, Z, gh, gw, Ld[3], Ld[3], stride=2, bias_key="ap3c_b")
@@ -476,25 +496,26 @@ class PairModel:
         pts = self._buf("pts3d", (Z, H, W, 3), F32)
         conf = self._buf("conf", (Z, H, W), F32)
         o.dpt_out(hd2, Hw["head4_w"], Hw["head4_b"], pts, conf, H * W, a.conf_min, Z,
-                  H * W * a.last_dim, H * W)
+                  H * W * a.last_dim, H * W, pmod=4)
         # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle
         aM = self.w.arch_mast3r
         idim = E + D
         hidd = 4 * idim
         odim = (aM.desc_dim + 1) * aM.patch ** 2
-        cat = self._buf("lf_cat", (2, S, idim), BF16)
-        cat[:, :, :E].copy_(hooks["h0"][2:])
-        cat[:, :, E:].copy_(hooks["h12"][2:])
-        lh = self._buf("lf_hid", (2, S, hidd), BF16)
-        o.gemm(cat, self.w.lf_fc1_w, lh, S, hidd, idim, 2, sA=S * idim, sB=hidd * idim,
-               sC=S * hidd, bias=self.w.lf_fc1_b, sBias=hidd, flags=_lib.EPI_GELU)
-        lo = self._buf("lf_out", (2, S, odim), F32)
-        o.gemm(lh, self.w.lf_fc2_w, lo, S, odim, hidd, 2, sA=S * hidd, sB=odim * hidd,
-               sC=S * odim, bias=self.w.lf_fc2_b, sBias=odim, flags=_lib.EPI_OUT_F32)
-        desc = self._buf("desc", (2, H, W, aM.desc_dim), F32)
-        desc16 = self._buf("desc16", (2, H, W, aM.desc_dim), torch.float16)
-        dconf = self._buf("desc_conf", (2, H, W), F32)
-        o.local_features(lo, desc, desc16, dconf, 2, H, W)
+        cat = self._buf("lf_cat", (2 * G, S, idim), BF16)
+        cv = cat.view(G, 2, S, idim)
+        cv[..., :E].copy_(hooks["h0"].view(G, 2, 2, S, E)[:, 1])
+        cv[..., E:].copy_(hooks["h12"].view(G, 2, 2, S, D)[:, 1])
+        lh = self._buf("lf_hid", (2 * G, S, hidd), BF16)
+        o.gemm(cat, self.w.lf_fc1_w, lh, S, hidd, idim, 2 * G, sA=S * idim, sB=hidd * idim,
+               sC=S * hidd, bias=self.w.lf_fc1_b, sBias=hidd, flags=_lib.EPI_GELU, wmod=2)
+        lo = self._buf("lf_out", (2 * G, S, odim), F32)
+        o.gemm(lh, self.w.lf_fc2_w, lo, S, odim, hidd, 2 * G, sA=S * hidd, sB=odim * hidd,
+               sC=S * odim, bias=self.w.lf_fc2_b, sBias=odim, flags=_lib.EPI_OUT_F32, wmod=2)
+        desc = self._buf("desc", (2 * G, H, W, aM.desc_dim), F32)
+        desc16 = self._buf("desc16", (2 * G, H, W, aM.desc_dim), torch.float16)
+        dconf = self._buf("desc_conf", (2 * G, H, W), F32)
+        o.local_features(lo, desc, desc16, dconf, 2 * G, H, W)
         return pts, conf, desc16, desc, dconf
 
     def _fusion_skip(self, k, path, skip, b, h, w, next_hw, out):
@@ -520,6 +541,53 @@ class PairModel:
         pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W)
         return dict(X=pts[0:2], C=conf[0:2], D16=desc16, D=desc, Q=dconf, feat_i=feat_i,
                     mast3r_X=pts[2:4], mast3r_C=conf[2:4])
+
+    # ---- monst3r_inference_mono (monst3r_utils.py:187-211) ----
+    def mono(self, feat, H, W):
+        """Self-pair decode of one frame's features feat bf16 [1,S,E].  Returns X [2,H,W,3]
+        (res11, res21), C [2,H,W] of the MonST3R heads (the MASt3R half of the batched
+        problem set runs too and is ignored, as its outputs are in the reference)."""
+        a = self.a
+        gh, gw = H // a.patch, W // a.patch
+        f = feat.reshape(1, gh * gw, a.enc_dim)
+        hooks = self.decode_multi(f, f, gh, gw)
+        pts, conf, _, _, _ = self.heads(hooks, gh, gw, H, W)
+        return pts[0:2], conf[0:2]
+
+    # ---- monst3r_decode_symmetric_batch (monst3r_utils.py:141-184) ----
+    def symmetric(self, feat_i, feat_j, H, W, chunk=4):
+        """B keyframe pairs (i_b, j_b), both directions, both models.  feat_i/feat_j bf16
+        [B,S,E].  The reference loops over b and runs 4 decoder calls + 8 heads per pair
+        sequentially; here `chunk` pairs (8 x chunk problems) go through every launch.
+        Returns fresh tensors in the reference's [4,B,...] order (Xii, Xji, Xjj, Xij):
+        X f32 [4,B,H,W,3], C [4,B,H,W] (MonST3R), D f32 [4,B,H,W,24], D16 f16, Q [4,B,H,W]
+        (MASt3R)."""
+        a = self.a
+        gh, gw = H // a.patch, W // a.patch
+        S, E = gh * gw, a.enc_dim
+        B = feat_i.shape[0]
+        fi, fj = feat_i.reshape(B, S, E), feat_j.reshape(B, S, E)
+        X = torch.empty((4, B, H, W, 3), dtype=F32, device=self.dev)
+        C = torch.empty((4, B, H, W), dtype=F32, device=self.dev)
+        D = torch.empty((4, B, H, W, 24), dtype=F32, device=self.dev)
+        D16 = torch.empty((4, B, H, W, 24), dtype=torch.float16, device=self.dev)
+        Q = torch.empty((4, B, H, W), dtype=F32, device=self.dev)
+        for b0 in range(0, B, chunk):
+            nb = min(chunk, B - b0)
+            # directed pairs g = b*2 + d: d = 0 → (i, j), d = 1 → (j, i)
+            f1 = torch.stack([fi[b0:b0 + nb], fj[b0:b0 + nb]], 1).reshape(2 * nb, S, E)
+            f2 = torch.stack([fj[b0:b0 + nb], fi[b0:b0 + nb]], 1).reshape(2 * nb, S, E)
+            hooks = self.decode_multi(f1, f2, gh, gw)
+            pts, conf, d16, d32, dq = self.heads(hooks, gh, gw, H, W)
+            # problem z = ((b*2 + d)*2 + model)*2 + side → reference slot d*2 + side
+            X[:, b0:b0 + nb] = pts.view(nb, 2, 2, 2, H, W, 3)[:, :, 0].reshape(
+                nb, 4, H, W, 3).transpose(0, 1)
+            C[:, b0:b0 + nb] = conf.view(nb, 2, 2, 2, H, W)[:, :, 0].reshape(
+                nb, 4, H, W).transpose(0, 1)
+            D[:, b0:b0 + nb] = d32.view(nb, 4, H, W, 24).transpose(0, 1)
+            D16[:, b0:b0 + nb] = d16.view(nb, 4, H, W, 24).transpose(0, 1)
+            Q[:, b0:b0 + nb] = dq.view(nb, 4, H, W).transpose(0, 1)
+        return dict(X=X, C=C, D=D, D16=D16, Q=Q)
 
 
 def build(device, seed_monst3r=0, seed_mast3r=1, small=False):

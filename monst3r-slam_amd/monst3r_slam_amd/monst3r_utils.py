@@ -1,0 +1,359 @@
+"""Model-level drop-in of mast3r_slam/monst3r_utils.py (and the frame helpers of
+mast3r_slam/frame.py) on the MI355X pair model.
+
+Same function names, argument order and return conventions as the reference, so the SLAM
+glue (tracker2.py, global_opt2.py, main_monster_slam.py) reads the same:
+
+  load_mast3r / load_monst3r              monst3r_utils.py:36-52
+  monst3r_asymmetric_inference            :255-297   (frame i vs keyframe j)
+  monst3r_match_asymmetric                :483-508   (+ matching.match)
+  monst3r_symmetric_inference             :95-138
+  monst3r_decode_symmetric_batch          :141-184   (true batching: chunked problem sets)
+  monst3r_match_symmetric                 :214-252
+  monst3r_inference_mono                  :187-211
+  apply_dynamic_mask_to_pointmaps         :300-341   (HIP kernel m3s_apply_dynamic_mask)
+  dynamic_mask_from_flow                  :625-637   (the mask arithmetic of get_dynamic_mask;
+                                                      RAFT / ego-flow / SAM2 are absent code)
+  resize_img / create_frame / Frame       monst3r_utils.py:739-782, frame.py:14-141
+
+Model handles: the reference keeps two nn.Modules; here both weight sets live in ONE
+PairModel (both decoders and all heads run as one batched problem set), so
+`load_monst3r` and `load_mast3r` return handles onto a shared model, built when the pair
+is first used.  Weights: `path=None` → seeded random weights with the reference's
+parameter names (no checkpoints offline); a path → the reference checkpoint format
+({"model": state_dict}) read with torch.load(weights_only=True).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import matching
+from . import model as Mdl
+from . import weights as Wt
+from .config import config
+
+# ---------------------------------------------------------------------------------------
+# model handles
+# ---------------------------------------------------------------------------------------
+_REGISTRY: dict = {}   # device str → {"monst3r": handle, "mast3r": handle}
+
+
+class ModelHandle:
+    """Stands for the reference's AsymmetricCroCo3DStereo (MonST3R) or AsymmetricMASt3R."""
+
+    def __init__(self, kind, state_dict, arch, device):
+        self.kind, self.sd, self.arch, self.device = kind, state_dict, arch, torch.device(device)
+        self._pair_model = None
+
+    def share_memory(self):        # main_monster_slam.py:206-207 (single process here)
+        return self
+
+    def pair_model(self) -> Mdl.PairModel:
+        reg = _REGISTRY.get(str(self.device), {})
+        mon, mas = reg.get("monst3r"), reg.get("mast3r")
+        if mon is None or mas is None:
+            raise RuntimeError("load_monst3r() and load_mast3r() must both be called on this "
+                               "device: the MI355X pair model batches both decoders")
+        if mon._pair_model is None:
+            pm = Mdl.PairModel(Mdl.PackedWeights(mon.sd, mon.arch, mas.sd, mas.arch,
+                                                 self.device), self.device)
+            mon._pair_model = mas._pair_model = pm
+        return mon._pair_model
+
+
+def _load_state_dict(path, arch, seed):
+    if path is None:
+        return Wt.make_state_dict(arch, seed)
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    sd = ck["model"] if isinstance(ck, dict) and "model" in ck else ck
+    missing = set(Wt.param_shapes(arch)) - set(sd)
+    if missing:
+        raise RuntimeError(f"checkpoint {path} lacks {len(missing)} parameters, e.g. "
+                           f"{sorted(missing)[:3]}")
+    return {k: sd[k].float() for k in Wt.param_shapes(arch)}
+
+
+def load_monst3r(path=None, device="cuda", arch=None):
+    """monst3r_utils.py:46-52 (MonST3R_PO-TA-S-W_ViTLarge_BaseDecoder_512_dpt).
+    `arch` (not in the reference) selects a reduced-width variant for tests."""
+    a = arch or Wt.MONST3R
+    h = ModelHandle("monst3r", _load_state_dict(path, a, 0), a, device)
+    _REGISTRY.setdefault(str(h.device), {})["monst3r"] = h
+    return h
+
+
+def load_mast3r(path=None, device="cuda", arch=None):
+    """monst3r_utils.py:36-43 (MASt3R_ViTLarge_BaseDecoder_512_catmlpdpt_metric)."""
+    a = arch or Wt.MAST3R
+    h = ModelHandle("mast3r", _load_state_dict(path, a, 1), a, device)
+    _REGISTRY.setdefault(str(h.device), {})["mast3r"] = h
+    return h
+
+
+# ---------------------------------------------------------------------------------------
+# frames (frame.py:14-141) and image preprocessing (monst3r_utils.py:739-782)
+# ---------------------------------------------------------------------------------------
+@dataclasses.dataclass
+class Frame:
+    """frame.py:14-50.  T_WC is the lietorch Sim3 data tensor [1,8] (t, q xyzw, s)."""
+    frame_id: int
+    img: torch.Tensor                 # [1,3,H,W] f32 in [-1,1]
+    img_shape: torch.Tensor           # [1,2] int
+    img_true_shape: torch.Tensor      # [1,2] int
+    uimg: torch.Tensor                # [H,W,3] f32 in [0,1] (host)
+    T_WC: Optional[torch.Tensor] = None
+    X_canon: Optional[torch.Tensor] = None
+    C: Optional[torch.Tensor] = None
+    feat: Optional[torch.Tensor] = None   # [1,S,1024] bf16 (MonST3R encoder)
+    pos: Optional[torch.Tensor] = None    # [1,S,2] int64
+    N: int = 0
+    N_updates: int = 0
+    K: Optional[torch.Tensor] = None
+    dynamic_mask: Optional[torch.Tensor] = None
+
+    def update_pointmap(self, X, C):
+        """frame.py:60-124, 'weighted_pointmap' (base.yaml:39) and the other modes that
+        need no host statistics."""
+        mode = config["tracking"]["filtering_mode"]
+        if self.N == 0:
+            self.X_canon, self.C, self.N, self.N_updates = X.clone(), C.clone(), 1, 1
+            return
+        if mode == "weighted_pointmap":
+            self.X_canon = (self.C * self.X_canon + C * X) / (self.C + C)
+            self.C = self.C + C
+            self.N += 1
+        elif mode == "recent":
+            self.X_canon, self.C, self.N = X.clone(), C.clone(), 1
+        elif mode == "first":
+            if self.N_updates == 1:
+                self.X_canon, self.C, self.N = X.clone(), C.clone(), 1
+        elif mode == "indep_conf":
+            m = C > self.C
+            self.X_canon[m.repeat(1, 3)] = X[m.repeat(1, 3)]
+            self.C[m] = C[m]
+            self.N = 1
+        else:
+            raise NotImplementedError(f"filtering_mode {mode}")
+        self.N_updates += 1
+
+    def get_average_conf(self):
+        return self.C / self.N if self.C is not None else None
+
+
+def _resize_pil_image(img, long_edge_size):
+    import PIL.Image
+    S = max(img.size)
+    interp = PIL.Image.LANCZOS if S > long_edge_size else PIL.Image.BICUBIC
+    new_size = tuple(int(round(x * long_edge_size / S)) for x in img.size)
+    return img.resize(new_size, interp)
+
+
+def img_norm(pil_img):
+    """dust3r ImgNorm = ToTensor + Normalize((0.5,)*3, (0.5,)*3) (d3r/utils/image.py:23)."""
+    a = np.asarray(pil_img, dtype=np.float32) / 255.0
+    return torch.from_numpy(((a - 0.5) / 0.5).transpose(2, 0, 1).copy())
+
+
+def resize_img(img, size, square_ok=False, return_transformation=False):
+    """monst3r_utils.py:749-782: long side → 512 (LANCZOS when shrinking, BICUBIC else)
+    or short side → 224, then a centre crop to a multiple of 16 (4:3 for square inputs)."""
+    import PIL.Image
+    assert size == 224 or size == 512
+    img = PIL.Image.fromarray(np.uint8(img * 255))
+    W1, H1 = img.size
+    if size == 224:
+        img = _resize_pil_image(img, round(size * max(W1 / H1, H1 / W1)))
+    else:
+        img = _resize_pil_image(img, size)
+    W, H = img.size
+    cx, cy = W // 2, H // 2
+    if size == 224:
+        half = min(cx, cy)
+        img = img.crop((cx - half, cy - half, cx + half, cy + half))
+    else:
+        halfw, halfh = ((2 * cx) // 16) * 8, ((2 * cy) // 16) * 8
+        if not square_ok and W == H:
+            halfh = 3 * halfw / 4
+        img = img.crop((cx - halfw, cy - halfh, cx + halfw, cy + halfh))
+    res = dict(img=img_norm(img)[None], true_shape=np.int32([img.size[::-1]]),
+               unnormalized_img=np.asarray(img))
+    if return_transformation:
+        return res, (W1 / W, H1 / H, (W - img.size[0]) / 2, (H - img.size[1]) / 2)
+    return res
+
+
+def create_frame(i, img, T_WC, K=None, img_size=512, device="cuda:0"):
+    """frame.py:130-141.  T_WC: Sim3 data [1,8] (or [8])."""
+    r = resize_img(img, img_size)
+    rgb = r["img"].to(device=device)
+    img_shape = torch.tensor(r["true_shape"], device=device)
+    img_true_shape = img_shape.clone()
+    uimg = torch.from_numpy(r["unnormalized_img"].copy()) / 255.0
+    ds = config["dataset"]["img_downsample"]
+    if ds > 1:
+        uimg = uimg[::ds, ::ds]
+        img_shape = img_shape // ds
+    T = torch.as_tensor(T_WC, dtype=torch.float32, device=device).reshape(1, 8)
+    return Frame(i, rgb, img_shape, img_true_shape, uimg, T, K=K)
+
+
+# ---------------------------------------------------------------------------------------
+# inference
+# ---------------------------------------------------------------------------------------
+def _hw(frame_or_shape):
+    s = frame_or_shape.img_true_shape if hasattr(frame_or_shape, "img_true_shape") \
+        else frame_or_shape
+    s = torch.as_tensor(s).reshape(-1)
+    return int(s[0]), int(s[1])
+
+
+def _ensure_feat(pm, frame):
+    """Encode with MonST3R's encoder once and cache on the frame (monst3r_utils.py:262-269)."""
+    if frame.feat is None:
+        feat, pos = pm.encode(frame.img)
+        frame.feat, frame.pos = feat.clone(), pos.clone()
+    return frame.feat
+
+
+def _downsample(*ts):
+    """mast3r_downsample (monst3r_utils.py:82-91): [..., ::d, ::d(, :)]."""
+    d = config["dataset"]["img_downsample"]
+    if d <= 1:
+        return ts
+    out = []
+    for t in ts:
+        out.append(t[..., ::d, ::d, :].contiguous() if t.dim() >= 4 and t.shape[-1] in (3, 24)
+                   else t[..., ::d, ::d].contiguous())
+    return tuple(out)
+
+
+@torch.inference_mode()
+def monst3r_asymmetric_inference(mast3r, monst3r, frame_i, frame_j):
+    """:255-297 → X, C (MonST3R heads) and D, Q (MASt3R heads), each [2,H,W(,c)]
+    (index 0 = ii, 1 = ji); both decoders consume MonST3R encoder features."""
+    pm = monst3r.pair_model()
+    _ensure_feat(pm, frame_i)
+    fj = _ensure_feat(pm, frame_j)
+    H, W = _hw(frame_i)
+    gh, gw = H // pm.a.patch, W // pm.a.patch
+    hooks = pm.decode(frame_i.feat.reshape(-1, pm.a.enc_dim), fj.reshape(-1, pm.a.enc_dim),
+                      None, gh, gw)
+    pts, conf, _, desc, dconf = pm.heads(hooks, gh, gw, H, W)
+    return _downsample(pts[0:2].clone(), conf[0:2].clone(), desc.clone(), dconf.clone())
+
+
+def _rearrange_pair(X, C, D, Q):
+    b = X.shape[0] // 2
+    Xs = X.reshape(2, b, -1, 3)
+    Cs = C.reshape(2, b, -1, 1)
+    Ds = D.reshape(2, b, -1, D.shape[-1])
+    Qs = Q.reshape(2, b, -1, 1)
+    return Xs, Cs, Ds, Qs
+
+
+def monst3r_match_asymmetric(mast3r, monst3r, frame_i, frame_j, idx_i2j_init=None):
+    """:483-508 → (idx_i2j, valid_match_j, Xii, Cii, Qii, Xji, Cji, Qji)."""
+    X, C, D, Q = monst3r_asymmetric_inference(mast3r, monst3r, frame_i, frame_j)
+    b = X.shape[0] // 2
+    idx_i2j, valid_match_j = matching.match(X[:b], X[b:], D[:b], D[b:],
+                                            idx_1_to_2_init=idx_i2j_init)
+    Xs, Cs, _, Qs = _rearrange_pair(X, C, D, Q)
+    return idx_i2j, valid_match_j, Xs[0], Cs[0], Qs[0], Xs[1], Cs[1], Qs[1]
+
+
+@torch.inference_mode()
+def monst3r_symmetric_inference(mast3r, monst3r, frame_i, frame_j):
+    """:95-138 → X, C, D, Q [4,H,W(,c)] in the order (ii, ji, jj, ij)."""
+    pm = monst3r.pair_model()
+    fi, fj = _ensure_feat(pm, frame_i), _ensure_feat(pm, frame_j)
+    H, W = _hw(frame_i)
+    out = pm.symmetric(fi, fj, H, W)
+    return _downsample(out["X"][:, 0], out["C"][:, 0], out["D"][:, 0], out["Q"][:, 0])
+
+
+@torch.inference_mode()
+def monst3r_decode_symmetric_batch(mast3r, monst3r, feat_i, pos_i, feat_j, pos_j, shape_i,
+                                   shape_j, chunk=4):
+    """:141-184 ("Assumes img shape the same") → X, C, D, Q [4,B,H,W(,c)].  The reference
+    loops over b; here `chunk` pairs = 8·chunk decoder/head problems share every launch."""
+    pm = monst3r.pair_model()
+    H, W = _hw(shape_i[0])
+    out = pm.symmetric(feat_i.to(Mdl.BF16), feat_j.to(Mdl.BF16), H, W, chunk=chunk)
+    return _downsample(out["X"], out["C"], out["D"], out["Q"])
+
+
+def monst3r_match_symmetric(mast3r, monst3r, feat_i, pos_i, feat_j, pos_j, shape_i, shape_j):
+    """:214-252 → (idx_i2j, idx_j2i, valid_match_j, valid_match_i, Qii, Qjj, Qji, Qij).
+    (global_opt2.py:54 omits `mast3r` — SURVEY §0.6a; here it is required, as in
+    global_opt.py:49-50.)"""
+    X, C, D, Q = monst3r_decode_symmetric_batch(mast3r, monst3r, feat_i, pos_i, feat_j,
+                                                pos_j, shape_i, shape_j)
+    b = X.shape[1]
+    X11 = torch.cat((X[0], X[2]), 0)
+    X21 = torch.cat((X[1], X[3]), 0)
+    D11 = torch.cat((D[0], D[2]), 0)
+    D21 = torch.cat((D[1], D[3]), 0)
+    idx_1_to_2, valid_match_2 = matching.match(X11, X21, D11, D21)
+    idx_i2j, idx_j2i = idx_1_to_2[:b], idx_1_to_2[b:]
+    valid_match_j, valid_match_i = valid_match_2[:b], valid_match_2[b:]
+    return (idx_i2j, idx_j2i, valid_match_j, valid_match_i, Q[0].reshape(b, -1, 1),
+            Q[2].reshape(b, -1, 1), Q[1].reshape(b, -1, 1), Q[3].reshape(b, -1, 1))
+
+
+@torch.inference_mode()
+def monst3r_inference_mono(monst3r, frame):
+    """:187-211 → (Xii [1,N,3], Cii [1,N,1])."""
+    pm = monst3r.pair_model()
+    f = _ensure_feat(pm, frame)
+    H, W = _hw(frame)
+    X, C = pm.mono(f, H, W)
+    X, C = _downsample(X.clone(), C.clone())
+    return X[0:1].reshape(1, -1, 3), C[0:1].reshape(1, -1, 1)
+
+
+# ---------------------------------------------------------------------------------------
+# dynamic mask (monst3r_utils.py:300-341, 625-637)
+# ---------------------------------------------------------------------------------------
+def dynamic_mask_from_flow(flow_ij, ego_flow_ij, threshold=0.35):
+    """The mask arithmetic of get_dynamic_mask (:625-637): err = |flow - ego_flow[:2]|,
+    min-max normalised, > threshold.  flow f32 [2,H,W], ego [>=2,H,W] → bool [H,W].
+    (RAFT optical flow, DepthBasedWarping ego-flow and SAM2 refinement are absent from the
+    reference checkout: their parity is unpinned; the inputs here come from the caller.)"""
+    _lib.require_cuda(flow_ij, ego_flow_ij, names=("flow_ij", "ego_flow_ij"))
+    f = flow_ij.float().contiguous()
+    e = ego_flow_ij[:2].float().contiguous()
+    H, W = f.shape[-2:]
+    mask = torch.empty((H, W), dtype=torch.uint8, device=f.device)
+    ws = torch.empty((H * W + 64,), dtype=torch.float32, device=f.device)
+    _lib.check(_lib.load().m3s_flow_error_mask(_lib.ptr(f), _lib.ptr(e), H * W,
+                                               float(threshold), _lib.ptr(mask), _lib.ptr(ws),
+                                               _lib.stream(f.device)), "flow_error_mask")
+    return mask.bool()
+
+
+def apply_dynamic_mask_to_pointmaps(X, C, dynamic_mask, D=None, Q=None,
+                                    mask_confidence_value=0.0, zero_descriptors=True):
+    """:300-341: C (and Q) := value and D := 0 where the mask is set; X unchanged.
+    X [b,h,w,3], C [b,h,w], D [b,h,w,F], Q [b,h,w], mask bool [h,w].  Returns new tensors
+    (the reference clones); the fill is one fused HIP pass."""
+    if dynamic_mask is None:
+        return X, C, D, Q
+    _lib.require_cuda(C, dynamic_mask, names=("C", "dynamic_mask"))
+    Cm = C.float().contiguous().clone()
+    Qm = None if Q is None else Q.float().contiguous().clone()
+    Dm = None if D is None else D.contiguous().clone()
+    b = Cm.shape[0]
+    hw = Cm[0].numel()
+    m = dynamic_mask.reshape(-1).to(torch.uint8).contiguous()
+    fdim = 0 if Dm is None else Dm.shape[-1]
+    is16 = int(Dm is not None and Dm.dtype == torch.float16)
+    _lib.check(_lib.load().m3s_apply_dynamic_mask(
+        _lib.ptr(m), _lib.ptr(Cm), _lib.ptr(Qm), _lib.ptr(Dm), is16, b, hw, fdim,
+        float(mask_confidence_value), int(bool(zero_descriptors)), _lib.stream(C.device)),
+        "apply_dynamic_mask")
+    return X, Cm, Dm, Qm

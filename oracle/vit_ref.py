@@ -219,3 +219,38 @@ def asymmetric_inference(sd_monst3r, a_monst3r, sd_mast3r, a_mast3r, img_i, img_
     D = torch.stack([m11["desc"][0], m21["desc"][0]])
     Q = torch.stack([m11["desc_conf"][0], m21["desc_conf"][0]])
     return X, C, D, Q, (fi, pi), (fj, pj)
+
+
+@torch.no_grad()
+def decode_symmetric_batch(sd_monst3r, a_monst3r, sd_mast3r, a_mast3r, feat_i, pos_i, feat_j,
+                           pos_j, H, W):
+    """monst3r_utils.monst3r_decode_symmetric_batch (:141-184): per pair b, the MASt3R and
+    MonST3R decoders on (i, j) and (j, i); returns X, C (MonST3R) and D, Q (MASt3R), each
+    stacked [4, B, ...] in the order (ii, ji, jj, ij) (:155-183)."""
+    X, C, D, Q = [], [], [], []
+    for b in range(feat_i.shape[0]):
+        f1, f2 = feat_i[b][None], feat_j[b][None]
+        p1, p2 = pos_i[b][None], pos_j[b][None]
+        res = []
+        for (fa, pa, fb, pb) in ((f1, p1, f2, p2), (f2, p2, f1, p1)):
+            e1, e2 = decoder(sd_mast3r, a_mast3r, fa, pa, fb, pb)
+            res += [head(sd_mast3r, a_mast3r, 1, e1, H, W), head(sd_mast3r, a_mast3r, 2, e2, H, W)]
+        D.append(torch.stack([r["desc"][0] for r in res]))
+        Q.append(torch.stack([r["desc_conf"][0] for r in res]))
+        res = []
+        for (fa, pa, fb, pb) in ((f1, p1, f2, p2), (f2, p2, f1, p1)):
+            d1, d2 = decoder(sd_monst3r, a_monst3r, fa, pa, fb, pb)
+            res += [head(sd_monst3r, a_monst3r, 1, d1, H, W),
+                    head(sd_monst3r, a_monst3r, 2, d2, H, W)]
+        X.append(torch.stack([r["pts3d"][0] for r in res]))
+        C.append(torch.stack([r["conf"][0] for r in res]))
+    return (torch.stack(X, 1), torch.stack(C, 1), torch.stack(D, 1), torch.stack(Q, 1))
+
+
+@torch.no_grad()
+def inference_mono(sd_monst3r, a_monst3r, feat, pos, H, W):
+    """monst3r_utils.monst3r_inference_mono (:187-211): self-pair MonST3R decode →
+    Xii [1,N,3], Cii [1,N,1]."""
+    d1, d2 = decoder(sd_monst3r, a_monst3r, feat, pos, feat, pos)
+    r11 = head(sd_monst3r, a_monst3r, 1, d1, H, W)
+    return r11["pts3d"].reshape(1, -1, 3), r11["conf"].reshape(1, -1, 1)
