@@ -12,7 +12,14 @@ The step is captured once in a HIP graph and replayed (no host work per frame).
 Multi-GPU: tracking is sequential per sequence → one independent replica per rank
 ("replicas only"); value = frames of all ranks / max rank time.
 
+Also measured at every N (field "keyframe_graph", configs[3]): 16 keyframes,
+64 pairs re-inferred symmetrically (4 directed decodes + 8 heads each) and matched both ways,
+edges sharded round-robin over the ranks with one RCCL all-gather of the per-edge records,
+keyframe encoding sharded likewise, then the factor-graph acceptance and the GPU GN solve
+(identical on every rank).  value = pairs/s of the whole job (max-over-ranks time).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--eager]
+                       [--no-graph] [--graph-steps K]
 """
 from __future__ import annotations
 
@@ -42,6 +49,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (debug)")
+    ap.add_argument("--no-graph", action="store_true", help="skip the keyframe-graph (C4) leg")
+    ap.add_argument("--graph-steps", type=int, default=2)
     return ap.parse_args()
 
 
@@ -98,6 +107,85 @@ def gemm_roofline(model, img, feat_k, dev):
     return dict(launches=len(probe), gemm_ms=t_ms, gemm_flops=flops,
                 avg_launch_us=t_ms / len(probe) * 1e3,
                 tflops=flops / (t_ms * 1e-3) / 1e12)
+
+
+class _Bound:
+    """Model handle (monst3r_utils.ModelHandle interface) over the bench's PairModel."""
+
+    def __init__(self, pm):
+        self._pm = pm
+
+    def pair_model(self):
+        return self._pm
+
+
+def graph_pairs(n_kf=16, n_pairs=64):
+    """Consecutive edges first, then 'retrieval-like' strides, until n_pairs."""
+    ii, jj = [], []
+    for d in (1, 2, 3, 4, 8, 5, 6, 7):
+        for k in range(n_kf - d):
+            if len(ii) < n_pairs:
+                ii.append(k)
+                jj.append(k + d)
+    return ii, jj
+
+
+def keyframe_graph_bench(model, dev, world, steps, warmup=1):
+    """configs[3]: sharded 64-pair symmetric re-inference + matching + GN over 16 keyframes."""
+    import numpy as np
+    from monst3r_slam_amd import global_opt as GO
+    from monst3r_slam_amd import parallel as P
+    from monst3r_slam_amd import synthetic as syn
+    n_kf = 16
+    ii, jj = graph_pairs(n_kf, 64)
+    sc = syn.keyframe_graph(P=n_kf, h=H, w=W, seed=3)
+    g = torch.Generator(device=dev).manual_seed(7)     # same images on every rank
+    imgs = torch.rand(n_kf, 1, 3, H, W, device=dev, generator=g) * 2 - 1
+    frames = GO.Keyframes(H, W, buffer=n_kf, device=dev)
+    frames.img[:n_kf] = imgs
+    frames.X[:n_kf] = torch.from_numpy(sc["Xs"]).to(dev)
+    frames.C[:n_kf] = torch.from_numpy(sc["Cs"]).to(dev)
+    frames.N[:n_kf] = 1
+    frames.img_true_shape[:n_kf] = torch.tensor([[H, W]], dtype=torch.int32, device=dev)
+    frames.n_size = n_kf
+    T0 = torch.from_numpy(sc["Twc"]).to(dev).reshape(n_kf, 1, 8)
+    h = _Bound(model)
+    group = None
+
+    def step():
+        frames.T_WC[:n_kf] = T0
+        P.shard_keyframe_features(frames, range(n_kf), model.encode, group)
+        graph = P.ShardedFactorGraph(h, h, frames, device=dev, group=group)
+        graph.add_factors(ii, jj, min_match_frac=0.0)
+        graph.solve_GN_rays()
+        return graph
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        graph = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    n = H * W
+    del np
+    return {"workload": "configs[3]: 16 keyframes, 64 pairs symmetric re-inference (MonST3R+"
+                        "MASt3R, 4 decodes + 8 heads each) + 128 directed matches + GN rays",
+            "pairs_per_s": len(ii) * steps / el, "ms_per_graph": el / steps * 1e3,
+            "steps": steps, "edges_accepted": int(graph.ii.numel()),
+            "gflop_per_pair": 3603.6, "tflops_achieved": len(ii) * 3603.6e9 * steps / el / 1e12,
+            "allgather_bytes_per_rank": int(-(-len(ii) // world) * P.record_bytes(n)),
+            "sharding": f"edges round-robin over {world} rank(s), RCCL all-gather"}
 
 
 def cpu_baseline():
@@ -215,6 +303,11 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline()
+    if not args.no_graph:
+        kg = keyframe_graph_bench(model, dev, world, args.graph_steps)
+        if rank == 0:
+            line["keyframe_graph"] = kg
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
