@@ -11,6 +11,7 @@
 //   the lanes), so the online-softmax max / sum per query are lane-local (+ one xor-32
 //   exchange).  P^T stays in registers as the B operand of O^T = V^T P^T; V^T fragments
 //   come from the V tile via ds_read_b64_tr_b16 (hardware transpose).
+#include <stdlib.h>
 #include "vit_common.h"
 
 namespace {
@@ -109,18 +110,20 @@ __device__ __forceinline__ s16x4 tr_read(const char* p) {
 __device__ __forceinline__ int k_swz(int r) { return (r >> 1) & 7; }
 __device__ __forceinline__ int v_swz(int r) { return ((r >> 1) & 1) * 4; }
 
-constexpr int AW = 4;                      // waves per block, QT query rows each
 constexpr int AKT = 64;                    // keys per tile
 constexpr int ASTAGES = 3;                 // DMA ring depth
 constexpr int TILE_BYTES = AKT * HD * 2;   // 8 KiB
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;
-constexpr int ACH = TILE_BYTES / 16 / (AW * 64);  // DMA chunks per thread per operand (2)
 constexpr uint32_t OOB = 0x80000000u;
 
+// AW waves per block (QT query rows each) share one K/V ring: AW = 4 when the grid has
+// blocks to spare, fewer when (S / 128) x heads x batch would leave CUs idle.
+template <int AW>
 __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, bf16_t* __restrict__ o,
     int64_t ldo, int64_t so_b, int Sq, int Sk, float c_log2) {
+  constexpr int ACH = TILE_BYTES / 16 / (AW * 64);  // DMA chunks per thread per operand
   __shared__ __attribute__((aligned(16))) char lds[ASTAGES * STAGE_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -338,12 +341,25 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   if (sk * ld_kv * 2 >= 0x7ffffff0) return M3S_ERR_TOO_LARGE;  // 31-bit buffer offsets
   if (((uintptr_t)d_o) % 8 || ld_o % 4 || stride_o % 4) return M3S_ERR_INVALID_ARG;
   const float c_log2 = 0.125f * 1.4426950408889634f;  // head_dim^-0.5 * log2(e)
-  dim3 grid(m3s_div_up(sq, AW * QT), (unsigned)heads, (unsigned)batch);
-  hipLaunchKernelGGL(attn_kernel, grid, dim3(AW * 64), 0, m3s_stream(stream),
-                     reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,
-                     reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v),
-                     ld_kv, stride_kv, reinterpret_cast<bf16_t*>(d_o), ld_o, stride_o, (int)sq,
-                     (int)sk, c_log2);
+  // waves per block: fill the 256 CUs first (the encoder's 16 heads x 6 query tiles of
+  // 128 rows would occupy only 96 CUs), else share each K/V tile among 4 waves
+  int aw = 4;
+  const int64_t hb = heads * batch;
+  // (AW = 1 is not offered: a 1-wave block holds a 48 KiB ring, so 3 blocks/CU = 3 waves
+  // would leave a SIMD idle)
+  while (aw > 2 && (int64_t)m3s_div_up(sq, aw * QT) * hb < 512) aw >>= 1;
+  if (const char* e = getenv("M3S_ATTN_AW")) aw = atoi(e) == 4 ? 4 : 2;  // tuning override
+  hipStream_t s = m3s_stream(stream);
+#define M3S_ATTN_LAUNCH(AWV)                                                                 \
+  hipLaunchKernelGGL(attn_kernel<AWV>, dim3(m3s_div_up(sq, AWV * QT), (unsigned)heads,      \
+                     (unsigned)batch), dim3(AWV * 64), 0, s,                                 \
+                     reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,                   \
+                     reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
+                     ld_kv, stride_kv, reinterpret_cast<bf16_t*>(d_o), ld_o, stride_o, (int)sq, \
+                     (int)sk, c_log2)
+  if (aw == 2) M3S_ATTN_LAUNCH(2);
+  else M3S_ATTN_LAUNCH(4);
+#undef M3S_ATTN_LAUNCH
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }

@@ -388,49 +388,83 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
   long long s_wait = 0, s_bar = 0, s_comp = 0;
 #endif
 
-  for (int kt = 0; kt < nk; kt++) {
-    M3S_T(t0);
-    // retire tile kt (leave the younger tiles in flight), then make it visible to all waves
-    const int ahead = min(nk - 1 - kt, STAGES - 2);
+  // K loop.  Fragments are double-buffered in registers: a phase (16 of the K-tile's BK)
+  // issues the LDS reads of the NEXT phase, its share of the DMA of tile kt+STAGES-1, then
+  // its MFMAs; the last phase issues its MFMAs first, then retires tile kt+1 (counted
+  // vmcnt + barrier: the MFMAs keep the matrix pipe busy meanwhile) and reads tile kt+1's
+  // first fragments.  The steady-state loop (every tile prefetches) is branch-free, so the
+  // scheduler sees whole phases; sched_group_barrier pins the read / DMA / MFMA order.
+  constexpr int KK = BK / 16;
+  constexpr int NR = TM + TN;                 // ds_read_b128 per phase
+  constexpr int NM = TM * TN;                 // MFMAs per phase
+  bf16x8 fa[2][TM], fb[2][TN];
+  auto read_frags = [&](int buf, const char* sA, int kk) {
+    const char* sB = sA + C::A_BYTES;
+    const int slot = ((kk * 2 + fh) ^ fsw) * 16;
+#pragma unroll
+    for (int i = 0; i < TM; i++) {
+      fa[buf][i] = *reinterpret_cast<const bf16x8*>(
+          sA + (wm * (BM / WM) + i * 32 + fr) * (BK * 2) + slot);
+      if (MODE == 2) fa[buf][i] = relu_frag(fa[buf][i]);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; j++)
+      fb[buf][j] = *reinterpret_cast<const bf16x8*>(
+          sB + (wn * (BN / WN) + j * 32 + fr) * (BK * 2) + slot);
+  };
+  auto mfmas = [&](int cur) {
+#pragma unroll
+    for (int i = 0; i < TM; i++)
+#pragma unroll
+      for (int j = 0; j < TN; j++)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][i], fb[cur][j], acc[i][j],
+                                                            0, 0, 0);
+  };
+  auto stage_of = [&](int t) { return lds + (t % STAGES) * C::ST_BYTES; };
+  if (nk > 0) {
+    const int ahead = min(nk - 1, STAGES - 2);
     if (STAGES >= 4 && ahead >= 2) vm_wait<C::L * 2>();
     else if (ahead >= 1) vm_wait<C::L>();
     else vm_wait<0>();
-    M3S_T(t1);
     block_sync_lds();
+    read_frags(0, lds, 0);
+  }
+
+  const int nsteady = nk - (STAGES - 1);      // kt < nsteady: tile kt+STAGES-1 exists
+  int kt = 0;
+  for (; kt < nsteady; kt++) {
+    M3S_T(t0);
+    M3S_T(t1);
     M3S_T(t2);
-    // the DMA of tile kt+STAGES-1 is spread over the MFMA phases of this tile so its issue
-    // cost overlaps MFMA execution
-    const bool pre = kt + STAGES - 1 < nk;
     const int pk0 = (kbase + kt + STAGES - 1) * BK;
     char* psb = lds + ((kt + STAGES - 1) % STAGES) * C::ST_BYTES;
     int pky, pkx, pci0;
     tap_of(pk0, pky, pkx, pci0);
-    const char* sA = lds + (kt % STAGES) * C::ST_BYTES;
-    const char* sB = sA + C::A_BYTES;
+    const char* sA = stage_of(kt);
 #pragma unroll
-    for (int kk = 0; kk < BK / 16; kk++) {
-      const int slot = ((kk * 2 + fh) ^ fsw) * 16;
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; i++) {
-        af[i] = *reinterpret_cast<const bf16x8*>(
-            sA + (wm * (BM / WM) + i * 32 + fr) * (BK * 2) + slot);
-        if (MODE == 2) af[i] = relu_frag(af[i]);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; j++)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(
-            sB + (wn * (BN / WN) + j * 32 + fr) * (BK * 2) + slot);
-      if (pre) {
+    for (int kk = 0; kk < KK; kk++) {
+      const int cur = kk & 1;
+      if (kk + 1 < KK) {
+        read_frags(cur ^ 1, sA, kk + 1);
 #pragma unroll
         for (int j = 0; j < C::L; j++)
-          if (j * (BK / 16) / C::L == kk) issue_chunk(j, pk0, psb, pky, pkx, pci0);
+          if (j * KK / C::L == kk) issue_chunk(j, pk0, psb, pky, pkx, pci0);
+        mfmas(cur);
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < C::L; j++)
+          if (j * KK / C::L == kk) issue_chunk(j, pk0, psb, pky, pkx, pci0);
+        mfmas(cur);
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+        // retire tile kt+1: tiles kt+2 .. kt+STAGES-1 (STAGES-2 of them) stay in flight
+        if (STAGES >= 4) vm_wait<C::L * 2>();
+        else if (STAGES == 3) vm_wait<C::L>();
+        else vm_wait<0>();
+        block_sync_lds();
+        read_frags(cur ^ 1, stage_of(kt + 1), 0);
       }
-#pragma unroll
-      for (int i = 0; i < TM; i++)
-#pragma unroll
-        for (int j = 0; j < TN; j++)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
 #ifdef M3S_GEMM_STAMPS
     M3S_T(t3);
@@ -438,6 +472,27 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
     s_bar += t2 - t1;
     s_comp += t3 - t2;
 #endif
+  }
+  // tail: the last STAGES-1 tiles (nothing left to prefetch)
+  for (; kt < nk; kt++) {
+    const char* sA = stage_of(kt);
+#pragma unroll
+    for (int kk = 0; kk < KK; kk++) {
+      const int cur = kk & 1;
+      if (kk + 1 < KK) {
+        read_frags(cur ^ 1, sA, kk + 1);
+        mfmas(cur);
+      } else {
+        mfmas(cur);
+        if (kt + 1 < nk) {
+          if (STAGES >= 4 && nk - 2 - kt >= 2) vm_wait<C::L * 2>();
+          else if (STAGES >= 3 && nk - 2 - kt >= 1) vm_wait<C::L>();
+          else vm_wait<0>();
+          block_sync_lds();
+          read_frags(cur ^ 1, stage_of(kt + 1), 0);
+        }
+      }
+    }
   }
   M3S_T(t_loop);
 
@@ -691,7 +746,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
 // ---------------------------------------------------------------------------------------
 // tile configurations
 // ---------------------------------------------------------------------------------------
-enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6 };
+enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7 };
 
 // Epilogue flag sets compiled as straight-line variants (8-wide vector path), per mode:
 //   GEMM: bf16 out, +RoPE, +GELU, f32 residual → f32, f32 out;  conv: bf16 out, +bf16
@@ -849,19 +904,23 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   const int nk = (d->K + 63) / 64;
   int cfg = forced_tile();
   if (cfg == 0) {
-    if (conv) cfg = tiles128 >= 1536 ? T256 : T64;
-    else if (nk >= 32) cfg = T128;
+    // measured on the pair shapes (tools/gemm_tune.py): 2 x 128^2 blocks per CU win for
+    // wide convs with several waves of tiles, for one-to-two waves of short-K GEMM tiles,
+    // and for large square-ish GEMMs
+    if (conv) cfg = tiles128 < 1536 ? T64 : (d->N >= 256 ? T128O2 : T256);
+    else if (nk >= 32) cfg = tiles128 >= 1024 ? T128O2 : T128;
     else if (tiles128 < 64 || nk < 8 || (tiles128 > 512 && nk < 16)) cfg = T64;
+    else if (tiles128 >= 256 && tiles128 <= 512 && nk <= 16) cfg = T128O2;
     else cfg = T128;
   }
-  if (cfg != T128 && cfg != T64 && cfg != T128K32 && cfg != T256) cfg = T128;
+  if (cfg != T128 && cfg != T64 && cfg != T128K32 && cfg != T256 && cfg != T128O2) cfg = T128;
   if (conv && d->Cin % 64 != 0) cfg = T128K32;  // tap-uniform K-tiles need Cin % BK == 0
   if (!conv && cfg == T128K32) cfg = T128;
   if (conv && d->Cin % 64 == 0 && cfg == T128K32) cfg = T128;
   int splits = d->split_k;
   if (splits <= 0) {
     splits = 1;
-    if (cfg == T128)
+    if (cfg == T128 || cfg == T128O2)
       while (tiles128 * splits * 2 <= 256 && nk / (splits * 2) >= 8) splits *= 2;
   }
   const bool can_split = !conv && !(d->flags & M3S_EPI_CONVT) && d->workspace &&
@@ -871,6 +930,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     case T128: return launch<128, 128, 64, 2, 2, 3, 1>(a, d->batch, s);
     case T128K32: return launch<128, 128, 32, 2, 2, 4, 2>(a, d->batch, s);
     case T256: return launch<256, 128, 64, 2, 2, 3, 1>(a, d->batch, s);
+    case T128O2: return launch<128, 128, 64, 2, 2, 2, 2>(a, d->batch, s);
     default: return launch<64, 128, 64, 2, 2, 3, 2>(a, d->batch, s);
   }
 }

@@ -60,3 +60,17 @@ for name, M, N, K, b, tile, split in shapes:
           f"comp/step {(s[:, 3] / nk).mean():6.0f} epi {s[:, 4].mean():6.0f} total "
           f"{s[:, 6].mean():7.0f} | epi: prefetch {s[:, 8].mean():5.0f} sync1 {s[:, 9].mean():5.0f} "
           f"lds+sync2 {s[:, 10].mean():5.0f} out {s[:, 11].mean():5.0f}", flush=True)
+    # s_memtime is per XCD: spans only within one XCD's blocks (block b → XCD b % 8)
+    bid = torch.arange(stamps.view(-1, 12).shape[0])[stamps.view(-1, 12)[:, 6].cpu() > 0]
+    sp, sps = [], []
+    for x in range(8):
+        m = (bid % 8) == x
+        if m.any():
+            sx, ex = t0[m], t0[m] + s[m, 6]
+            sp.append(float(ex.max() - sx.min()))
+            sps.append(float((sx - sx.min()).quantile(0.9)))
+    ev = e0.elapsed_time(e1) * 1e3
+    print(f"          per-XCD span {sum(sp) / len(sp):8.0f} cyc (max {max(sp):8.0f}) → "
+          f"{max(sp) / ev:5.0f} cyc/us vs event {ev:6.1f} us | start p90 {sum(sps) / len(sps):6.0f}"
+          f" | block total p10 {s[:, 6].quantile(0.1):6.0f} p90 {s[:, 6].quantile(0.9):6.0f}",
+          flush=True)

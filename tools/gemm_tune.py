@@ -87,7 +87,7 @@ for name, M, N, K, b, kind in gemms:
     def fn_for(split, A=A, B=B, C=C, M=M, N=N, K=K, b=b, flags=flags, R=R, bias=bias):
         return lambda: ops.gemm(A, B, C, M, N, K, b, sA=M * K, sB=N * K, sC=M * N, bias=bias,
                                 sBias=N, R=R, sR=M * N, flags=flags, split_k=split)
-    cfgs = [(1, 1), (2, 1)] if quick else [(1, 1), (1, 2), (1, 4), (2, 1), (2, 2), (4, 1), (4, 2),
+    cfgs = [(1, 1), (2, 1), (7, 1), (7, 2)] if quick else [(1, 1), (1, 2), (1, 4), (2, 1), (2, 2), (4, 1), (4, 2),
                                            (5, 1), (5, 2), (6, 1), (6, 2), (6, 4)]
     run(f"{name} {M}x{N}x{K}x{b}", 2.0 * M * N * K * b, fn_for, cfgs,
         ref=lambda A=A, B=B: torch.bmm(A, B.transpose(1, 2)))
@@ -110,7 +110,7 @@ for name, H, W, cin, cout, b in convs:
     xn = x.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
     wn = w.reshape(cout, 3, 3, cin).permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
     run(f"conv {name} {H}x{W} {cin}->{cout} x{b}", 2.0 * Ho * Wo * cout * 9 * cin * b, fn_for,
-        [(1, 1), (2, 1), (3, 1), (4, 1), (5, 1), (6, 1)],
+        [(1, 1), (2, 1), (6, 1), (7, 1)] if quick else [(1, 1), (2, 1), (3, 1), (6, 1), (7, 1)],
         ref=lambda xn=xn, wn=wn, st=st: torch.nn.functional.conv2d(xn, wn, padding=1, stride=st))
 
 # attention (encoder: 1 x 16 heads, decoder: 4 x 12 heads; 768 tokens, head dim 64)
@@ -118,8 +118,15 @@ for name, b, heads in [("attn enc", 1, 16), ("attn dec x4", 4, 12)]:
     S, C = 768, heads * 64
     qkv = torch.randn(b, S, 3 * C, device=dev).bfloat16()
     o = torch.empty(b, S, C, device=dev, dtype=torch.bfloat16)
+    us_aw = {}
+    for aw in ("2", "4"):
+        os.environ["M3S_ATTN_AW"] = aw
+        us_aw[aw] = graph_us(lambda: ops.attn(qkv, 3 * C, S * 3 * C, qkv[:, :, C:], qkv[:, :, 2 * C:],
+                                              3 * C, S * 3 * C, o, C, S * C, b, heads, S, S))
+    del os.environ["M3S_ATTN_AW"]
     us = graph_us(lambda: ops.attn(qkv, 3 * C, S * 3 * C, qkv[:, :, C:], qkv[:, :, 2 * C:], 3 * C,
                                    S * 3 * C, o, C, S * C, b, heads, S, S))
+    print(f"{name} AW=2 {us_aw['2']:.1f}us AW=4 {us_aw['4']:.1f}us")
     qh = qkv.reshape(b, S, 3, heads, 64).permute(2, 0, 3, 1, 4).contiguous()
     ur = graph_us(lambda: torch.nn.functional.scaled_dot_product_attention(qh[0], qh[1], qh[2]))
     fl = 4.0 * S * S * 64 * heads * b
