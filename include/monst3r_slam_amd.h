@@ -232,12 +232,15 @@ int m3s_vit_rope(void* d_t, int64_t ld, int64_t stride, const int64_t* d_pos,
 /* Multi-head attention, head dim 64 (croco/blocks.py:81-112 self, :132-169 cross):
  * o = softmax(q k^T / 8) v.  q [B][Sq] rows of ld_q bf16 (head h at column h*64), k,v
  * [B][Sk] rows of ld_kv; RoPE already applied (m3s_vit_rope).  o bf16 [B][Sq][ld_o].
- * The pos/rope arguments are reserved (must be NULL/0). */
+ * The pos/rope arguments are reserved (must be NULL/0).  With a device workspace (16-B
+ * aligned, optional) a small (query tile x head x batch) grid is split along the keys
+ * (flash-decoding): per-split unnormalised O, max and sum in f32, merged by a second
+ * kernel; up to splits x B x heads x sq x 68 floats of workspace are used. */
 int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q, const void* d_k,
                       const void* d_v, int64_t ld_kv, int64_t stride_kv, const int64_t* d_qpos,
                       const int64_t* d_kpos, int64_t stride_pos, void* d_o, int64_t ld_o,
                       int64_t stride_o, int64_t batch, int64_t heads, int64_t sq, int64_t sk,
-                      float rope_base, void* stream);
+                      float rope_base, void* d_workspace, int64_t workspace_bytes, void* stream);
 
 /* Patch-embed im2col: img f32 NCHW [B][3][H][W] → bf16 [B][(H/16)(W/16)][3*16*16]
  * with K ordered (c, ky, kx) like the conv weight [1024][3][16][16]. */

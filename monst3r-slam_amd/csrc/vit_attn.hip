@@ -12,6 +12,8 @@
 //   exchange).  P^T stays in registers as the B operand of O^T = V^T P^T; V^T fragments
 //   come from the V tile via ds_read_b64_tr_b16 (hardware transpose).
 #include <stdlib.h>
+#include <algorithm>
+#include <type_traits>
 #include "vit_common.h"
 
 namespace {
@@ -115,6 +117,7 @@ constexpr int ASTAGES = 3;                 // DMA ring depth
 constexpr int TILE_BYTES = AKT * HD * 2;   // 8 KiB
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;
 constexpr uint32_t OOB = 0x80000000u;
+constexpr int PART_LD = HD + 4;            // split partial row: O[64], m, l, pad
 
 // AW waves per block (QT query rows each) share one K/V ring: AW = 4 when the grid has
 // blocks to spare, fewer when (S / 128) x heads x batch would leave CUs idle.
@@ -122,7 +125,8 @@ template <int AW>
 __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, bf16_t* __restrict__ o,
-    int64_t ldo, int64_t so_b, int Sq, int Sk, float c_log2) {
+    int64_t ldo, int64_t so_b, int Sq, int Sk, float c_log2, int splits, int tiles_per_split,
+    float* __restrict__ part) {
   constexpr int ACH = TILE_BYTES / 16 / (AW * 64);  // DMA chunks per thread per operand
   __shared__ __attribute__((aligned(16))) char lds[ASTAGES * STAGE_BYTES];
   const int tid = threadIdx.x;
@@ -131,7 +135,8 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
   const int r = lane & 31, hh = lane >> 5;
   const int q0 = blockIdx.x * (AW * QT) + wid * QT;
   const int h = blockIdx.y;
-  const int64_t b = blockIdx.z;
+  const int64_t b = blockIdx.z / splits;
+  const int sp = blockIdx.z - (int)b * splits;   // key split (flash-decoding style)
   const bf16_t* Q = q + b * sq_b + h * HD;
 
   // Q fragments (B operand of S^T = K Q^T): query q0 + r, d = 16 ks + 8 hh .. +7
@@ -162,8 +167,11 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
     k_off[i] = (uint32_t)(((int64_t)row * ldkv + (slot ^ k_swz(row)) * 8) * 2);
     v_off[i] = (uint32_t)(((int64_t)row * ldkv + (slot ^ v_swz(row)) * 8) * 2);
   }
-  const int nkt = (Sk + AKT - 1) / AKT;
-  auto issue = [&](int kt, int stage) {
+  const int nkt_all = (Sk + AKT - 1) / AKT;
+  const int kt0 = sp * tiles_per_split;
+  const int nkt = max(0, min(nkt_all - kt0, tiles_per_split));  // tiles of this split
+  auto issue = [&](int ktl, int stage) {
+    const int kt = kt0 + ktl;
     char* sb = lds + stage * STAGE_BYTES;
     const uint32_t t0 = (uint32_t)((int64_t)kt * AKT * ldkv * 2);
 #pragma unroll
@@ -187,12 +195,16 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
   for (int st = 0; st < ASTAGES - 1; st++)
     if (st < nkt) issue(st, st);
 
-  for (int kt = 0; kt < nkt; kt++) {
-    if (kt + 1 < nkt) vm_wait<2 * ACH>();
+  // one key tile; TAIL (the last, partial tile only) masks keys >= Sk — a separate
+  // instantiation, so full tiles carry no per-score masking code
+  auto tile = [&](int ktl, auto tail_tag) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
+    const int kt = kt0 + ktl;
+    if (ktl + 1 < nkt) vm_wait<2 * ACH>();
     else vm_wait<0>();
     block_sync_lds();
-    if (kt + ASTAGES - 1 < nkt) issue(kt + ASTAGES - 1, (kt + ASTAGES - 1) % ASTAGES);
-    const char* sK = lds + (kt % ASTAGES) * STAGE_BYTES;
+    if (ktl + ASTAGES - 1 < nkt) issue(ktl + ASTAGES - 1, (ktl + ASTAGES - 1) % ASTAGES);
+    const char* sK = lds + (ktl % ASTAGES) * STAGE_BYTES;
     const char* sV = sK + TILE_BYTES;
 
     // S^T (keys x queries), two 32-key halves
@@ -210,13 +222,12 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
       }
     }
     // online softmax over the tile's keys (accumulator rows), per query (lane)
-    const bool tail = (kt + 1) * AKT > Sk;
     float tmax = -INFINITY;
 #pragma unroll
     for (int hs = 0; hs < 2; hs++)
 #pragma unroll
       for (int i = 0; i < 16; i++) {
-        if (tail) {
+        if constexpr (TAIL) {
           const int key = kt * AKT + hs * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
           if (key >= Sk) s[hs][i] = -INFINITY;
         }
@@ -282,8 +293,25 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
       }
     }
 #undef M3S_VT
+  };
+  for (int ktl = 0; ktl < nkt; ktl++) {
+    if ((kt0 + ktl + 1) * AKT > Sk) tile(ktl, std::true_type{});
+    else tile(ktl, std::false_type{});
   }
   if (qrow >= Sq) return;
+  if (part) {  // split: unnormalised O, running max m and sum l → [split][b][h][q][68] f32
+    float* P = part + ((((int64_t)sp * (gridDim.z / splits) + b) * gridDim.y + h) * Sq + qrow) *
+                          PART_LD;
+#pragma unroll
+    for (int d = 0; d < 2; d++)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; g4++)
+        *reinterpret_cast<float4*>(P + d * 32 + 8 * g4 + 4 * hh) =
+            make_float4(oacc[d][4 * g4], oacc[d][4 * g4 + 1], oacc[d][4 * g4 + 2],
+                        oacc[d][4 * g4 + 3]);
+    if (hh == 0) *reinterpret_cast<float2*>(P + HD) = make_float2(m, l);
+    return;
+  }
   const float inv_l = 1.0f / l;
   bf16_t* O = o + b * so_b + (int64_t)qrow * ldo + h * HD;
 #pragma unroll
@@ -295,6 +323,40 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
       for (int j = 0; j < 4; j++) w[j] = f2bf(oacc[d][4 * g4 + j] * inv_l);
       *reinterpret_cast<bf16x4*>(O + d * 32 + 8 * g4 + 4 * hh) = w;
     }
+}
+
+// Merge the key splits: M = max m_s, O = sum_s O_s 2^((m_s - M) c) / sum_s l_s 2^((m_s - M) c).
+// One thread per (b, h, q, 8 head dims).
+__global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part,
+                                                           int splits, int64_t rows, int heads,
+                                                           int Sq, float c_log2,
+                                                           bf16_t* __restrict__ o, int64_t ldo,
+                                                           int64_t so_b) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows * 8) return;
+  const int64_t row = idx >> 3;       // (b, h, q)
+  const int d8 = (int)(idx & 7) * 8;
+  const int qi = (int)(row % Sq);
+  const int64_t bh = row / Sq;
+  const int h = (int)(bh % heads);
+  const int64_t b = bh / heads;
+  float M = -INFINITY;
+  for (int s = 0; s < splits; s++) M = fmaxf(M, part[((int64_t)s * rows + row) * PART_LD + HD]);
+  float L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < splits; s++) {
+    const float* P = part + ((int64_t)s * rows + row) * PART_LD;
+    const float w = __builtin_amdgcn_exp2f((P[HD] - M) * c_log2);
+    L += P[HD + 1] * w;
+    const float4 a0 = *reinterpret_cast<const float4*>(P + d8);
+    const float4 a1 = *reinterpret_cast<const float4*>(P + d8 + 4);
+    acc[0] += a0.x * w; acc[1] += a0.y * w; acc[2] += a0.z * w; acc[3] += a0.w * w;
+    acc[4] += a1.x * w; acc[5] += a1.y * w; acc[6] += a1.z * w; acc[7] += a1.w * w;
+  }
+  const float inv = 1.0f / L;
+  bf16x8 out;
+#pragma unroll
+  for (int j = 0; j < 8; j++) out[j] = f2bf(acc[j] * inv);
+  *reinterpret_cast<bf16x8*>(o + b * so_b + (int64_t)qi * ldo + h * HD + d8) = out;
 }
 
 }  // namespace
@@ -326,7 +388,7 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
                                  const int64_t* d_qpos, const int64_t* d_kpos, int64_t stride_pos,
                                  void* d_o, int64_t ld_o, int64_t stride_o, int64_t batch,
                                  int64_t heads, int64_t sq, int64_t sk, float rope_base,
-                                 void* stream) {
+                                 void* d_workspace, int64_t workspace_bytes, void* stream) {
   if (!d_q || !d_k || !d_v || !d_o || batch <= 0 || heads <= 0 || sq <= 0 || sk <= 0)
     return M3S_ERR_INVALID_ARG;
   if ((((uintptr_t)d_q) | ((uintptr_t)d_k) | ((uintptr_t)d_v)) % 16) return M3S_ERR_INVALID_ARG;
@@ -341,24 +403,40 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   if (sk * ld_kv * 2 >= 0x7ffffff0) return M3S_ERR_TOO_LARGE;  // 31-bit buffer offsets
   if (((uintptr_t)d_o) % 8 || ld_o % 4 || stride_o % 4) return M3S_ERR_INVALID_ARG;
   const float c_log2 = 0.125f * 1.4426950408889634f;  // head_dim^-0.5 * log2(e)
-  // waves per block: fill the 256 CUs first (the encoder's 16 heads x 6 query tiles of
-  // 128 rows would occupy only 96 CUs), else share each K/V tile among 4 waves
+  // AW waves per block share each K/V tile; AW = 2 (tuning override only) doubles the
+  // grid.  Key splits (flash-decoding; partials merged by attn_combine_kernel) are
+  // available through M3S_ATTN_SPLITS: measured on the 768-token shapes, the combine
+  // pass costs what the wider grid saves, so the default is one split.
   int aw = 4;
   const int64_t hb = heads * batch;
-  // (AW = 1 is not offered: a 1-wave block holds a 48 KiB ring, so 3 blocks/CU = 3 waves
-  // would leave a SIMD idle)
-  while (aw > 2 && (int64_t)m3s_div_up(sq, aw * QT) * hb < 512) aw >>= 1;
-  if (const char* e = getenv("M3S_ATTN_AW")) aw = atoi(e) == 4 ? 4 : 2;  // tuning override
+  if (const char* e = getenv("M3S_ATTN_AW")) aw = atoi(e) == 2 ? 2 : 4;
+  const int nkt = (int)m3s_div_up(sk, AKT);
+  int splits = 1;
+  if (const char* e = getenv("M3S_ATTN_SPLITS")) splits = std::max(1, std::min(nkt, atoi(e)));
+  int tps = (nkt + splits - 1) / splits;
+  splits = (nkt + tps - 1) / tps;
+  const int64_t part_bytes = (int64_t)splits * hb * sq * PART_LD * 4;
+  if (splits > 1 && (!d_workspace || part_bytes > workspace_bytes || (uintptr_t)d_workspace % 16))
+    splits = 1, tps = nkt;
+  if (splits * hb > 65535) return M3S_ERR_TOO_LARGE;
+  float* part = splits > 1 ? reinterpret_cast<float*>(d_workspace) : nullptr;
   hipStream_t s = m3s_stream(stream);
 #define M3S_ATTN_LAUNCH(AWV)                                                                 \
   hipLaunchKernelGGL(attn_kernel<AWV>, dim3(m3s_div_up(sq, AWV * QT), (unsigned)heads,      \
-                     (unsigned)batch), dim3(AWV * 64), 0, s,                                 \
+                     (unsigned)(batch * splits)), dim3(AWV * 64), 0, s,                      \
                      reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,                   \
                      reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
                      ld_kv, stride_kv, reinterpret_cast<bf16_t*>(d_o), ld_o, stride_o, (int)sq, \
-                     (int)sk, c_log2)
+                     (int)sk, c_log2, splits, tps, part)
   if (aw == 2) M3S_ATTN_LAUNCH(2);
   else M3S_ATTN_LAUNCH(4);
+  if (splits > 1) {
+    M3S_LAUNCH_CHECK();
+    const int64_t rows = hb * sq;
+    hipLaunchKernelGGL(attn_combine_kernel, dim3(m3s_div_up(rows * 8, 256)), dim3(256), 0, s,
+                       part, splits, rows, (int)heads, (int)sq, c_log2,
+                       reinterpret_cast<bf16_t*>(d_o), ld_o, stride_o);
+  }
 #undef M3S_ATTN_LAUNCH
   M3S_LAUNCH_CHECK();
   return M3S_OK;

@@ -102,7 +102,8 @@ class Ops:
     def attn(self, q, ldq, sq_b, k, v, ldkv, skv_b, o, ldo, so_b, batch, heads, sq, sk):
         _lib.check(self.lib.m3s_vit_attention(_p(q), ldq, sq_b, _p(k), _p(v), ldkv, skv_b, None,
                                               None, 0, _p(o), ldo, so_b, batch, heads, sq, sk, 0.0,
-                                              self._s()), "vit_attention")
+                                              _p(self.ws), self.ws.numel(), self._s()),
+                   "vit_attention")
 
     def patchify(self, img, out, b, h, w):
         _lib.check(self.lib.m3s_vit_patchify(_p(img), _p(out), b, h, w, self._s()), "patchify")

@@ -230,3 +230,21 @@ def test_full_model_vs_fp32_restatement(dev):
     sdM = {k: v.to(dev) for k, v in sdM.items()}
     X, C, D, Q, _, _ = V.asymmetric_inference(sdm, am, sdM, aM, img_i, img_j)
     _compare_pair(out, X, C, D, Q, "full-vs-fp32")
+
+
+@pytest.mark.parametrize("splits", ["1", "3", "5"])
+def test_attention_key_splits(ops, dev, monkeypatch, splits):
+    """Flash-decoding key splits (partial O, max, sum merged by the combine kernel) with a
+    ragged last key tile and a ragged last split: Sk = 300 = 4 x 64 + 44."""
+    monkeypatch.setenv("M3S_ATTN_SPLITS", splits)
+    g = torch.Generator(device=dev).manual_seed(9)
+    Sq, Sk, heads = 200, 300, 2
+    D = heads * 64
+    q = torch.randn(3, Sq, D, device=dev, generator=g).bfloat16()
+    kv = torch.randn(3, Sk, 2 * D, device=dev, generator=g).bfloat16()
+    o = torch.empty(3, Sq, D, device=dev, dtype=torch.bfloat16)
+    ops.attn(q, D, Sq * D, kv, kv[:, :, D:], 2 * D, Sk * 2 * D, o, D, Sq * D, 3, heads, Sq, Sk)
+    qq = q.float().reshape(3, Sq, heads, 64).transpose(1, 2)
+    kk, vv = kv.float().reshape(3, Sk, 2, heads, 64).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(qq @ kk.transpose(-1, -2) / 8.0, -1) @ vv).transpose(1, 2).reshape(3, Sq, D)
+    assert _rel(o, ref) < 2e-2
