@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="no HIP graph (debug)")
     ap.add_argument("--no-graph", action="store_true", help="skip the keyframe-graph (C4) leg")
     ap.add_argument("--graph-steps", type=int, default=2)
+    ap.add_argument("--streams", action="store_true",
+                    help="overlap independent chains on side streams (measured slower)")
     return ap.parse_args()
 
 
@@ -95,6 +97,7 @@ def time_replays(g, dev, n):
 def gemm_roofline(model, img, feat_k, dev):
     """Live HIP-event timing of every GEMM launch of one eager pair inference (events on
     the stream the kernels run on): algorithmic FLOPs / summed kernel time."""
+    serial, model.serial = model.serial, True  # one stream: per-launch timing, no overlap
     model.ops.probe = []
     model.pair(img, feat_j=feat_k)
     torch.cuda.synchronize(dev)
@@ -102,6 +105,7 @@ def gemm_roofline(model, img, feat_k, dev):
     model.pair(img, feat_j=feat_k)
     torch.cuda.synchronize(dev)
     probe, model.ops.probe = model.ops.probe, None
+    model.serial = serial
     t_ms = sum(a.elapsed_time(b) for a, b, _ in probe)
     flops = sum(f for _, _, f in probe)
     return dict(launches=len(probe), gemm_ms=t_ms, gemm_flops=flops,
@@ -243,6 +247,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     model, tr, img_f = setup(dev, rank)
+    model.serial = not args.streams
 
     def step():
         return tr.track(img_f)

@@ -37,6 +37,14 @@ def _p(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+class _Nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 class Ops:
     """Thin, checked wrappers over the ViT C ABI on the current torch stream."""
 
@@ -44,8 +52,18 @@ class Ops:
         self.lib = _lib.load()
         self.dev = dev
         self.probe = None  # list → (start_event, end_event, flops) per GEMM (bench roofline)
-        # f32 split-K scratch (the M = 768 GEMMs split K when their grid cannot fill 256 CUs)
-        self.ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+        # f32 split-K / attention-split scratch, one per stream (the M = 768 GEMMs split K
+        # when their grid cannot fill 256 CUs; concurrent streams must not share it)
+        self._ws = {}
+
+    @property
+    def ws(self):
+        sid = torch.cuda.current_stream(self.dev).cuda_stream
+        w = self._ws.get(sid)
+        if w is None:
+            w = torch.empty(64 << 20, dtype=torch.uint8, device=self.dev)
+            self._ws[sid] = w
+        return w
 
     def _s(self):
         return _lib.stream(self.dev)
@@ -60,7 +78,8 @@ class Ops:
         d.bias, d.strideBias = _p(bias), sBias
         d.R, d.ldr, d.strideR = _p(R), ldr if ldr is not None else N, sR
         d.M, d.N, d.K, d.batch, d.flags = M, N, K, batch, flags
-        d.workspace, d.workspace_bytes, d.split_k = _p(self.ws), self.ws.numel(), split_k
+        ws = self.ws
+        d.workspace, d.workspace_bytes, d.split_k = _p(ws), ws.numel(), split_k
         d.weight_mod = wmod
         if bias is not None:
             d.flags |= _lib.EPI_BIAS
@@ -100,9 +119,10 @@ class Ops:
         return tab
 
     def attn(self, q, ldq, sq_b, k, v, ldkv, skv_b, o, ldo, so_b, batch, heads, sq, sk):
+        ws = self.ws
         _lib.check(self.lib.m3s_vit_attention(_p(q), ldq, sq_b, _p(k), _p(v), ldkv, skv_b, None,
                                               None, 0, _p(o), ldo, so_b, batch, heads, sq, sk, 0.0,
-                                              _p(self.ws), self.ws.numel(), self._s()),
+                                              _p(ws), ws.numel(), self._s()),
                    "vit_attention")
 
     def patchify(self, img, out, b, h, w):
@@ -249,6 +269,36 @@ class PairModel:
         self.dev = device
         self.ops = Ops(device)
         self._bufs = {}
+        # Independent chains run on side streams (captured into the same HIP graph): the
+        # decoder's norm_y + k/v projection overlap the self-attention half of the layer,
+        # the MASt3R local-feature MLP overlaps the DPT heads, the DPT's four
+        # act_postprocess branches run concurrently — when `serial` is False.  Measured on
+        # the tracking step (tools/gpu_cmd_r1y.sh): the side-stream kernels take CUs from
+        # the critical path and the graph gains dependency edges, 118.5 vs 124.9 frames/s
+        # serial, so one stream is the default.
+        self.side = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
+        self.serial = True
+
+    # ---- streams ----
+    def _on(self, k):
+        """Context: launch on side stream k (after everything queued so far on the current
+        stream), or on the current stream when serial."""
+        if self.serial:
+            return _Nullctx()
+        main = torch.cuda.current_stream(self.dev)
+        self.side[k].wait_stream(main)
+        return torch.cuda.stream(self.side[k])
+
+    def _event(self):
+        if self.serial:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        return ev
+
+    def _wait(self, ev):
+        if ev is not None:
+            torch.cuda.current_stream(self.dev).wait_event(ev)
 
     # ---- buffers ----
     def _buf(self, key, shape, dtype):
@@ -353,22 +403,29 @@ class PairModel:
         R32 = _lib.EPI_OUT_F32 | _lib.EPI_RES_F32
         for i in range(a.dec_depth):
             P = W.dec[i]
-            # y_ = norm_y(previous output of the other side) — before this layer updates x
-            o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1, pmod=4)
+            # y_ = norm_y(previous output of the other side), then its k/v projection: on a
+            # side stream, overlapping the self-attention half of the layer (the side chain
+            # must read x before this layer's first residual update writes it)
+            with self._on(0):
+                o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1, pmod=4)
+                ev_lny = self._event()
+                o.gemm(yn, P["kv_w"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
+                       sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4)
+                ev_kv = self._event()
             # self-attention
             o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
             o.gemm(xn, P["qkv_w"], qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
                    bias=P["qkv_b"], sBias=3 * D, rope=(rt, 2 * D, S), wmod=4)
             o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,
                    D, S * D, Z, a.dec_heads, S, S)
+            self._wait(ev_lny)
             o.gemm(att, P["proj_w"], x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["proj_b"],
                    sBias=D, R=x, sR=S * D, flags=R32, wmod=4)
             # cross-attention: q from norm2(x), k/v from y_
             o.ln(x, P["ln2_g"], P["ln2_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
             o.gemm(xn, P["q_w"], q, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["q_b"],
                    sBias=D, rope=(rt, D, S), wmod=4)
-            o.gemm(yn, P["kv_w"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D, sC=S * 2 * D,
-                   bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4)
+            self._wait(ev_kv)
             o.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, att, D, S * D, Z, a.dec_heads,
                    S, S)
             o.gemm(att, P["cproj_w"], x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D,
@@ -444,7 +501,55 @@ class PairModel:
         S, E, D = gh * gw, a.enc_dim, a.dec_dim
         Ld = a.layer_dims
         F = a.feature_dim
-        # act_postprocess
+        # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle, on
+        # side stream 1 (independent of the DPT: overlaps all of it)
+        aM = self.w.arch_mast3r
+        idim = E + D
+        hidd = 4 * idim
+        odim = (aM.desc_dim + 1) * aM.patch ** 2
+        desc = self._buf("desc", (2 * G, H, W, aM.desc_dim), F32)
+        desc16 = self._buf("desc16", (2 * G, H, W, aM.desc_dim), torch.float16)
+        dconf = self._buf("desc_conf", (2 * G, H, W), F32)
+        with self._on(1):
+            cat = self._buf("lf_cat", (2 * G, S, idim), BF16)
+            cv = cat.view(G, 2, S, idim)
+            cv[..., :E].copy_(hooks["h0"].view(G, 2, 2, S, E)[:, 1])
+            cv[..., E:].copy_(hooks["h12"].view(G, 2, 2, S, D)[:, 1])
+            lh = self._buf("lf_hid", (2 * G, S, hidd), BF16)
+            o.gemm(cat, self.w.lf_fc1_w, lh, S, hidd, idim, 2 * G, sA=S * idim,
+                   sB=hidd * idim, sC=S * hidd, bias=self.w.lf_fc1_b, sBias=hidd,
+                   flags=_lib.EPI_GELU, wmod=2)
+            lo = self._buf("lf_out", (2 * G, S, odim), F32)
+            o.gemm(lh, self.w.lf_fc2_w, lo, S, odim, hidd, 2 * G, sA=S * hidd,
+                   sB=odim * hidd, sC=S * odim, bias=self.w.lf_fc2_b, sBias=odim,
+                   flags=_lib.EPI_OUT_F32, wmod=2)
+            o.local_features(lo, desc, desc16, dconf, 2 * G, H, W)
+            ev_lf = self._event()
+        # act_postprocess + layer_rn (3x3, no bias → F channels): branches 1-3 on side
+        # stream 0, branch 0 (the largest) on the current stream
+        g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
+        dims = [(4 * gh, 4 * gw), (2 * gh, 2 * gw), (gh, gw), (g3h, g3w)]
+        R = [self._buf(f"rn{k}", (Z, dims[k][0], dims[k][1], F), BF16) for k in range(4)]
+        with self._on(0):
+            t1 = self._buf("ap_t1", (Z, S, Ld[1]), BF16)
+            o.gemm(hooks["h6"], Hw["ap1_w"], t1, S, Ld[1], D, Z, sA=S * D, sB=Ld[1] * D,
+                   sC=S * Ld[1], bias=Hw["ap1_b"], sBias=Ld[1], wmod=4)
+            L1 = self._buf("ap_L1", (Z, 2 * gh, 2 * gw, Ld[1]), BF16)
+            o.gemm(t1, Hw["ap1t_w"], L1, S, 4 * Ld[1], Ld[1], Z, sA=S * Ld[1],
+                   sB=4 * Ld[1] * Ld[1], sC=4 * S * Ld[1], bias=Hw["ap1t_b"], sBias=Ld[1],
+                   convt=(2, Ld[1], gw), wmod=4)
+            self._conv3(L1, "rn1_w", R[1], Z, dims[1][0], dims[1][1], Ld[1], F)
+            L2 = self._buf("ap_L2", (Z, gh, gw, Ld[2]), BF16)
+            o.gemm(hooks["h9"], Hw["ap2_w"], L2, S, Ld[2], D, Z, sA=S * D, sB=Ld[2] * D,
+                   sC=S * Ld[2], bias=Hw["ap2_b"], sBias=Ld[2], wmod=4)
+            self._conv3(L2, "rn2_w", R[2], Z, gh, gw, Ld[2], F)
+            t3 = self._buf("ap_t3", (Z, gh, gw, Ld[3]), BF16)
+            o.gemm(hooks["h12"], Hw["ap3_w"], t3, S, Ld[3], D, Z, sA=S * D, sB=Ld[3] * D,
+                   sC=S * Ld[3], bias=Hw["ap3_b"], sBias=Ld[3], wmod=4)
+            L3 = self._buf("ap_L3", (Z, g3h, g3w, Ld[3]), BF16)
+            self._conv3(t3, "ap3c_w", L3, Z, gh, gw, Ld[3], Ld[3], stride=2, bias_key="ap3c_b")
+            self._conv3(L3, "rn3_w", R[3], Z, g3h, g3w, Ld[3], F)
+            ev_ap = self._event()
         t0 = self._buf("ap_t0", (Z, S, Ld[0]), BF16)
         o.gemm(hooks["h0"], Hw["ap0_w"], t0, S, Ld[0], E, Z, sA=S * E, sB=Ld[0] * E,
                sC=S * Ld[0], bias=Hw["ap0_b"], sBias=Ld[0], wmod=4)
@@ -452,29 +557,8 @@ class PairModel:
         o.gemm(t0, Hw["ap0t_w"], L0, S, 16 * Ld[0], Ld[0], Z, sA=S * Ld[0],
                sB=16 * Ld[0] * Ld[0], sC=16 * S * Ld[0], bias=Hw["ap0t_b"], sBias=Ld[0],
                convt=(4, Ld[0], gw), wmod=4)
-        t1 = self._buf("ap_t1", (Z, S, Ld[1]), BF16)
-        o.gemm(hooks["h6"], Hw["ap1_w"], t1, S, Ld[1], D, Z, sA=S * D, sB=Ld[1] * D,
-               sC=S * Ld[1], bias=Hw["ap1_b"], sBias=Ld[1], wmod=4)
-        L1 = self._buf("ap_L1", (Z, 2 * gh, 2 * gw, Ld[1]), BF16)
-        o.gemm(t1, Hw["ap1t_w"], L1, S, 4 * Ld[1], Ld[1], Z, sA=S * Ld[1], sB=4 * Ld[1] * Ld[1],
-               sC=4 * S * Ld[1], bias=Hw["ap1t_b"], sBias=Ld[1], convt=(2, Ld[1], gw), wmod=4)
-        L2 = self._buf("ap_L2", (Z, gh, gw, Ld[2]), BF16)
-        o.gemm(hooks["h9"], Hw["ap2_w"], L2, S, Ld[2], D, Z, sA=S * D, sB=Ld[2] * D,
-               sC=S * Ld[2], bias=Hw["ap2_b"], sBias=Ld[2], wmod=4)
-        t3 = self._buf("ap_t3", (Z, gh, gw, Ld[3]), BF16)
-        o.gemm(hooks["h12"], Hw["ap3_w"], t3, S, Ld[3], D, Z, sA=S * D, sB=Ld[3] * D,
-               sC=S * Ld[3], bias=Hw["ap3_b"], sBias=Ld[3], wmod=4)
-        g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
-        L3 = self._buf("ap_L3", (Z, g3h, g3w, Ld[3]), BF16)
-        self._conv3(t3, "ap3c_w", L3, Z, gh, gw, Ld[3], Ld[3], stride=2, bias_key="ap3c_b")
-        # layer_rn (3x3, no bias) → F channels
-        dims = [(4 * gh, 4 * gw), (2 * gh, 2 * gw), (gh, gw), (g3h, g3w)]
-        R = []
-        for k, Lk in enumerate([L0, L1, L2, L3]):
-            hh, ww = dims[k]
-            r = self._buf(f"rn{k}", (Z, hh, ww, F), BF16)
-            self._conv3(Lk, f"rn{k}_w", r, Z, hh, ww, Ld[k], F)
-            R.append(r)
+        self._conv3(L0, "rn0_w", R[0], Z, dims[0][0], dims[0][1], Ld[0], F)
+        self._wait(ev_ap)
         # refinenets: path_k = up2(out_conv(RCU2(path_{k+1} + RCU1(R_k)))) with the next
         # level's skip pre-added by the upsample (consumed as RCU1's residual addend)
         p4 = self._buf("path4", (Z, gh, gw, F), BF16)
@@ -498,25 +582,7 @@ class PairModel:
         conf = self._buf("conf", (Z, H, W), F32)
         o.dpt_out(hd2, Hw["head4_w"], Hw["head4_b"], pts, conf, H * W, a.conf_min, Z,
                   H * W * a.last_dim, H * W, pmod=4)
-        # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle
-        aM = self.w.arch_mast3r
-        idim = E + D
-        hidd = 4 * idim
-        odim = (aM.desc_dim + 1) * aM.patch ** 2
-        cat = self._buf("lf_cat", (2 * G, S, idim), BF16)
-        cv = cat.view(G, 2, S, idim)
-        cv[..., :E].copy_(hooks["h0"].view(G, 2, 2, S, E)[:, 1])
-        cv[..., E:].copy_(hooks["h12"].view(G, 2, 2, S, D)[:, 1])
-        lh = self._buf("lf_hid", (2 * G, S, hidd), BF16)
-        o.gemm(cat, self.w.lf_fc1_w, lh, S, hidd, idim, 2 * G, sA=S * idim, sB=hidd * idim,
-               sC=S * hidd, bias=self.w.lf_fc1_b, sBias=hidd, flags=_lib.EPI_GELU, wmod=2)
-        lo = self._buf("lf_out", (2 * G, S, odim), F32)
-        o.gemm(lh, self.w.lf_fc2_w, lo, S, odim, hidd, 2 * G, sA=S * hidd, sB=odim * hidd,
-               sC=S * odim, bias=self.w.lf_fc2_b, sBias=odim, flags=_lib.EPI_OUT_F32, wmod=2)
-        desc = self._buf("desc", (2 * G, H, W, aM.desc_dim), F32)
-        desc16 = self._buf("desc16", (2 * G, H, W, aM.desc_dim), torch.float16)
-        dconf = self._buf("desc_conf", (2 * G, H, W), F32)
-        o.local_features(lo, desc, desc16, dconf, 2 * G, H, W)
+        self._wait(ev_lf)
         return pts, conf, desc16, desc, dconf
 
     def _fusion_skip(self, k, path, skip, b, h, w, next_hw, out):
