@@ -176,8 +176,12 @@ enum {
   M3S_EPI_OUT_F32 = 32,   /* store f32 (default bf16)                          */
   M3S_PRO_RELU = 64,      /* ReLU applied to A while loading (conv prologue)   */
   M3S_EPI_CONVT = 128,    /* scatter rows/cols as ConvTranspose(k=s, stride=s) */
-  M3S_EPI_ROPE = 256      /* 2D RoPE on columns < rope_cols (head dim 64), after bias;
+  M3S_EPI_ROPE = 256,     /* 2D RoPE on columns < rope_cols (head dim 64), after bias;
                              not combined with a residual or CONVT                   */
+  M3S_EPI_DPT_OUT = 512   /* DPT regression tail fused into a conv with N = 128 (one tile
+                             spans the row): relu(acc + bias) · W4ᵀ + b4 (1x1, 128 → 4), then
+                             reg_dense_depth / conf (d3r/heads/postprocess.py:10-58) written
+                             to dpt_pts / dpt_conf; C is not written               */
 };
 
 typedef struct {
@@ -197,6 +201,11 @@ typedef struct {
   int32_t rope_cols, rope_tokens;          /* ROPE: rotated columns; row m → token m % rope_tokens */
   int32_t weight_mod;                      /* >0: batch g reads B / bias of batch g % weight_mod
                                               (P problem groups sharing one weight stack) */
+  const float* dpt_w4;                     /* DPT_OUT: f32 [heads][4][128] (head g % weight_mod) */
+  const float* dpt_b4;                     /* DPT_OUT: f32 [heads][4]                  */
+  float* dpt_pts;                          /* DPT_OUT: f32 [batch][M][3]               */
+  float* dpt_conf;                         /* DPT_OUT: f32 [batch][M]                  */
+  float dpt_conf_min;                      /* DPT_OUT: conf = conf_min + exp(c)        */
 } m3s_gemm_desc;
 
 /* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 8 == 0; conv: Cin % 32 == 0.

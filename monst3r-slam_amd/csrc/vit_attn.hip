@@ -125,18 +125,31 @@ template <int AW>
 __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, bf16_t* __restrict__ o,
-    int64_t ldo, int64_t so_b, int Sq, int Sk, float c_log2, int splits, int tiles_per_split,
-    float* __restrict__ part) {
+    int64_t ldo, int64_t so_b, int Sq, int Sk, int heads, float c_log2, int splits,
+    int tiles_per_split, float* __restrict__ part) {
   constexpr int ACH = TILE_BYTES / 16 / (AW * 64);  // DMA chunks per thread per operand
   __shared__ __attribute__((aligned(16))) char lds[ASTAGES * STAGE_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
-  const int q0 = blockIdx.x * (AW * QT) + wid * QT;
-  const int h = blockIdx.y;
-  const int64_t b = blockIdx.z / splits;
-  const int sp = blockIdx.z - (int)b * splits;   // key split (flash-decoding style)
+  // 1-D grid (query tile fastest, then head, then batch x split) remapped so that each
+  // XCD gets a contiguous id range: the query tiles of one head share an XCD and its L2
+  // holds that head's K/V (round-robin dispatch would fetch it once per query tile)
+  const int nqt = (Sq + AW * QT - 1) / (AW * QT);
+  const int total = gridDim.x, orig = blockIdx.x;
+  int lin = orig;
+  if (total >= 16) {
+    const int qq = total / 8, rr = total % 8, xcd = orig % 8;
+    lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  }
+  const int qt = lin % nqt;
+  const int hz = lin / nqt;
+  const int h = hz % heads;
+  const int bz = hz / heads;
+  const int q0 = qt * (AW * QT) + wid * QT;
+  const int64_t b = bz / splits;
+  const int sp = bz - (int)b * splits;   // key split (flash-decoding style)
   const bf16_t* Q = q + b * sq_b + h * HD;
 
   // Q fragments (B operand of S^T = K Q^T): query q0 + r, d = 16 ks + 8 hh .. +7
@@ -300,8 +313,8 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
   }
   if (qrow >= Sq) return;
   if (part) {  // split: unnormalised O, running max m and sum l → [split][b][h][q][68] f32
-    float* P = part + ((((int64_t)sp * (gridDim.z / splits) + b) * gridDim.y + h) * Sq + qrow) *
-                          PART_LD;
+    const int64_t nb = (int64_t)total / ((int64_t)nqt * heads * splits);  // batch
+    float* P = part + ((((int64_t)sp * nb + b) * heads + h) * Sq + qrow) * PART_LD;
 #pragma unroll
     for (int d = 0; d < 2; d++)
 #pragma unroll
@@ -418,16 +431,17 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   const int64_t part_bytes = (int64_t)splits * hb * sq * PART_LD * 4;
   if (splits > 1 && (!d_workspace || part_bytes > workspace_bytes || (uintptr_t)d_workspace % 16))
     splits = 1, tps = nkt;
-  if (splits * hb > 65535) return M3S_ERR_TOO_LARGE;
+  if ((int64_t)m3s_div_up(sq, 2 * QT) * hb * splits >= (1ll << 31)) return M3S_ERR_TOO_LARGE;
   float* part = splits > 1 ? reinterpret_cast<float*>(d_workspace) : nullptr;
   hipStream_t s = m3s_stream(stream);
 #define M3S_ATTN_LAUNCH(AWV)                                                                 \
-  hipLaunchKernelGGL(attn_kernel<AWV>, dim3(m3s_div_up(sq, AWV * QT), (unsigned)heads,      \
-                     (unsigned)(batch * splits)), dim3(AWV * 64), 0, s,                      \
+  hipLaunchKernelGGL(attn_kernel<AWV>,                                                      \
+                     dim3((unsigned)(m3s_div_up(sq, AWV * QT) * heads * batch * splits)),    \
+                     dim3(AWV * 64), 0, s,                                                   \
                      reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,                   \
                      reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
                      ld_kv, stride_kv, reinterpret_cast<bf16_t*>(d_o), ld_o, stride_o, (int)sq, \
-                     (int)sk, c_log2, splits, tps, part)
+                     (int)sk, (int)heads, c_log2, splits, tps, part)
   if (aw == 2) M3S_ATTN_LAUNCH(2);
   else M3S_ATTN_LAUNCH(4);
   if (splits > 1) {

@@ -25,6 +25,7 @@
 //   registers (v_pk_max_i16 on the bf16 bits).
 // XCD-aware bijective tile order (cdna_hip_programming.md T1).
 #include <stdlib.h>
+#include <algorithm>
 #include "vit_common.h"
 
 namespace {
@@ -50,12 +51,18 @@ struct Args {
   int Hin, Win, Cin, Hout, Wout, stride;
   int ct_s, ct_cout, ct_gw;
   int tiles_m, tiles_n;
+  int nmajor;              // tile order within a group (see gemm_kernel)
   int splits;
   int vec;                 // 8-wide vector epilogue allowed (alignment / N % 8 checked on host)
   float* ws;               // split-K partials [batch*splits][M][N]
   const float* rope_tab;   // [tokens][2 (y,x)][2 (cos,sin)][16]
   int rope_cols, rope_tokens;
   int wmod;                // > 0: weights / bias of batch g % wmod
+  const float* dpt_w4;     // DPT_OUT tail (see m3s_gemm_desc)
+  const float* dpt_b4;
+  float* dpt_pts;
+  float* dpt_conf;
+  float dpt_conf_min;
 };
 
 // ---------------------------------------------------------------------------------------
@@ -267,15 +274,30 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
   static_assert(C::L * (STAGES - 2) <= 63, "vmcnt range");
   __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
 
+  // 1-D grid over (batch x split) groups x tiles.  Workgroups are dispatched to the 8
+  // XCDs round-robin by linear id; the bijective remap gives each XCD a contiguous range
+  // of remapped ids (cdna_hip_programming.md T1), so neighbouring tiles share its L2.
+  // Within a group the tile order is M-major (an XCD sweeps N for one A band: A reused)
+  // or N-major (an XCD sweeps the M bands of a few weight columns: B reused), whichever
+  // the host estimated to fetch fewer bytes.
   const int nwg = a.tiles_m * a.tiles_n;
+  const int total = gridDim.x;
   const int orig = blockIdx.x;
-  int wgid = orig;
-  if (nwg >= 16) {
-    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
-    wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  int wid_lin = orig;
+  if (total >= 16) {
+    const int q = total / 8, r = total % 8, xcd = orig % 8;
+    wid_lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
   }
-  const int tm = wgid / a.tiles_n, tn = wgid - tm * a.tiles_n;
-  const int zz = blockIdx.z;
+  const int zz = wid_lin / nwg;
+  const int wgid = wid_lin - zz * nwg;
+  int tm, tn;
+  if (a.nmajor) {
+    tn = wgid / a.tiles_m;
+    tm = wgid - tn * a.tiles_m;
+  } else {
+    tm = wgid / a.tiles_n;
+    tn = wgid - tm * a.tiles_n;
+  }
   const int g = SPLIT ? zz / a.splits : zz;
   const int split = SPLIT ? zz - g * a.splits : 0;
   const int m0 = tm * BM;
@@ -571,6 +593,48 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
   block_sync_lds();
   M3S_T(t_e2);
 
+  if constexpr (EPI >= 0 && (EPI & M3S_EPI_DPT_OUT) != 0) {
+    // fused DPT tail: one pixel (row) per thread, all BN = 128 channels in the LDS tile
+    static_assert(BN == 128 && !SPLIT, "DPT_OUT needs the full 128-channel row in one tile");
+    const int gw = a.wmod > 0 ? g % a.wmod : g;
+    const float* w4 = a.dpt_w4 + (int64_t)gw * 512;
+    const float* b4 = a.dpt_b4 + (int64_t)gw * 4;
+    const float* cb = (EPI & M3S_EPI_BIAS) ? a.bias + (int64_t)gw * a.sBias : nullptr;
+    for (int row = tid; row < BM; row += NT) {
+      const int m = m0 + row;
+      if (m >= a.M) break;
+      float o4[4] = {b4[0], b4[1], b4[2], b4[3]};
+      const float* src = cs + row * C::CST;
+#pragma unroll 4
+      for (int c = 0; c < 128; c += 4) {
+        float4 x = *reinterpret_cast<const float4*>(src + c);
+        if (cb) {
+          x.x += cb[c];
+          x.y += cb[c + 1];
+          x.z += cb[c + 2];
+          x.w += cb[c + 3];
+        }
+        x.x = fmaxf(x.x, 0.f);
+        x.y = fmaxf(x.y, 0.f);
+        x.z = fmaxf(x.z, 0.f);
+        x.w = fmaxf(x.w, 0.f);
+#pragma unroll
+        for (int oo = 0; oo < 4; oo++)
+          o4[oo] += w4[oo * 128 + c] * x.x + w4[oo * 128 + c + 1] * x.y +
+                    w4[oo * 128 + c + 2] * x.z + w4[oo * 128 + c + 3] * x.w;
+      }
+      // reg_dense_depth('exp') + conf ('exp', conf_min): as dpt_out_kernel (vit_misc.hip)
+      const float d = sqrtf(o4[0] * o4[0] + o4[1] * o4[1] + o4[2] * o4[2]);
+      const float sc = expm1f(d) / fmaxf(d, 1e-8f);
+      float* P = a.dpt_pts + ((int64_t)g * a.M + m) * 3;
+      P[0] = o4[0] * sc;
+      P[1] = o4[1] * sc;
+      P[2] = o4[2] * sc;
+      a.dpt_conf[(int64_t)g * a.M + m] = a.dpt_conf_min + expf(o4[3]);
+    }
+    return;
+  }
+
   if (SPLIT) {
     float* P = a.ws + (int64_t)zz * a.M * a.N;
 #pragma unroll 4
@@ -591,7 +655,7 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
 #ifdef M3S_GEMM_STAMPS
     if (tid == 0) {
       M3S_T(t_end);
-      long long* o = g_m3s_stamps + ((int64_t)blockIdx.z * gridDim.x + blockIdx.x) * 12;
+      long long* o = g_m3s_stamps + (int64_t)blockIdx.x * 12;
       o[8] = t_e0 - t_loop;
       o[9] = t_e1 - t_e0;
       o[10] = t_e2 - t_e1;
@@ -684,7 +748,7 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
 #ifdef M3S_GEMM_STAMPS
   if (tid == 0) {
     M3S_T(t_end);
-    long long* o = g_m3s_stamps + ((int64_t)blockIdx.z * gridDim.x + blockIdx.x) * 12;
+    long long* o = g_m3s_stamps + (int64_t)blockIdx.x * 12;
       o[8] = t_e0 - t_loop;
       o[9] = t_e1 - t_e0;
       o[10] = t_e2 - t_e1;
@@ -783,6 +847,10 @@ void launch_main(Args& a, dim3 grid, hipStream_t s) {
       if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0>(a, grid, s, key)) return;
       if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RES_BF16>(a, grid, s, key)) return;
       if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RELU>(a, grid, s, key)) return;
+      if constexpr (BN == 128)
+        if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RELU | M3S_EPI_DPT_OUT>(
+                a, grid, s, key))
+          return;
     }
   }
   hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, -1>), grid,
@@ -794,7 +862,24 @@ int launch(Args& a, int batch, hipStream_t s) {
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = (a.N + BN - 1) / BN;
   const bool split = a.splits > 1;
-  dim3 grid((unsigned)(a.tiles_m * a.tiles_n), 1, (unsigned)(batch * (split ? a.splits : 1)));
+  const int64_t groups = (int64_t)batch * (split ? a.splits : 1);
+  if ((int64_t)a.tiles_m * a.tiles_n * groups >= (1ll << 31)) return M3S_ERR_TOO_LARGE;
+  dim3 grid((unsigned)(a.tiles_m * a.tiles_n * groups));
+  // tile order: the operand bytes an XCD's L2 must fetch for its contiguous chunk of T
+  // tiles — M-major touches ceil(T / tiles_n) A bands and min(T, tiles_n) B columns,
+  // N-major ceil(T / tiles_m) B columns and min(T, tiles_m) A bands; take the smaller
+  if (a.mode == 0) {
+    const int64_t T = ((int64_t)a.tiles_m * a.tiles_n * groups + 7) / 8;
+    const double band = (double)BM * a.K * 2, col = (double)BN * a.K * 2;
+    const double costM = band * std::min<int64_t>(a.tiles_m, (T + a.tiles_n - 1) / a.tiles_n + 1) +
+                         col * std::min<int64_t>(T, a.tiles_n);
+    const double costN = col * std::min<int64_t>(a.tiles_n, (T + a.tiles_m - 1) / a.tiles_m + 1) +
+                         band * std::min<int64_t>(T, a.tiles_m);
+    a.nmajor = costN < costM;
+    if (const char* e = getenv("M3S_GEMM_ORDER")) a.nmajor = atoi(e);  // tuning override
+  } else {
+    a.nmajor = 0;
+  }
   if (split) {
     hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true, -1>), grid, dim3(NT),
                        0, s, a);
@@ -885,6 +970,11 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   a.rope_cols = d->rope_cols;
   a.rope_tokens = d->rope_tokens;
   a.wmod = d->weight_mod > 0 ? d->weight_mod : 0;
+  a.dpt_w4 = d->dpt_w4;
+  a.dpt_b4 = d->dpt_b4;
+  a.dpt_pts = d->dpt_pts;
+  a.dpt_conf = d->dpt_conf;
+  a.dpt_conf_min = d->dpt_conf_min;
   const bool out32 = d->flags & M3S_EPI_OUT_F32;
   const bool has_bias = d->bias && (d->flags & M3S_EPI_BIAS);
   a.vec = d->N % 8 == 0 && d->ldc % 8 == 0 && d->strideC % 8 == 0 && aligned16(d->C) &&
@@ -893,6 +983,13 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
           (!d->R || (d->ldr % 8 == 0 && d->strideR % 8 == 0 && aligned16(d->R)));
   (void)out32;
   if ((d->flags & M3S_EPI_ROPE) && !a.vec) return M3S_ERR_INVALID_ARG;
+  if (d->flags & M3S_EPI_DPT_OUT) {
+    // compiled only as the conv variant BIAS? | RELU | DPT_OUT on the 8-wide vector path
+    const int rest = d->flags & ~(M3S_EPI_DPT_OUT | M3S_EPI_RELU | M3S_EPI_BIAS);
+    if (d->mode != 1 || d->N != 128 || rest != 0 || !(d->flags & M3S_EPI_RELU) || !a.vec ||
+        !d->dpt_w4 || !d->dpt_b4 || !d->dpt_pts || !d->dpt_conf)
+      return M3S_ERR_INVALID_ARG;
+  }
   hipStream_t s = m3s_stream(stream);
 
   // Tile choice (measured on the pair shapes, tools/gemm_tune.py): 128x128 tiles (one

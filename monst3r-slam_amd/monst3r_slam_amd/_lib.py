@@ -73,11 +73,13 @@ class GemmDesc(ctypes.Structure):
                 ("ct_s", ctypes.c_int32), ("ct_cout", ctypes.c_int32), ("ct_gw", ctypes.c_int32),
                 ("workspace", _P), ("workspace_bytes", _I64), ("split_k", ctypes.c_int32),
                 ("rope_table", _P), ("rope_cols", ctypes.c_int32),
-                ("rope_tokens", ctypes.c_int32), ("weight_mod", ctypes.c_int32)]
+                ("rope_tokens", ctypes.c_int32), ("weight_mod", ctypes.c_int32),
+                ("dpt_w4", _P), ("dpt_b4", _P), ("dpt_pts", _P), ("dpt_conf", _P),
+                ("dpt_conf_min", ctypes.c_float)]
 
 
 (EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT,
- EPI_ROPE) = (1, 2, 4, 8, 16, 32, 64, 128, 256)
+ EPI_ROPE, EPI_DPT_OUT) = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512)
 
 _lib = None
 

@@ -70,7 +70,7 @@ class Ops:
 
     def gemm(self, A, B, C, M, N, K, batch=1, *, lda=None, ldb=None, ldc=None, sA=0, sB=0,
              sC=0, bias=None, sBias=0, R=None, ldr=None, sR=0, flags=0, conv=None, convt=None,
-             rope=None, split_k=0, wmod=0):
+             rope=None, split_k=0, wmod=0, dpt=None):
         d = _lib.GemmDesc()
         d.A, d.lda, d.strideA = _p(A), lda if lda is not None else K, sA
         d.B, d.ldb, d.strideB = _p(B), ldb if ldb is not None else K, sB
@@ -81,6 +81,10 @@ class Ops:
         ws = self.ws
         d.workspace, d.workspace_bytes, d.split_k = _p(ws), ws.numel(), split_k
         d.weight_mod = wmod
+        if dpt is not None:  # fused DPT tail: (W4 [h][4][128], b4 [h][4], pts, conf, conf_min)
+            d.flags |= _lib.EPI_DPT_OUT
+            d.dpt_w4, d.dpt_b4, d.dpt_pts, d.dpt_conf = (_p(t) for t in dpt[:4])
+            d.dpt_conf_min = float(dpt[4])
         if bias is not None:
             d.flags |= _lib.EPI_BIAS
         if conv is not None:
@@ -449,7 +453,7 @@ class PairModel:
 
     # ---- DPT heads (batched over z) ----
     def _conv3(self, x, wkey, out, b, hin, win, cin, cout, stride=1, bias_key=None, R=None,
-               flags=0):
+               flags=0, dpt=None):
         o, H = self.ops, self.w.h
         hout = (hin + 2 - 3) // stride + 1
         wout = (win + 2 - 3) // stride + 1
@@ -457,7 +461,7 @@ class PairModel:
                sB=cout * 9 * cin, sC=hout * wout * cout,
                bias=H[bias_key] if bias_key else None, sBias=cout, R=R,
                sR=hout * wout * cout, flags=flags, conv=(hin, win, cin, hout, wout, stride),
-               wmod=4)
+               wmod=4, dpt=dpt)
         return hout, wout
 
     def _rcu(self, x, k, u, b, h, w, out, addend_res=None):
@@ -575,13 +579,13 @@ class PairModel:
         self._conv3(p1, "head0_w", hd0, Z, h2, w2, F, F // 2, bias_key="head0_b")
         hup = self._buf("head_up", (Z, H, W, F // 2), BF16)
         o.up2(hd0, hup, Z, h2, w2, F // 2, H, W)
-        hd2 = self._buf("head2", (Z, H, W, a.last_dim), BF16)
-        self._conv3(hup, "head2_w", hd2, Z, H, W, F // 2, a.last_dim, bias_key="head2_b",
-                    flags=_lib.EPI_RELU)
+        # conv3x3 → last_dim + ReLU with the 1x1 (last_dim → 4) + reg_dense_depth / conf
+        # fused into its epilogue: the 128-channel map never reaches HBM
         pts = self._buf("pts3d", (Z, H, W, 3), F32)
         conf = self._buf("conf", (Z, H, W), F32)
-        o.dpt_out(hd2, Hw["head4_w"], Hw["head4_b"], pts, conf, H * W, a.conf_min, Z,
-                  H * W * a.last_dim, H * W, pmod=4)
+        self._conv3(hup, "head2_w", pts, Z, H, W, F // 2, a.last_dim, bias_key="head2_b",
+                    flags=_lib.EPI_RELU,
+                    dpt=(Hw["head4_w"], Hw["head4_b"], pts, conf, a.conf_min))
         self._wait(ev_lf)
         return pts, conf, desc16, desc, dconf
 

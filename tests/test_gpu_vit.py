@@ -248,3 +248,34 @@ def test_attention_key_splits(ops, dev, monkeypatch, splits):
     kk, vv = kv.float().reshape(3, Sk, 2, heads, 64).permute(2, 0, 3, 1, 4)
     ref = (torch.softmax(qq @ kk.transpose(-1, -2) / 8.0, -1) @ vv).transpose(1, 2).reshape(3, Sq, D)
     assert _rel(o, ref) < 2e-2
+
+
+@pytest.mark.parametrize("H,W,b", [(48, 64, 4), (96, 128, 2)])
+def test_conv_fused_dpt_tail(ops, dev, H, W, b):
+    """head.2 conv3x3 (128 → 128) + bias + ReLU with the 1x1 (128 → 4) + reg_dense_depth /
+    conf fused into the GEMM epilogue (EPI_DPT_OUT), per-head weights by weight_mod, against
+    torch fp32 (d3r/heads/postprocess.py:10-58)."""
+    g = torch.Generator(device=dev).manual_seed(12)
+    cin = cout = 128
+    x = torch.randn(b, H, W, cin, device=dev, generator=g).bfloat16()
+    w = (torch.randn(2, cout, cin, 3, 3, device=dev, generator=g) / (9 * cin) ** 0.5)
+    bias = torch.randn(2, cout, device=dev, generator=g) * 0.1
+    w4 = torch.randn(2, 4, cout, device=dev, generator=g) / cout ** 0.5 * 0.5
+    b4 = torch.randn(2, 4, device=dev, generator=g) * 0.1
+    wp = w.bfloat16().permute(0, 1, 3, 4, 2).reshape(2, cout, 9 * cin).contiguous()
+    pts = torch.empty(b, H, W, 3, device=dev)
+    conf = torch.empty(b, H, W, device=dev)
+    ops.gemm(x, wp, pts, H * W, cout, 9 * cin, b, sA=H * W * cin, sB=cout * 9 * cin,
+             sC=H * W * cout, bias=bias, sBias=cout, flags=4, conv=(H, W, cin, H, W, 1),
+             wmod=2, dpt=(w4, b4, pts, conf, 1.0))
+    xin = x.float().permute(0, 3, 1, 2)
+    ref_p, ref_c = [], []
+    for z in range(b):
+        y = F.relu(F.conv2d(xin[z:z + 1], w[z % 2].bfloat16().float(), bias[z % 2], padding=1))
+        o = F.conv2d(y, w4[z % 2][:, :, None, None], b4[z % 2]).permute(0, 2, 3, 1)[0]
+        d = o[..., :3].norm(dim=-1, keepdim=True)
+        ref_p.append(o[..., :3] / d.clamp(min=1e-8) * torch.expm1(d))
+        ref_c.append(1.0 + o[..., 3].exp())
+    ref_p, ref_c = torch.stack(ref_p), torch.stack(ref_c)
+    assert _rel(pts, ref_p) < 1e-2
+    assert _rel(conf, ref_c) < 1e-2
