@@ -192,6 +192,17 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
             "sharding": f"edges round-robin over {world} rank(s), RCCL all-gather"}
 
 
+def pmc_traffic():
+    """HBM bytes of the GEMM launches of one pair inference, from the committed rocprofv3
+    PMC passes (tools/pmc_traffic.py over FETCH_SIZE / WRITE_SIZE runs of this bench; PMC
+    counters cannot be read from inside the timed run).  None if absent."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_gemm_traffic.json")
+    if not os.path.exists(path):
+        return None
+    g = json.load(open(path))["gemm"]
+    return g
+
+
 def cpu_baseline():
     """The reference-equivalent CPU path on this box's host cores, bounded sample:
     the fp32 PyTorch restatement of the pair inference at 224x224 (configs[0] plumbing
@@ -279,6 +290,7 @@ def main():
     if rank == 0:
         pair_ms = time_replays(g_pair, dev, max(5, args.steps // 2)) if g_pair else None
         roof = gemm_roofline(model, img_f, tr.kf.feat, dev)
+        pmc = pmc_traffic()
         ms = elapsed / args.steps * 1e3
         line = {
             "metric": METRIC,
@@ -300,7 +312,12 @@ def main():
             "pair_inference_ms": pair_ms,
             "roofline": {"bound": "mfma", "achieved": roof["tflops"], "peak": BF16_DENSE_TFLOPS,
                          "unit": "TFLOP/s", "frac": roof["tflops"] / BF16_DENSE_TFLOPS,
-                         "traffic": None, "kernel": "gemm_kernel (bf16 MFMA GEMM / implicit conv)",
+                         "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                         "traffic_unit": "HBM bytes per GEMM launch (PMC FETCH_SIZE x2 + "
+                                         "WRITE_SIZE, profiles/r01_pmc_gemm_traffic.json)",
+                         "traffic_per_pair_bytes": pmc["hbm_bytes_per_pair"] if pmc else None,
+                         "l2_hit_rate": pmc["l2_hit_rate"] if pmc else None,
+                         "kernel": "gemm_kernel (bf16 MFMA GEMM / implicit conv)",
                          "gemm_launches_per_pair": roof["launches"],
                          "gemm_ms_per_pair": roof["gemm_ms"],
                          "gemm_gflop_per_pair": roof["gemm_flops"] / 1e9,
