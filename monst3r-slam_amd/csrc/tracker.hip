@@ -1,11 +1,12 @@
 // Frontend pose tracker (FrameTracker2.opt_pose_ray_dist_sim3 / opt_pose_calib_sim3,
-// tracker2.py:299-409) as three gfx950 kernels per Gauss-Newton iteration-pair:
-//   track_points_kernel<MODE>: per point residual (4 rows ray+dist, or 3 rows u,v,log z),
-//     Jacobian J = -d(rd)/dP * [I, -[P]x, P], Huber-robust whitening, and the 28+7+1
-//     sums of A^T A, -A^T b and 0.5 b^T b; wave64 butterfly + LDS per workgroup.
-//   track_solve_kernel: one workgroup reduces the partials (f64, fixed order), 7x7
-//     Cholesky, tau = H^-1 g, T <- Exp(tau) * T (lietorch retr), check_convergence
-//     (nonlinear_optimizer.py:5-25, NaN-aware on iteration 0) and sets a done flag.
+// tracker2.py:299-409), ONE gfx950 kernel per Gauss-Newton iteration:
+//   every workgroup: per point residual (4 rows ray+dist, or 3 rows u,v,log z), Jacobian
+//     J = -d(rd)/dP * [I, -[P]x, P], Huber-robust whitening, and the 28+7+1 sums of A^T A,
+//     -A^T b and 0.5 b^T b; wave64 butterfly + LDS → one partial row per workgroup;
+//   the LAST workgroup to finish (agent-scope release / ticket / acquire,
+//     cdna_hip_programming.md §6 G16): f64 reduction of the partials in fixed block order
+//     (deterministic), 7x7 Cholesky, tau = H^-1 g, T <- Exp(tau) * T (lietorch retr),
+//     check_convergence (nonlinear_optimizer.py:5-25, NaN-aware on iteration 0), done flag.
 // All max_iters iterations are enqueued without a host sync; once the flag is set the
 // remaining launches return at entry.
 #include "common.h"
@@ -23,6 +24,7 @@ struct TrackState {
   float T[8];        // current T_CkCf
   double old_cost;
   int done, fail, iters, conv;
+  unsigned ticket;   // workgroups of the current iteration that have published partials
 };
 
 struct TrackParams {
@@ -82,14 +84,19 @@ __global__ void track_init_kernel(const float* __restrict__ Twc_k, const float* 
   st->fail = 0;
   st->iters = 0;
   st->conv = 0;
+  st->ticket = 0;
 }
 
+__device__ void track_solve(TrackState* st, const float* partial, int nblocks, float rel_error,
+                            float delta_norm);
+
 template <int MODE>
-__global__ __launch_bounds__(kThreads) void track_points_kernel(
-    const TrackState* __restrict__ st, TrackParams prm, const float* __restrict__ K,
+__global__ __launch_bounds__(kThreads) void track_iter_kernel(
+    TrackState* __restrict__ st, TrackParams prm, const float* __restrict__ K,
     const float* __restrict__ Xf, const float* __restrict__ Xk, const float* __restrict__ Qk,
     const uint8_t* __restrict__ valid, const float* __restrict__ meas_k,
-    const uint8_t* __restrict__ valid_meas, int64_t n, float* __restrict__ partial) {
+    const uint8_t* __restrict__ valid_meas, int64_t n, float* __restrict__ partial,
+    float rel_error, float delta_norm) {
   if (st->done) return;
   if (MODE == TRACK_CALIB) {
     prm.fx = K[0];
@@ -184,13 +191,29 @@ __global__ __launch_bounds__(kThreads) void track_points_kernel(
     for (int w = 1; w < kThreads / M3S_WAVE; w++) v += red[w][threadIdx.x];
     partial[blockIdx.x * kAcc + threadIdx.x] = v;
   }
+  // publish this workgroup's partial row; the last to arrive reduces and solves
+  __shared__ unsigned s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t =
+        __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == gridDim.x - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  track_solve(st, partial, (int)gridDim.x, rel_error, delta_norm);
 }
 
-__global__ __launch_bounds__(kThreads) void track_solve_kernel(TrackState* st,
-                                                               const float* __restrict__ partial,
-                                                               int nblocks, float rel_error,
-                                                               float delta_norm) {
-  if (st->done) return;
+__device__ void track_solve(TrackState* st, const float* partial, int nblocks, float rel_error,
+                            float delta_norm) {
   __shared__ double sacc[kAcc];
   // f64 reduction of the partials: lane-per-(accumulator, block-slice), then fixed order
   const int tid = threadIdx.x;
@@ -236,6 +259,7 @@ __global__ __launch_bounds__(kThreads) void track_solve_kernel(TrackState* st,
       L[i][j] = t / L[j][j];
     }
   }
+  st->ticket = 0;  // next iteration (next launch) counts from zero again
   if (!ok) {
     st->fail = 1;
     st->done = 1;
@@ -323,11 +347,8 @@ int run_track(const float* Twc_k, const float* Twc_f, const float* Xf, const flo
   int nb = (int)((n + kThreads - 1) / kThreads);
   if (nb > kBlocks) nb = kBlocks;
   for (int it = 0; it < max_iters; it++) {
-    hipLaunchKernelGGL(track_points_kernel<MODE>, dim3(nb), dim3(kThreads), 0, s, st, prm, K, Xf,
-                       Xk, Qk, valid, meas_k, valid_meas, n, partial);
-    M3S_LAUNCH_CHECK();
-    hipLaunchKernelGGL(track_solve_kernel, dim3(1), dim3(kThreads), 0, s, st, partial, nb,
-                       rel_error, delta_norm);
+    hipLaunchKernelGGL(track_iter_kernel<MODE>, dim3(nb), dim3(kThreads), 0, s, st, prm, K, Xf,
+                       Xk, Qk, valid, meas_k, valid_meas, n, partial, rel_error, delta_norm);
     M3S_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(track_finish_kernel, dim3(1), dim3(64), 0, s, Twc_k, st, T_WCf, T_CkCf,
