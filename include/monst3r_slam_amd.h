@@ -231,6 +231,15 @@ int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_gamma,
                       float eps, int64_t batch, int64_t stride_x, int64_t stride_y,
                       int64_t stride_param, int64_t param_mod, int x_batch_xor, void* stream);
 
+/* Two LayerNorms of the same f32 rows in one pass (the decoder's norm1 of x and norm_y of
+ * the other side, croco/blocks.py:184-187): y[b] = LN(x[b]; gamma/beta of b) and
+ * y2[b ^ 1] = LN(x[b]; gamma2/beta2 of b ^ 1), both bf16; batch even; param_mod as above. */
+int m3s_vit_layernorm_dual(const float* d_x, const float* d_gamma, const float* d_beta,
+                           void* d_y, const float* d_gamma2, const float* d_beta2, void* d_y2,
+                           int64_t rows, int64_t dim, float eps, int64_t batch,
+                           int64_t stride_x, int64_t stride_y, int64_t stride_param,
+                           int64_t param_mod, void* stream);
+
 /* In-place 2-D RoPE (curope kernels.cu:17-82; pos_embed.py:106-158) on a bf16 view
  * t [B][S] rows of ld (head h at column h*64): dims [0,32) rotate by pos y, [32,64) by
  * pos x, pairs (i, i+16), angle = pos * base^(-i/16).  pos int64 [B][S][2] (y, x). */

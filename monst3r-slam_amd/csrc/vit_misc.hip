@@ -7,14 +7,19 @@
 namespace {
 
 // ---- LayerNorm: one wave per row -----------------------------------------------------
-template <bool XBF, bool YF32>
+// DUAL: the decoder's norm1(x) and norm_y of the other side read the same rows, so one
+// pass writes y[b] = LN(x[b ^ xxor]; params b) and y2[b ^ 1] = LN(x[b]; params2 of b ^ 1)
+// from one set of row statistics (y2 only with xxor == 0).
+template <bool XBF, bool YF32, bool DUAL = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ x,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
                                                         void* __restrict__ y, int64_t rows,
                                                         int dim, float eps, int64_t sx,
                                                         int64_t sy, int64_t sp, int64_t pmod,
-                                                        int xxor) {
+                                                        int xxor, const float* __restrict__ gamma2 = nullptr,
+                                                        const float* __restrict__ beta2 = nullptr,
+                                                        void* __restrict__ y2 = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t b = blockIdx.y;
@@ -80,6 +85,18 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
 #pragma unroll
         for (int k = 0; k < 4; k++) ob[k] = f2bf(o[k]);
         *reinterpret_cast<bf16x4*>(yr + 4 * c4) = ob;
+      }
+      if constexpr (DUAL) {
+        const int64_t b2 = b ^ 1;
+        const int64_t pb2 = pmod > 0 ? b2 % pmod : b2;
+        const float* g2 = gamma2 + pb2 * sp;
+        const float* be2 = beta2 + pb2 * sp;
+        bf16x4 ob;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          ob[k] = f2bf((v[i][k] - mean) * rstd * g2[4 * c4 + k] + be2[4 * c4 + k]);
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(y2) + b2 * sy + row * dim + 4 * c4) =
+            ob;
       }
     }
   }
@@ -222,10 +239,23 @@ __global__ __launch_bounds__(256) void local_feat_kernel(const float* __restrict
   const float inv = 1.0f / sqrtf(n2);
   const int64_t pix = idx;
 #pragma unroll
-  for (int c = 0; c < 24; c++) {
-    const float dv = v[c] * inv;
-    if (desc) desc[pix * 24 + c] = dv;
-    if (desc16) desc16[pix * 24 + c] = (_Float16)dv;
+  for (int c = 0; c < 24; c++) v[c] *= inv;
+  // 16-B vector stores (96 B f32 / 48 B f16 per pixel, pixels of a row are contiguous)
+  if (desc) {
+    float4* d4 = reinterpret_cast<float4*>(desc + pix * 24);
+#pragma unroll
+    for (int q = 0; q < 6; q++) d4[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  }
+  if (desc16) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    h8* h = reinterpret_cast<h8*>(desc16 + pix * 24);
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      h8 o;
+#pragma unroll
+      for (int t = 0; t < 8; t++) o[t] = (_Float16)v[8 * q + t];
+      h[q] = o;
+    }
   }
   dconf[pix] = expf(f[24 * 256]);
 }
@@ -257,6 +287,24 @@ extern "C" int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_
     hipLaunchKernelGGL((layernorm_kernel<false, true>), grid, dim3(256), 0, s, d_x, d_gamma,
                        d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,
                        x_batch_xor);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_vit_layernorm_dual(const float* d_x, const float* d_gamma,
+                                      const float* d_beta, void* d_y, const float* d_gamma2,
+                                      const float* d_beta2, void* d_y2, int64_t rows,
+                                      int64_t dim, float eps, int64_t batch, int64_t stride_x,
+                                      int64_t stride_y, int64_t stride_param, int64_t param_mod,
+                                      void* stream) {
+  if (!d_x || !d_gamma || !d_beta || !d_y || !d_gamma2 || !d_beta2 || !d_y2 || rows <= 0 ||
+      batch <= 0 || batch % 2)
+    return M3S_ERR_INVALID_ARG;
+  if (dim % 4 || dim > 4096 || dim <= 0) return M3S_ERR_INVALID_ARG;
+  dim3 grid(m3s_div_up(rows, 4), (unsigned)batch);
+  hipLaunchKernelGGL((layernorm_kernel<false, false, true>), grid, dim3(256), 0,
+                     m3s_stream(stream), d_x, d_gamma, d_beta, d_y, rows, (int)dim, eps,
+                     stride_x, stride_y, stride_param, param_mod, 0, d_gamma2, d_beta2, d_y2);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }

@@ -111,6 +111,11 @@ class Ops:
             _p(x), int(x.dtype == BF16), _p(g), _p(b), _p(y), int(y_f32), rows, dim, LN_EPS,
             batch, sx, sy, sp, pmod, xor, self._s()), "vit_layernorm")
 
+    def ln_dual(self, x, g, b, y, g2, b2, y2, rows, dim, batch, sx, sy, sp, pmod=0):
+        _lib.check(self.lib.m3s_vit_layernorm_dual(
+            _p(x), _p(g), _p(b), _p(y), _p(g2), _p(b2), _p(y2), rows, dim, LN_EPS, batch, sx, sy,
+            sp, pmod, self._s()), "vit_layernorm_dual")
+
     def rope(self, t, ld, stride, pos, stride_pos, batch, S, heads, base):
         _lib.check(self.lib.m3s_vit_rope(_p(t), ld, stride, _p(pos), stride_pos, batch, S, heads,
                                          float(base), self._s()), "vit_rope")
@@ -410,14 +415,22 @@ class PairModel:
             # y_ = norm_y(previous output of the other side), then its k/v projection: on a
             # side stream, overlapping the self-attention half of the layer (the side chain
             # must read x before this layer's first residual update writes it)
-            with self._on(0):
-                o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1, pmod=4)
-                ev_lny = self._event()
+            if self.serial:
+                # norm1(x) and norm_y(other side's x) share the row statistics: one pass
+                o.ln_dual(x, P["ln1_g"], P["ln1_b"], xn, P["lny_g"], P["lny_b"], yn, S, D, Z,
+                          S * D, S * D, D, pmod=4)
                 o.gemm(yn, P["kv_w"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
                        sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4)
-                ev_kv = self._event()
+                ev_lny = ev_kv = None
+            else:
+                with self._on(0):
+                    o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1, pmod=4)
+                    ev_lny = self._event()
+                    o.gemm(yn, P["kv_w"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
+                           sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4)
+                    ev_kv = self._event()
+                o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
             # self-attention
-            o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
             o.gemm(xn, P["qkv_w"], qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
                    bias=P["qkv_b"], sBias=3 * D, rope=(rt, 2 * D, S), wmod=4)
             o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,

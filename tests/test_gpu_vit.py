@@ -279,3 +279,17 @@ def test_conv_fused_dpt_tail(ops, dev, H, W, b):
     ref_p, ref_c = torch.stack(ref_p), torch.stack(ref_c)
     assert _rel(pts, ref_p) < 1e-2
     assert _rel(conf, ref_c) < 1e-2
+
+
+def test_layernorm_dual(ops, dev):
+    """norm1(x[b]) → y[b] and norm_y(x[b]) → y2[b ^ 1] from one pass (decoder, z pairs)."""
+    g = torch.Generator(device=dev).manual_seed(14)
+    x = torch.randn(8, 768, 768, device=dev, generator=g) * 2 + 0.5
+    g1, b1, g2, b2 = (torch.randn(4, 768, device=dev, generator=g) for _ in range(4))
+    y = torch.empty(8, 768, 768, device=dev, dtype=torch.bfloat16)
+    y2 = torch.empty_like(y)
+    ops.ln_dual(x, g1, b1, y, g2, b2, y2, 768, 768, 8, 768 * 768, 768 * 768, 768, pmod=4)
+    ref1 = torch.stack([F.layer_norm(x[b], (768,), g1[b % 4], b1[b % 4], 1e-6) for b in range(8)])
+    ref2 = torch.stack([F.layer_norm(x[b ^ 1], (768,), g2[b % 4], b2[b % 4], 1e-6)
+                        for b in range(8)])
+    assert _rel(y, ref1) < 1e-2 and _rel(y2, ref2) < 1e-2
