@@ -810,7 +810,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
 // ---------------------------------------------------------------------------------------
 // tile configurations
 // ---------------------------------------------------------------------------------------
-enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7 };
+enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7, T96 = 8, T96O2 = 9 };
 
 // Epilogue flag sets compiled as straight-line variants (8-wide vector path), per mode:
 //   GEMM: bf16 out, +RoPE, +GELU, f32 residual → f32, f32 out;  conv: bf16 out, +bf16
@@ -1010,7 +1010,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     else if (tiles128 >= 256 && tiles128 <= 512 && nk <= 16) cfg = T128O2;
     else cfg = T128;
   }
-  if (cfg != T128 && cfg != T64 && cfg != T128K32 && cfg != T256 && cfg != T128O2) cfg = T128;
+  if (cfg < 1 || cfg > 9 || cfg == 4 || cfg == 5) cfg = T128;
   if (conv && d->Cin % 64 != 0) cfg = T128K32;  // tap-uniform K-tiles need Cin % BK == 0
   if (!conv && cfg == T128K32) cfg = T128;
   if (conv && d->Cin % 64 == 0 && cfg == T128K32) cfg = T128;
@@ -1028,6 +1028,9 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     case T128K32: return launch<128, 128, 32, 2, 2, 4, 2>(a, d->batch, s);
     case T256: return launch<256, 128, 64, 2, 2, 3, 1>(a, d->batch, s);
     case T128O2: return launch<128, 128, 64, 2, 2, 2, 2>(a, d->batch, s);
+    // 96 x 128 tiles (waves 1 x 4, each 96 x 32): 768-token problems tile to 8 bands
+    case T96: return launch<96, 128, 64, 1, 4, 3, 1>(a, d->batch, s);
+    case T96O2: return launch<96, 128, 64, 1, 4, 2, 2>(a, d->batch, s);
     default: return launch<64, 128, 64, 2, 2, 3, 2>(a, d->batch, s);
   }
 }

@@ -66,16 +66,24 @@ class Tracker:
     def track(self, img, T_WCf_init=None):
         """One frame.  Returns dict(new_kf, lost, T_WCf, idx_f2k, match_frac, info, ...);
         the scalar flags are device tensors."""
+        out = self.model.pair(img, feat_j=self.kf.feat)
+        return self.track_outputs(out, T_WCf_init)
+
+    def track_outputs(self, out, T_WCf_init=None):
+        """tracker2.py:127-270 on the pair-inference outputs X [2,H,W,3] (ii, ji), C [2,H,W],
+        D16 f16 [2,H,W,24], Q [2,H,W] — everything after monst3r_asymmetric_inference.
+        Host-sync free: where the reference returns early (match_frac < min_match_frac,
+        :196-198; Cholesky failure, :234-236) the frame is `lost` and the keyframe fusion
+        is masked off on the device instead of skipped."""
         cfg_t = self.cfg["tracking"]
         kf = self.kf
-        out = self.model.pair(img, feat_j=kf.feat)
         Xii, Xji = out["X"][0:1], out["X"][1:2]
         H, W = Xii.shape[1:3]
         n = H * W
         # matching.match(Xii, Xji, Dii, Dji, idx_init)  (monst3r_utils.py:498-499)
         idx, valid_match = M.match(Xii, Xji, out["D16"][0:1], out["D16"][1:2], self.idx_f2k,
                                    self.cfg["matching"])
-        self.idx_f2k.copy_(idx)
+        self.idx_f2k.copy_(idx)                            # tracker2.py:127
         idx = idx[0]
         valid_match = valid_match[0]                       # [N,1]
         Qff = out["Q"][0].reshape(n, 1)
@@ -97,18 +105,20 @@ class Tracker:
         T_WCf0 = kf.T_WC if T_WCf_init is None else T_WCf_init
         T_WCf, T_CkCf, info = T.opt_pose_ray_dist_sim3(Xf, kf.X_canon, T_WCf0, kf.T_WC, Qk,
                                                        valid_opt, cfg_t, check=False)
+        lost = (match_frac < cfg_t["min_match_frac"]) | (info[1] != 0)
+        ok = (~lost).float()
         # keyframe.update_pointmap(T_CkCf.act(Xkf), Ckf) — weighted_pointmap (frame.py:105-109)
         Xkk = sim3_act(T_CkCf, Xkf)
-        kf.X_canon.copy_((kf.C * kf.X_canon + Ckf * Xkk) / (kf.C + Ckf))
-        kf.C.add_(Ckf)
-        kf.N.add_(1.0)
+        fused = (kf.C * kf.X_canon + Ckf * Xkk) / (kf.C + Ckf)
+        kf.X_canon.copy_(torch.where(lost, kf.X_canon, fused))
+        kf.C.add_(Ckf * ok)
+        kf.N.add_(ok)
         # keyframe selection (tracker2.py:246-257)
         match_frac_k = valid_kf.float().mean()
         sel = torch.zeros(n, dtype=torch.int32, device=idx.device)
         sel.index_add_(0, idx, valid_match[:, 0].int())    # |unique(idx[valid])|, no sort/sync
         unique_frac_f = (sel > 0).sum().float() / n
-        new_kf = torch.minimum(match_frac_k, unique_frac_f) < cfg_t["match_frac_thresh"]
-        lost = (match_frac < cfg_t["min_match_frac"]) | (info[1] != 0)
+        new_kf = (torch.minimum(match_frac_k, unique_frac_f) < cfg_t["match_frac_thresh"]) & ~lost
         return dict(new_kf=new_kf, lost=lost, T_WCf=T_WCf, T_CkCf=T_CkCf, idx_f2k=idx,
                     valid_match=valid_match, match_frac=match_frac, info=info,
-                    feat_i=out["feat_i"], pair=out)
+                    feat_i=out.get("feat_i"), pair=out)

@@ -1,0 +1,66 @@
+"""GPU: the per-frame tracking glue of FrameTracker2.track (tracker2.py:127-270) over a
+synthetic sequence (analytic pointmaps instead of the random-weight ViT):
+frame t is tracked against the keyframe with the previous frame's matches as the
+iterative-projection seed (tracker2.py:127), the keyframe pointmap is fused frame after
+frame, and every per-frame result is compared with the numpy/C oracle of the same glue
+(oracle/frontend_ref.py): match indices and validity bit-exact, poses |dT| <= 1e-4, fused
+keyframe pointmap / confidence / count and the lost / new-keyframe decisions."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+H, W = 96, 128
+
+
+def _frames(T=6, seed=0):
+    from monst3r_slam_amd import synthetic as syn
+    rng = np.random.default_rng(seed)
+    out = []
+    for t in range(T):
+        X11, X21, D11, D21 = syn.pair(H, W, seed=seed + t, shift_px=(0.6 + 0.3 * t, -0.4 + 0.2 * t))
+        X = np.stack([X11, X21]).astype(np.float32)
+        C = (1.0 + np.exp(rng.normal(1.0, 0.5, size=(2, H, W)))).astype(np.float32)
+        Q = (1.0 + np.exp(rng.normal(1.0, 0.5, size=(2, H, W)))).astype(np.float32)
+        if t == 3:
+            Q[:] = 1.2      # all Qk <= Q_conf: match_frac 0 → the frame is lost
+        D = np.stack([D11, D21]).astype(np.float16)
+        out.append((X, C, D, Q))
+    return out
+
+
+def test_tracking_sequence_vs_oracle(dev):
+    from monst3r_slam_amd import synthetic as syn
+    from monst3r_slam_amd.config import default_config
+    from monst3r_slam_amd.frontend import Tracker
+    from oracle import frontend_ref as FR
+    cfg = default_config()
+    frames = _frames()
+    Xk0 = syn.backproject(syn.depth_surface(H, W, 5), syn.intrinsics(H, W)).reshape(-1, 3)
+    Ck0 = np.full((H * W, 1), 2.0, np.float32)
+    Tk = np.array([0.1, -0.05, 0.02, 0, 0, 0, 1, 1.0], np.float32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    tr = Tracker(model=None, cfg=cfg)
+    tr.add_keyframe(None, t(Tk), X=t(Xk0.astype(np.float32)), C=t(Ck0),
+                    feat=torch.zeros(1, device=dev))
+    kf_ref = FR.Keyframe(Xk0, Ck0, Tk)
+    idx_ref = None
+    for step, (X, C, D, Q) in enumerate(frames):
+        out = dict(X=t(X), C=t(C), D16=t(D), Q=t(Q))
+        res = tr.track_outputs(out)
+        ref = FR.track_outputs(X, C, D, Q, kf_ref, idx_ref, cfg["matching"], cfg["tracking"])
+        idx_ref = ref["idx"][None]
+        torch.cuda.synchronize()
+        assert np.array_equal(res["idx_f2k"].cpu().numpy(), ref["idx"]), step
+        assert np.array_equal(res["valid_match"].cpu().numpy(), ref["valid"]), step
+        assert bool(res["lost"]) == ref["lost"], step
+        if ref["lost"]:
+            assert step == 3
+        else:
+            dT = np.abs(res["T_WCf"].cpu().numpy() - ref["T_WCf"]).max()
+            assert dT <= 1e-4, (step, dT)
+            assert bool(res["new_kf"]) == ref["new_kf"], step
+        np.testing.assert_allclose(tr.kf.X_canon.cpu().numpy(), kf_ref.X_canon, rtol=1e-4,
+                                   atol=1e-5)
+        np.testing.assert_allclose(tr.kf.C.cpu().numpy(), kf_ref.C, rtol=1e-6)
+        assert float(tr.kf.N) == kf_ref.N, step

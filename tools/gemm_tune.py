@@ -87,7 +87,7 @@ for name, M, N, K, b, kind in gemms:
     def fn_for(split, A=A, B=B, C=C, M=M, N=N, K=K, b=b, flags=flags, R=R, bias=bias):
         return lambda: ops.gemm(A, B, C, M, N, K, b, sA=M * K, sB=N * K, sC=M * N, bias=bias,
                                 sBias=N, R=R, sR=M * N, flags=flags, split_k=split)
-    cfgs = [(1, 1), (2, 1), (7, 1), (7, 2)] if quick else [(1, 1), (1, 2), (1, 4), (2, 1), (2, 2), (4, 1), (4, 2),
+    cfgs = [(1, 1), (2, 1), (7, 1), (8, 1), (9, 1), (8, 2)] if quick else [(1, 1), (1, 2), (1, 4), (2, 1), (2, 2), (4, 1), (4, 2),
                                            (5, 1), (5, 2), (6, 1), (6, 2), (6, 4)]
     run(f"{name} {M}x{N}x{K}x{b}", 2.0 * M * N * K * b, fn_for, cfgs,
         ref=lambda A=A, B=B: torch.bmm(A, B.transpose(1, 2)))
