@@ -178,10 +178,14 @@ enum {
   M3S_EPI_CONVT = 128,    /* scatter rows/cols as ConvTranspose(k=s, stride=s) */
   M3S_EPI_ROPE = 256,     /* 2D RoPE on columns < rope_cols (head dim 64), after bias;
                              not combined with a residual or CONVT                   */
-  M3S_EPI_DPT_OUT = 512   /* DPT regression tail fused into a conv with N = 128 (one tile
+  M3S_EPI_DPT_OUT = 512,  /* DPT regression tail fused into a conv with N = 128 (one tile
                              spans the row): relu(acc + bias) · W4ᵀ + b4 (1x1, 128 → 4), then
                              reg_dense_depth / conf (d3r/heads/postprocess.py:10-58) written
                              to dpt_pts / dpt_conf; C is not written               */
+  M3S_IN_FP8 = 1024,      /* A and B are OCP fp8 e4m3 (1 byte; K, lda, ldb, strides % 16
+                             == 0; GEMM mode only): scaled-MFMA 32x32x64 path; the f32
+                             accumulator is multiplied by col_scale[n] before the epilogue */
+  M3S_EPI_OUT_FP8 = 2048  /* store C as OCP fp8 e4m3 (saturated to ±448)           */
 };
 
 typedef struct {
@@ -206,6 +210,9 @@ typedef struct {
   float* dpt_pts;                          /* DPT_OUT: f32 [batch][M][3]               */
   float* dpt_conf;                         /* DPT_OUT: f32 [batch][M]                  */
   float dpt_conf_min;                      /* DPT_OUT: conf = conf_min + exp(c)        */
+  const float* col_scale;                  /* IN_FP8: f32 [N] per weight batch (dequant of
+                                              A·B: activation scale x weight row scale) */
+  int64_t stride_col_scale;                /* IN_FP8: elements between batches (weight_mod) */
 } m3s_gemm_desc;
 
 /* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 8 == 0; conv: Cin % 32 == 0.

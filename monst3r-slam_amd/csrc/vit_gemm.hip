@@ -26,6 +26,7 @@
 // XCD-aware bijective tile order (cdna_hip_programming.md T1).
 #include <stdlib.h>
 #include <algorithm>
+#include <type_traits>
 #include "vit_common.h"
 
 namespace {
@@ -63,6 +64,8 @@ struct Args {
   float* dpt_pts;
   float* dpt_conf;
   float dpt_conf_min;
+  const float* cscale;     // IN_FP8: per-column dequant scale, batch stride sCscale
+  int64_t sCscale;
 };
 
 // ---------------------------------------------------------------------------------------
@@ -86,7 +89,8 @@ __device__ __forceinline__ Epi make_epi(const Args& a, int g) {
   const int64_t gw = a.wmod > 0 ? g % a.wmod : g;
   e.bias = (a.bias && (a.flags & M3S_EPI_BIAS)) ? a.bias + gw * a.sBias : nullptr;
   e.R = a.R ? reinterpret_cast<const char*>(a.R) + (int64_t)g * a.sR * (res32 ? 4 : 2) : nullptr;
-  e.C = reinterpret_cast<char*>(a.C) + (int64_t)g * a.sC * (out32 ? 4 : 2);
+  const int osz = out32 ? 4 : ((a.flags & M3S_EPI_OUT_FP8) ? 1 : 2);
+  e.C = reinterpret_cast<char*>(a.C) + (int64_t)g * a.sC * osz;
   e.flags = a.flags;
   e.ldc = a.ldc;
   e.ldr = a.ldr;
@@ -176,6 +180,9 @@ __device__ __forceinline__ void epi_vec8(const Epi& e, float* v, float* p, int m
     float* c = reinterpret_cast<float*>(e.C) + off;
     *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else if (e.flags & M3S_EPI_OUT_FP8) {
+    *reinterpret_cast<uint2*>(e.C + off) = make_uint2(pack4_fp8(v[0], v[1], v[2], v[3]),
+                                                      pack4_fp8(v[4], v[5], v[6], v[7]));
   } else {
     bf16x8 o;
 #pragma unroll
@@ -201,6 +208,7 @@ __device__ __forceinline__ void epi_one(const Epi& e, float v, float p, int m, i
     v += bf2f(reinterpret_cast<const bf16_t*>(e.R)[(int64_t)m * e.ldr + n]);
   if (e.flags & M3S_EPI_RELU) v = fmaxf(v, 0.f);
   if (e.flags & M3S_EPI_OUT_F32) reinterpret_cast<float*>(e.C)[off] = v;
+  else if (e.flags & M3S_EPI_OUT_FP8) e.C[off] = (char)(pack4_fp8(v, 0.f, 0.f, 0.f) & 0xff);
   else reinterpret_cast<bf16_t*>(e.C)[off] = f2bf(v);
 }
 
@@ -262,8 +270,12 @@ __device__ long long* g_m3s_stamps;
 
 // EPI >= 0: the epilogue flag set, fixed at compile time (straight-line epilogue code, and
 // the 8-wide vector path assumed); EPI < 0: flags read at run time.
+// F8: A and B hold OCP fp8 e4m3 bytes.  K / lda / ldb / strides then arrive in 2-byte units
+// (host halves them), so the LDS-DMA ring, swizzle and row bytes are those of the bf16
+// kernel; only the fragments differ: a 32x32x64 scaled MFMA consumes 64 bytes of a row per
+// phase, lane half h holding bytes [32h, 32h + 32) (two swizzled 16-B chunks).
 template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, bool SPLIT,
-          int EPI>
+          int EPI, bool F8 = false>
 __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
   M3S_T(t_start);
   using C = Cfg<BM, BN, BK, STAGES>;
@@ -416,31 +428,55 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
   // vmcnt + barrier: the MFMAs keep the matrix pipe busy meanwhile) and reads tile kt+1's
   // first fragments.  The steady-state loop (every tile prefetches) is branch-free, so the
   // scheduler sees whole phases; sched_group_barrier pins the read / DMA / MFMA order.
-  constexpr int KK = BK / 16;
-  constexpr int NR = TM + TN;                 // ds_read_b128 per phase
+  constexpr int KK = F8 ? BK / 32 : BK / 16;  // MFMA phases per K-tile
+  constexpr int NR = (TM + TN) * (F8 ? 2 : 1); // ds_read_b128 per phase
   constexpr int NM = TM * TN;                 // MFMAs per phase
-  bf16x8 fa[2][TM], fb[2][TN];
+  using frag_t = std::conditional_t<F8, i32x8, bf16x8>;
+  frag_t fa[2][TM], fb[2][TN];
   auto read_frags = [&](int buf, const char* sA, int kk) {
     const char* sB = sA + C::A_BYTES;
-    const int slot = ((kk * 2 + fh) ^ fsw) * 16;
+    if constexpr (F8) {
+      const int s0 = ((kk * 4 + 2 * fh) ^ fsw) * 16, s1 = ((kk * 4 + 2 * fh + 1) ^ fsw) * 16;
 #pragma unroll
-    for (int i = 0; i < TM; i++) {
-      fa[buf][i] = *reinterpret_cast<const bf16x8*>(
-          sA + (wm * (BM / WM) + i * 32 + fr) * (BK * 2) + slot);
-      if (MODE == 2) fa[buf][i] = relu_frag(fa[buf][i]);
+      for (int i = 0; i < TM; i++) {
+        const char* row = sA + (wm * (BM / WM) + i * 32 + fr) * (BK * 2);
+        const int4 lo = *reinterpret_cast<const int4*>(row + s0);
+        const int4 hi = *reinterpret_cast<const int4*>(row + s1);
+        fa[buf][i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      }
+#pragma unroll
+      for (int j = 0; j < TN; j++) {
+        const char* row = sB + (wn * (BN / WN) + j * 32 + fr) * (BK * 2);
+        const int4 lo = *reinterpret_cast<const int4*>(row + s0);
+        const int4 hi = *reinterpret_cast<const int4*>(row + s1);
+        fb[buf][j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      }
+    } else {
+      const int slot = ((kk * 2 + fh) ^ fsw) * 16;
+#pragma unroll
+      for (int i = 0; i < TM; i++) {
+        fa[buf][i] = *reinterpret_cast<const bf16x8*>(
+            sA + (wm * (BM / WM) + i * 32 + fr) * (BK * 2) + slot);
+        if (MODE == 2) fa[buf][i] = relu_frag(fa[buf][i]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; j++)
+        fb[buf][j] = *reinterpret_cast<const bf16x8*>(
+            sB + (wn * (BN / WN) + j * 32 + fr) * (BK * 2) + slot);
     }
-#pragma unroll
-    for (int j = 0; j < TN; j++)
-      fb[buf][j] = *reinterpret_cast<const bf16x8*>(
-          sB + (wn * (BN / WN) + j * 32 + fr) * (BK * 2) + slot);
   };
   auto mfmas = [&](int cur) {
 #pragma unroll
     for (int i = 0; i < TM; i++)
 #pragma unroll
-      for (int j = 0; j < TN; j++)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][i], fb[cur][j], acc[i][j],
-                                                            0, 0, 0);
+      for (int j = 0; j < TN; j++) {
+        if constexpr (F8)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+              fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0, 0, 0, 0);
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][i], fb[cur][j], acc[i][j],
+                                                              0, 0, 0);
+      }
   };
   auto stage_of = [&](int t) { return lds + (t % STAGES) * C::ST_BYTES; };
   if (nk > 0) {
@@ -517,6 +553,18 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
     }
   }
   M3S_T(t_loop);
+  if constexpr (F8) {  // dequant: acc(i, j) *= col_scale[n] (n = this lane's column)
+    const float* cs_g = a.cscale + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sCscale;
+#pragma unroll
+    for (int j = 0; j < TN; j++) {
+      const int n = n0 + wn * (BN / WN) + j * 32 + fr;
+      const float sc = n < a.N ? cs_g[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; i++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc[i][j][r] *= sc;
+    }
+  }
 
   // ---- epilogue through LDS: f32 tile [BM][CST] ----
   constexpr int VPR = BN / 8;                 // 8-column vectors per row
@@ -725,6 +773,9 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
           float* cp = reinterpret_cast<float*>(e.C) + off;
           *reinterpret_cast<float4*>(cp) = make_float4(x[0], x[1], x[2], x[3]);
           *reinterpret_cast<float4*>(cp + 4) = make_float4(x[4], x[5], x[6], x[7]);
+        } else if (fl & M3S_EPI_OUT_FP8) {
+          *reinterpret_cast<uint2*>(e.C + off) = make_uint2(pack4_fp8(x[0], x[1], x[2], x[3]),
+                                                            pack4_fp8(x[4], x[5], x[6], x[7]));
         } else {
           bf16x8 o;
 #pragma unroll
@@ -816,19 +867,40 @@ enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7, T96 = 8, T9
 //   GEMM: bf16 out, +RoPE, +GELU, f32 residual → f32, f32 out;  conv: bf16 out, +bf16
 //   residual, +ReLU.  Any other combination (or an unaligned shape) runs the generic
 //   run-time-flag epilogue.  Each set exists with and without bias.
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, int E>
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, int E,
+          bool F8 = false>
 bool try_epi(Args& a, dim3 grid, hipStream_t s, int key) {
   if (key == E) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, E>), grid,
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, E, F8>), grid,
                        dim3(NT), 0, s, a);
     return true;
   }
   if (key == (E | M3S_EPI_BIAS)) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, E | M3S_EPI_BIAS>),
-                       grid, dim3(NT), 0, s, a);
+    hipLaunchKernelGGL(
+        (gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, E | M3S_EPI_BIAS, F8>), grid,
+        dim3(NT), 0, s, a);
     return true;
   }
   return false;
+}
+
+// fp8 operands (GEMM mode): the epilogue sets the ViT uses — qkv / q / kv (+RoPE), fc1
+// (+GELU, fp8 out for the next fp8 GEMM), proj / fc2 (f32 residual), plain bf16 / f32
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC>
+void launch_main_f8(Args& a, dim3 grid, hipStream_t s) {
+  const int key = a.flags & ~(M3S_IN_FP8 | (a.bias ? 0 : M3S_EPI_BIAS));
+  if (a.vec) {
+    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_ROPE, true>(a, grid, s, key)) return;
+    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_GELU | M3S_EPI_OUT_FP8, true>(
+            a, grid, s, key))
+      return;
+    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, true>(
+            a, grid, s, key))
+      return;
+    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, 0, true>(a, grid, s, key)) return;
+  }
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, false, -1, true>), grid,
+                     dim3(NT), 0, s, a);
 }
 
 template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE>
@@ -857,7 +929,7 @@ void launch_main(Args& a, dim3 grid, hipStream_t s) {
                      dim3(NT), 0, s, a);
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC>
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, bool F8 = false>
 int launch(Args& a, int batch, hipStream_t s) {
   a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = (a.N + BN - 1) / BN;
@@ -881,12 +953,14 @@ int launch(Args& a, int batch, hipStream_t s) {
     a.nmajor = 0;
   }
   if (split) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true, -1>), grid, dim3(NT),
-                       0, s, a);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true, -1, F8>), grid,
+                       dim3(NT), 0, s, a);
     M3S_LAUNCH_CHECK();
     const int64_t nv = (int64_t)a.M * ((a.N + 7) / 8);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(m3s_div_up(nv, 256), (unsigned)batch),
                        dim3(256), 0, s, a);
+  } else if constexpr (F8) {
+    launch_main_f8<BM, BN, BK, WM, WN, STAGES, OCC>(a, grid, s);
   } else if (a.mode == 0) {
     launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 0>(a, grid, s);
   } else if (a.flags & M3S_PRO_RELU) {
@@ -930,10 +1004,18 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   if ((d->mode == 0 && d->lda % 8) || d->ldb % 8 || d->strideA % 8 || d->strideB % 8)
     return M3S_ERR_INVALID_ARG;
   if (d->batch > 65535) return M3S_ERR_TOO_LARGE;
+  const bool f8 = d->flags & M3S_IN_FP8;
+  if (f8 && (d->mode != 0 || d->K % 16 || d->lda % 16 || d->ldb % 16 || d->strideA % 16 ||
+             d->strideB % 16 || !d->col_scale || (d->flags & M3S_EPI_CONVT)))
+    return M3S_ERR_INVALID_ARG;
+  if ((d->flags & M3S_EPI_OUT_FP8) && (d->flags & M3S_EPI_OUT_F32)) return M3S_ERR_INVALID_ARG;
+  // fp8 operands are addressed in 2-byte units (the bf16 kernel's byte layout, §F8)
+  const int64_t eK = f8 ? d->K / 2 : d->K, elda = f8 ? d->lda / 2 : d->lda;
+  const int64_t eldb = f8 ? d->ldb / 2 : d->ldb;
   // buffer addressing: each operand's per-batch span must fit a 31-bit byte offset
-  const int64_t spanA = d->mode == 0 ? ((int64_t)(d->M - 1) * d->lda + d->K) * 2
+  const int64_t spanA = d->mode == 0 ? ((int64_t)(d->M - 1) * elda + eK) * 2
                                      : (int64_t)d->Hin * d->Win * d->Cin * 2;
-  const int64_t spanB = ((int64_t)(d->N - 1) * d->ldb + d->K) * 2;
+  const int64_t spanB = ((int64_t)(d->N - 1) * eldb + eK) * 2;
   if (spanA >= NUM_RECORDS || spanB >= NUM_RECORDS) return M3S_ERR_TOO_LARGE;
   Args a;
   a.A = reinterpret_cast<const bf16_t*>(d->A);
@@ -975,6 +1057,15 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   a.dpt_pts = d->dpt_pts;
   a.dpt_conf = d->dpt_conf;
   a.dpt_conf_min = d->dpt_conf_min;
+  a.cscale = d->col_scale;
+  a.sCscale = d->stride_col_scale;
+  if (f8) {
+    a.K = (int)eK;
+    a.lda = elda;
+    a.ldb = eldb;
+    a.sA = d->strideA / 2;
+    a.sB = d->strideB / 2;
+  }
   const bool out32 = d->flags & M3S_EPI_OUT_F32;
   const bool has_bias = d->bias && (d->flags & M3S_EPI_BIAS);
   a.vec = d->N % 8 == 0 && d->ldc % 8 == 0 && d->strideC % 8 == 0 && aligned16(d->C) &&
@@ -998,7 +1089,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   // 64x128, or 256x128 once the grid has several waves of workgroups.
   const bool conv = d->mode == 1;
   const int64_t tiles128 = (int64_t)((d->M + 127) / 128) * ((d->N + 127) / 128) * d->batch;
-  const int nk = (d->K + 63) / 64;
+  const int nk = (int)((eK + 63) / 64);     // K-tiles of 128 bytes per row
   int cfg = forced_tile();
   if (cfg == 0) {
     // measured on the pair shapes (tools/gemm_tune.py): 2 x 128^2 blocks per CU win for
@@ -1023,6 +1114,13 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   const bool can_split = !conv && !(d->flags & M3S_EPI_CONVT) && d->workspace &&
                          (int64_t)splits * d->batch * d->M * d->N * 4 <= d->workspace_bytes;
   if (splits > 1 && can_split) a.splits = splits;
+  if (f8) {
+    switch (cfg) {
+      case T64: return launch<64, 128, 64, 2, 2, 3, 2, true>(a, d->batch, s);
+      case T128O2: return launch<128, 128, 64, 2, 2, 2, 2, true>(a, d->batch, s);
+      default: return launch<128, 128, 64, 2, 2, 3, 1, true>(a, d->batch, s);
+    }
+  }
   switch (cfg) {
     case T128: return launch<128, 128, 64, 2, 2, 3, 1>(a, d->batch, s);
     case T128K32: return launch<128, 128, 32, 2, 2, 4, 2>(a, d->batch, s);

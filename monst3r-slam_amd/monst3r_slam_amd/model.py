@@ -70,7 +70,10 @@ class Ops:
 
     def gemm(self, A, B, C, M, N, K, batch=1, *, lda=None, ldb=None, ldc=None, sA=0, sB=0,
              sC=0, bias=None, sBias=0, R=None, ldr=None, sR=0, flags=0, conv=None, convt=None,
-             rope=None, split_k=0, wmod=0, dpt=None):
+             rope=None, split_k=0, wmod=0, dpt=None, fp8=None, out_fp8=False):
+        """fp8 = (col_scale f32 [.., N], stride): A and B are OCP e4m3 bytes (torch
+        float8_e4m3fn / uint8), the f32 accumulator is scaled per column; out_fp8: C is
+        stored as e4m3."""
         d = _lib.GemmDesc()
         d.A, d.lda, d.strideA = _p(A), lda if lda is not None else K, sA
         d.B, d.ldb, d.strideB = _p(B), ldb if ldb is not None else K, sB
@@ -81,6 +84,11 @@ class Ops:
         ws = self.ws
         d.workspace, d.workspace_bytes, d.split_k = _p(ws), ws.numel(), split_k
         d.weight_mod = wmod
+        if fp8 is not None:
+            d.flags |= _lib.IN_FP8
+            d.col_scale, d.stride_col_scale = _p(fp8[0]), fp8[1]
+        if out_fp8:
+            d.flags |= _lib.EPI_OUT_FP8
         if dpt is not None:  # fused DPT tail: (W4 [h][4][128], b4 [h][4], pts, conf, conf_min)
             d.flags |= _lib.EPI_DPT_OUT
             d.dpt_w4, d.dpt_b4, d.dpt_pts, d.dpt_conf = (_p(t) for t in dpt[:4])

@@ -293,3 +293,59 @@ def test_layernorm_dual(ops, dev):
     ref2 = torch.stack([F.layer_norm(x[b ^ 1], (768,), g2[b % 4], b2[b % 4], 1e-6)
                         for b in range(8)])
     assert _rel(y, ref1) < 1e-2 and _rel(y2, ref2) < 1e-2
+
+
+def _fp8(t):
+    return t.clamp(-448, 448).to(torch.float8_e4m3fn)
+
+
+@pytest.mark.parametrize("M,N,K,batch,mode", [(768, 3072, 1024, 1, "gelu8"), (768, 768, 768, 4, "res"),
+                                              (200, 384, 256, 2, "plain"), (768, 1024, 4096, 1, "res"),
+                                              (768, 2304, 768, 4, "rope")])
+def test_gemm_fp8(ops, dev, M, N, K, batch, mode):
+    """OCP e4m3 operands on the scaled 32x32x64 MFMA, per-column dequant scale, the ViT
+    epilogue sets (GELU → fp8 out, f32 residual incl. split-K, RoPE), weight_mod batches.
+    Reference: the same e4m3 values in fp32 (products exact, f32 sums: tolerance 1e-3;
+    fp8 outputs compared after the same e4m3 rounding of the reference: 1 ulp ≈ 2^-3)."""
+    from monst3r_slam_amd import _lib
+    from oracle import vit_ref as V
+    g = torch.Generator(device=dev).manual_seed(21)
+    A = _fp8(torch.randn(batch, M, K, device=dev, generator=g))
+    W = torch.randn(2, N, K, device=dev, generator=g) / K ** 0.5
+    s = W.abs().amax(-1) / 448.0                                 # per output row
+    B = _fp8(W / s[..., None])
+    bias = torch.randn(2, N, device=dev, generator=g) * 0.1
+    cs = (s * 0.5).contiguous()                                  # activation scale 0.5
+    ref = torch.stack([(A[z].float() @ B[z % 2].float().t()) * cs[z % 2] + bias[z % 2]
+                       for z in range(batch)])
+    kw = dict(sA=M * K, sB=N * K, sC=M * N, bias=bias, sBias=N, wmod=2, fp8=(cs, N))
+    if mode == "gelu8":
+        C = torch.empty(batch, M, N, device=dev, dtype=torch.uint8)
+        ops.gemm(A.view(torch.uint8), B.view(torch.uint8), C, M, N, K, batch,
+                 flags=_lib.EPI_GELU, out_fp8=True, **kw)
+        out = C.view(torch.float8_e4m3fn).float()
+        refq = _fp8(F.gelu(ref)).float()
+        assert (out - refq).abs().max() <= 0.13 * refq.abs().max(), float((out - refq).abs().max())
+        assert float((out - refq).abs().mean()) < 2e-3 * float(refq.abs().max())
+    elif mode == "res":
+        x = torch.randn(batch, M, N, device=dev, generator=g)
+        ref = ref + x
+        ops.gemm(A.view(torch.uint8), B.view(torch.uint8), x, M, N, K, batch, R=x, sR=M * N,
+                 flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, **kw)
+        assert _rel(x, ref) < 1e-3
+    elif mode == "rope":
+        C = torch.empty(batch, M, N, device=dev, dtype=torch.bfloat16)
+        pos = V.positions(1, 24, 32, dev)[0].contiguous()
+        tab = ops.rope_table(pos, 100.0)
+        ops.gemm(A.view(torch.uint8), B.view(torch.uint8), C, M, N, K, batch, rope=(tab, 2 * N // 3, M),
+                 **kw)
+        y = ref.reshape(batch, M, 3, N // 192, 64)
+        posb = V.positions(batch, 24, 32, dev)
+        r2 = y.clone()
+        for j in (0, 1):
+            r2[:, :, j] = V.rope2d(y[:, :, j].transpose(1, 2), posb, 100.0).transpose(1, 2)
+        assert _rel(C, r2.reshape(batch, M, N)) < 1e-2
+    else:
+        C = torch.empty(batch, M, N, device=dev, dtype=torch.bfloat16)
+        ops.gemm(A.view(torch.uint8), B.view(torch.uint8), C, M, N, K, batch, **kw)
+        assert _rel(C, ref) < 1e-2
