@@ -228,22 +228,24 @@ int m3s_vit_gemm(const m3s_gemm_desc* desc, void* stream);
 int m3s_vit_rope_table(const int64_t* d_pos, int64_t tokens, float base, float* d_table,
                        void* stream);
 
-/* LayerNorm over the last dim (eps), x f32/bf16 [rows][dim] → y bf16 or f32
- * (x_is_bf16 / y_is_f32 flags); batch strides in elements.  dim ≤ 4096, dim % 4 == 0.
+/* LayerNorm over the last dim (eps), x f32/bf16 [rows][dim] → y (x_is_bf16 flag;
+ * y_type 0 bf16, 1 f32, 2 OCP fp8 e4m3 saturated to ±448 — the A operand of the
+ * M3S_IN_FP8 GEMMs); batch strides in elements.  dim ≤ 4096, dim % 4 == 0.
  * param_mod > 0: batch b uses gamma/beta of batch b % param_mod.
  * Batch b of y normalises batch (b ^ x_batch_xor) of x: with x_batch_xor = 1 the
  * decoder's norm_y(other side) (croco/blocks.py:187) runs for both sides in one launch. */
 int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_gamma,
-                      const float* d_beta, void* d_y, int y_is_f32, int64_t rows, int64_t dim,
+                      const float* d_beta, void* d_y, int y_type, int64_t rows, int64_t dim,
                       float eps, int64_t batch, int64_t stride_x, int64_t stride_y,
                       int64_t stride_param, int64_t param_mod, int x_batch_xor, void* stream);
 
 /* Two LayerNorms of the same f32 rows in one pass (the decoder's norm1 of x and norm_y of
  * the other side, croco/blocks.py:184-187): y[b] = LN(x[b]; gamma/beta of b) and
- * y2[b ^ 1] = LN(x[b]; gamma2/beta2 of b ^ 1), both bf16; batch even; param_mod as above. */
+ * y2[b ^ 1] = LN(x[b]; gamma2/beta2 of b ^ 1), both bf16 (y_fp8 = 0) or both e4m3
+ * (y_fp8 = 1); batch even; param_mod as above. */
 int m3s_vit_layernorm_dual(const float* d_x, const float* d_gamma, const float* d_beta,
                            void* d_y, const float* d_gamma2, const float* d_beta2, void* d_y2,
-                           int64_t rows, int64_t dim, float eps, int64_t batch,
+                           int y_fp8, int64_t rows, int64_t dim, float eps, int64_t batch,
                            int64_t stride_x, int64_t stride_y, int64_t stride_param,
                            int64_t param_mod, void* stream);
 
@@ -256,7 +258,8 @@ int m3s_vit_rope(void* d_t, int64_t ld, int64_t stride, const int64_t* d_pos,
 
 /* Multi-head attention, head dim 64 (croco/blocks.py:81-112 self, :132-169 cross):
  * o = softmax(q k^T / 8) v.  q [B][Sq] rows of ld_q bf16 (head h at column h*64), k,v
- * [B][Sk] rows of ld_kv; RoPE already applied (m3s_vit_rope).  o bf16 [B][Sq][ld_o].
+ * [B][Sk] rows of ld_kv; RoPE already applied (m3s_vit_rope).  o [B][Sq][ld_o]: bf16,
+ * or OCP e4m3 bytes saturated to ±448 when o_fp8 (the fp8 output projection's A operand).
  * The pos/rope arguments are reserved (must be NULL/0).  With a device workspace (16-B
  * aligned, optional) a small (query tile x head x batch) grid is split along the keys
  * (flash-decoding): per-split unnormalised O, max and sum in f32, merged by a second
@@ -264,8 +267,9 @@ int m3s_vit_rope(void* d_t, int64_t ld, int64_t stride, const int64_t* d_pos,
 int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q, const void* d_k,
                       const void* d_v, int64_t ld_kv, int64_t stride_kv, const int64_t* d_qpos,
                       const int64_t* d_kpos, int64_t stride_pos, void* d_o, int64_t ld_o,
-                      int64_t stride_o, int64_t batch, int64_t heads, int64_t sq, int64_t sk,
-                      float rope_base, void* d_workspace, int64_t workspace_bytes, void* stream);
+                      int64_t stride_o, int o_fp8, int64_t batch, int64_t heads, int64_t sq,
+                      int64_t sk, float rope_base, void* d_workspace, int64_t workspace_bytes,
+                      void* stream);
 
 /* Patch-embed im2col: img f32 NCHW [B][3][H][W] → bf16 [B][(H/16)(W/16)][3*16*16]
  * with K ordered (c, ky, kx) like the conv weight [1024][3][16][16]. */

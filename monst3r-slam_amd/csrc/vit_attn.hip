@@ -124,8 +124,8 @@ constexpr int PART_LD = HD + 4;            // split partial row: O[64], m, l, pa
 template <int AW>
 __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
-    const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, bf16_t* __restrict__ o,
-    int64_t ldo, int64_t so_b, int Sq, int Sk, int heads, float c_log2, int splits,
+    const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, void* __restrict__ o,
+    int64_t ldo, int64_t so_b, int o_fp8, int Sq, int Sk, int heads, float c_log2, int splits,
     int tiles_per_split, float* __restrict__ part) {
   constexpr int ACH = TILE_BYTES / 16 / (AW * 64);  // DMA chunks per thread per operand
   __shared__ __attribute__((aligned(16))) char lds[ASTAGES * STAGE_BYTES];
@@ -326,7 +326,18 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
     return;
   }
   const float inv_l = 1.0f / l;
-  bf16_t* O = o + b * so_b + (int64_t)qrow * ldo + h * HD;
+  if (o_fp8) {  // e4m3 output: the A operand of the fp8 output projection
+    uint8_t* O8 = reinterpret_cast<uint8_t*>(o) + b * so_b + (int64_t)qrow * ldo + h * HD;
+#pragma unroll
+    for (int d = 0; d < 2; d++)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; g4++)
+        *reinterpret_cast<uint32_t*>(O8 + d * 32 + 8 * g4 + 4 * hh) =
+            pack4_fp8(oacc[d][4 * g4] * inv_l, oacc[d][4 * g4 + 1] * inv_l,
+                      oacc[d][4 * g4 + 2] * inv_l, oacc[d][4 * g4 + 3] * inv_l);
+    return;
+  }
+  bf16_t* O = reinterpret_cast<bf16_t*>(o) + b * so_b + (int64_t)qrow * ldo + h * HD;
 #pragma unroll
   for (int d = 0; d < 2; d++)
 #pragma unroll
@@ -343,8 +354,8 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
 __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part,
                                                            int splits, int64_t rows, int heads,
                                                            int Sq, float c_log2,
-                                                           bf16_t* __restrict__ o, int64_t ldo,
-                                                           int64_t so_b) {
+                                                           void* __restrict__ o, int64_t ldo,
+                                                           int64_t so_b, int o_fp8) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= rows * 8) return;
   const int64_t row = idx >> 3;       // (b, h, q)
@@ -366,10 +377,17 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
     acc[4] += a1.x * w; acc[5] += a1.y * w; acc[6] += a1.z * w; acc[7] += a1.w * w;
   }
   const float inv = 1.0f / L;
+  const int64_t off = b * so_b + (int64_t)qi * ldo + h * HD + d8;
+  if (o_fp8) {
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(o) + off) =
+        make_uint2(pack4_fp8(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv),
+                   pack4_fp8(acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv));
+    return;
+  }
   bf16x8 out;
 #pragma unroll
   for (int j = 0; j < 8; j++) out[j] = f2bf(acc[j] * inv);
-  *reinterpret_cast<bf16x8*>(o + b * so_b + (int64_t)qi * ldo + h * HD + d8) = out;
+  *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16_t*>(o) + off) = out;
 }
 
 }  // namespace
@@ -399,8 +417,9 @@ extern "C" int m3s_vit_rope_table(const int64_t* d_pos, int64_t tokens, float ba
 extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q, const void* d_k,
                                  const void* d_v, int64_t ld_kv, int64_t stride_kv,
                                  const int64_t* d_qpos, const int64_t* d_kpos, int64_t stride_pos,
-                                 void* d_o, int64_t ld_o, int64_t stride_o, int64_t batch,
-                                 int64_t heads, int64_t sq, int64_t sk, float rope_base,
+                                 void* d_o, int64_t ld_o, int64_t stride_o, int o_fp8,
+                                 int64_t batch, int64_t heads, int64_t sq, int64_t sk,
+                                 float rope_base,
                                  void* d_workspace, int64_t workspace_bytes, void* stream) {
   if (!d_q || !d_k || !d_v || !d_o || batch <= 0 || heads <= 0 || sq <= 0 || sk <= 0)
     return M3S_ERR_INVALID_ARG;
@@ -440,7 +459,7 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
                      dim3(AWV * 64), 0, s,                                                   \
                      reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,                   \
                      reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
-                     ld_kv, stride_kv, reinterpret_cast<bf16_t*>(d_o), ld_o, stride_o, (int)sq, \
+                     ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,          \
                      (int)sk, (int)heads, c_log2, splits, tps, part)
   if (aw == 2) M3S_ATTN_LAUNCH(2);
   else M3S_ATTN_LAUNCH(4);
@@ -449,7 +468,7 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
     const int64_t rows = hb * sq;
     hipLaunchKernelGGL(attn_combine_kernel, dim3(m3s_div_up(rows * 8, 256)), dim3(256), 0, s,
                        part, splits, rows, (int)heads, (int)sq, c_log2,
-                       reinterpret_cast<bf16_t*>(d_o), ld_o, stride_o);
+                       d_o, ld_o, stride_o, o_fp8 ? 1 : 0);
   }
 #undef M3S_ATTN_LAUNCH
   M3S_LAUNCH_CHECK();

@@ -10,7 +10,8 @@ namespace {
 // DUAL: the decoder's norm1(x) and norm_y of the other side read the same rows, so one
 // pass writes y[b] = LN(x[b ^ xxor]; params b) and y2[b ^ 1] = LN(x[b]; params2 of b ^ 1)
 // from one set of row statistics (y2 only with xxor == 0).
-template <bool XBF, bool YF32, bool DUAL = false>
+// YT: output type 0 bf16, 1 f32, 2 OCP e4m3 (the A operand of the fp8 GEMMs, unscaled).
+template <bool XBF, int YT, bool DUAL = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ x,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
@@ -76,9 +77,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
       float o[4];
 #pragma unroll
       for (int k = 0; k < 4; k++) o[k] = (v[i][k] - mean) * rstd * g[4 * c4 + k] + be[4 * c4 + k];
-      if (YF32) {
+      if constexpr (YT == 1) {
         float* yr = reinterpret_cast<float*>(y) + b * sy + row * dim;
         *reinterpret_cast<float4*>(yr + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
+      } else if constexpr (YT == 2) {
+        uint8_t* yr = reinterpret_cast<uint8_t*>(y) + b * sy + row * dim;
+        *reinterpret_cast<uint32_t*>(yr + 4 * c4) = pack4_fp8(o[0], o[1], o[2], o[3]);
       } else {
         bf16_t* yr = reinterpret_cast<bf16_t*>(y) + b * sy + row * dim;
         bf16x4 ob;
@@ -91,12 +95,19 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
         const int64_t pb2 = pmod > 0 ? b2 % pmod : b2;
         const float* g2 = gamma2 + pb2 * sp;
         const float* be2 = beta2 + pb2 * sp;
-        bf16x4 ob;
+        float o2[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-          ob[k] = f2bf((v[i][k] - mean) * rstd * g2[4 * c4 + k] + be2[4 * c4 + k]);
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(y2) + b2 * sy + row * dim + 4 * c4) =
-            ob;
+        for (int k = 0; k < 4; k++) o2[k] = (v[i][k] - mean) * rstd * g2[4 * c4 + k] + be2[4 * c4 + k];
+        if constexpr (YT == 2) {
+          *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(y2) + b2 * sy + row * dim +
+                                       4 * c4) = pack4_fp8(o2[0], o2[1], o2[2], o2[3]);
+        } else {
+          bf16x4 ob;
+#pragma unroll
+          for (int k = 0; k < 4; k++) ob[k] = f2bf(o2[k]);
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(y2) + b2 * sy + row * dim +
+                                     4 * c4) = ob;
+        }
       }
     }
   }
@@ -263,37 +274,35 @@ __global__ __launch_bounds__(256) void local_feat_kernel(const float* __restrict
 }  // namespace
 
 extern "C" int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_gamma,
-                                 const float* d_beta, void* d_y, int y_is_f32, int64_t rows,
+                                 const float* d_beta, void* d_y, int y_type, int64_t rows,
                                  int64_t dim, float eps, int64_t batch, int64_t stride_x,
                                  int64_t stride_y, int64_t stride_param, int64_t param_mod,
                                  int x_batch_xor, void* stream) {
   if (!d_x || !d_gamma || !d_beta || !d_y || rows <= 0 || batch <= 0) return M3S_ERR_INVALID_ARG;
-  if (dim % 4 || dim > 4096 || dim <= 0) return M3S_ERR_INVALID_ARG;
+  if (dim % 4 || dim > 4096 || dim <= 0 || y_type < 0 || y_type > 2) return M3S_ERR_INVALID_ARG;
   dim3 grid(m3s_div_up(rows, 4), (unsigned)batch);
   hipStream_t s = m3s_stream(stream);
-  if (x_is_bf16 && !y_is_f32)
-    hipLaunchKernelGGL((layernorm_kernel<true, false>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,
-                       x_batch_xor);
-  else if (x_is_bf16 && y_is_f32)
-    hipLaunchKernelGGL((layernorm_kernel<true, true>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,
-                       x_batch_xor);
-  else if (!x_is_bf16 && !y_is_f32)
-    hipLaunchKernelGGL((layernorm_kernel<false, false>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,
-                       x_batch_xor);
-  else
-    hipLaunchKernelGGL((layernorm_kernel<false, true>), grid, dim3(256), 0, s, d_x, d_gamma,
-                       d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,
-                       x_batch_xor);
+#define M3S_LN(XB, YT)                                                                        \
+  hipLaunchKernelGGL((layernorm_kernel<XB, YT>), grid, dim3(256), 0, s, d_x, d_gamma, d_beta, \
+                     d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,    \
+                     x_batch_xor)
+  if (x_is_bf16) {
+    if (y_type == 0) M3S_LN(true, 0);
+    else if (y_type == 1) M3S_LN(true, 1);
+    else M3S_LN(true, 2);
+  } else {
+    if (y_type == 0) M3S_LN(false, 0);
+    else if (y_type == 1) M3S_LN(false, 1);
+    else M3S_LN(false, 2);
+  }
+#undef M3S_LN
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }
 
 extern "C" int m3s_vit_layernorm_dual(const float* d_x, const float* d_gamma,
                                       const float* d_beta, void* d_y, const float* d_gamma2,
-                                      const float* d_beta2, void* d_y2, int64_t rows,
+                                      const float* d_beta2, void* d_y2, int y_fp8, int64_t rows,
                                       int64_t dim, float eps, int64_t batch, int64_t stride_x,
                                       int64_t stride_y, int64_t stride_param, int64_t param_mod,
                                       void* stream) {
@@ -302,9 +311,14 @@ extern "C" int m3s_vit_layernorm_dual(const float* d_x, const float* d_gamma,
     return M3S_ERR_INVALID_ARG;
   if (dim % 4 || dim > 4096 || dim <= 0) return M3S_ERR_INVALID_ARG;
   dim3 grid(m3s_div_up(rows, 4), (unsigned)batch);
-  hipLaunchKernelGGL((layernorm_kernel<false, false, true>), grid, dim3(256), 0,
-                     m3s_stream(stream), d_x, d_gamma, d_beta, d_y, rows, (int)dim, eps,
-                     stride_x, stride_y, stride_param, param_mod, 0, d_gamma2, d_beta2, d_y2);
+  if (y_fp8)
+    hipLaunchKernelGGL((layernorm_kernel<false, 2, true>), grid, dim3(256), 0,
+                       m3s_stream(stream), d_x, d_gamma, d_beta, d_y, rows, (int)dim, eps,
+                       stride_x, stride_y, stride_param, param_mod, 0, d_gamma2, d_beta2, d_y2);
+  else
+    hipLaunchKernelGGL((layernorm_kernel<false, 0, true>), grid, dim3(256), 0,
+                       m3s_stream(stream), d_x, d_gamma, d_beta, d_y, rows, (int)dim, eps,
+                       stride_x, stride_y, stride_param, param_mod, 0, d_gamma2, d_beta2, d_y2);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }

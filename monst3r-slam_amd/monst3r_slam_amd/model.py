@@ -30,6 +30,7 @@ from . import weights as Wt
 
 BF16 = torch.bfloat16
 F32 = torch.float32
+U8 = torch.uint8
 LN_EPS = 1e-6
 
 
@@ -115,13 +116,16 @@ class Ops:
         _lib.check(self.lib.m3s_vit_gemm(ctypes.byref(d), self._s()), "vit_gemm")
 
     def ln(self, x, g, b, y, rows, dim, batch=1, sx=0, sy=0, sp=0, y_f32=False, xor=0, pmod=0):
+        """y dtype picks the output: bf16, f32 (or y_f32) or uint8/float8_e4m3fn (e4m3)."""
+        yt = 1 if (y_f32 or y.dtype == F32) else 2 if y.element_size() == 1 else 0
         _lib.check(self.lib.m3s_vit_layernorm(
-            _p(x), int(x.dtype == BF16), _p(g), _p(b), _p(y), int(y_f32), rows, dim, LN_EPS,
+            _p(x), int(x.dtype == BF16), _p(g), _p(b), _p(y), yt, rows, dim, LN_EPS,
             batch, sx, sy, sp, pmod, xor, self._s()), "vit_layernorm")
 
     def ln_dual(self, x, g, b, y, g2, b2, y2, rows, dim, batch, sx, sy, sp, pmod=0):
         _lib.check(self.lib.m3s_vit_layernorm_dual(
-            _p(x), _p(g), _p(b), _p(y), _p(g2), _p(b2), _p(y2), rows, dim, LN_EPS, batch, sx, sy,
+            _p(x), _p(g), _p(b), _p(y), _p(g2), _p(b2), _p(y2), int(y.element_size() == 1), rows,
+            dim, LN_EPS, batch, sx, sy,
             sp, pmod, self._s()), "vit_layernorm_dual")
 
     def rope(self, t, ld, stride, pos, stride_pos, batch, S, heads, base):
@@ -138,7 +142,8 @@ class Ops:
     def attn(self, q, ldq, sq_b, k, v, ldkv, skv_b, o, ldo, so_b, batch, heads, sq, sk):
         ws = self.ws
         _lib.check(self.lib.m3s_vit_attention(_p(q), ldq, sq_b, _p(k), _p(v), ldkv, skv_b, None,
-                                              None, 0, _p(o), ldo, so_b, batch, heads, sq, sk, 0.0,
+                                              None, 0, _p(o), ldo, so_b,
+                                              int(o.element_size() == 1), batch, heads, sq, sk, 0.0,
                                               _p(ws), ws.numel(), self._s()),
                    "vit_attention")
 
@@ -170,6 +175,21 @@ def _conv_pack(w):
 def _convt_pack(w):
     """ConvTranspose [Cin][Cout][s][s] → [(a, b, co)][ci]."""
     return w.permute(2, 3, 1, 0).reshape(-1, w.shape[0])
+
+
+def quant_e4m3(w):
+    """Per-output-row symmetric e4m3 quantisation of a [.., N, K] weight stack:
+    w ≈ q * scale[.., N, None], |q| ≤ 448.  Returns (q uint8 [.., N, K], scale f32 [.., N])."""
+    w = w.float()
+    sc = (w.abs().amax(-1) / 448.0).clamp_min(1e-12)
+    q = (w / sc[..., None]).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    return q.contiguous(), sc.contiguous()
+
+
+# the transformer GEMMs that run on the fp8 MFMA in fp8 mode (SURVEY §8 C5); patch embed,
+# decoder_embed and the DPT/local-feature heads stay bf16
+ENC_FP8 = ("qkv_w", "proj_w", "fc1_w", "fc2_w")
+DEC_FP8 = ("qkv_w", "proj_w", "q_w", "kv_w", "cproj_w", "fc1_w", "fc2_w")
 
 
 class PackedWeights:
@@ -272,6 +292,14 @@ class PackedWeights:
         self.lf_fc1_b = f32(torch.stack([sd_mast3r[f"{h}.head_local_features.fc1.bias"] for h in lf]))
         self.lf_fc2_w = bf(torch.stack([sd_mast3r[f"{h}.head_local_features.fc2.weight"] for h in lf]))
         self.lf_fc2_b = f32(torch.stack([sd_mast3r[f"{h}.head_local_features.fc2.bias"] for h in lf]))
+        self.enc8 = self.dec8 = None
+
+    def enable_fp8(self):
+        """e4m3 copies (+ per-row scales) of the encoder / decoder transformer weights,
+        quantised from the bf16 packs (the bf16 packs stay for the bf16 path)."""
+        if self.enc8 is None:
+            self.enc8 = {k: quant_e4m3(self.enc[k]) for k in ENC_FP8}
+            self.dec8 = [{k: quant_e4m3(P[k]) for k in DEC_FP8} for P in self.dec]
 
 
 # ---------------------------------------------------------------------------------------
@@ -295,6 +323,26 @@ class PairModel:
         # serial, so one stream is the default.
         self.side = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
         self.serial = True
+        self.fp8 = False
+
+    def set_fp8(self, on=True):
+        """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
+        operands on the scaled MFMA — LayerNorm, attention and the fc1 GELU epilogue emit
+        e4m3 activations (unscaled, saturated to ±448), weights are per-row scaled, the
+        residual stream stays f32 and q/k/v stay bf16 (attention runs in bf16)."""
+        if on:
+            self.w.enable_fp8()
+        self.fp8 = bool(on)
+
+    def _wt(self, P, P8, key, i=None, n=None):
+        """(B operand, extra gemm kwargs) for weight `key` (layer i of a stacked pack, or
+        the z-stack with per-problem scales of stride n)."""
+        if not self.fp8 or key not in P8:
+            return (P[key] if i is None else P[key][i]), {}
+        q, sc = P8[key]
+        if i is None:
+            return q, dict(fp8=(sc, n))
+        return q[i], dict(fp8=(sc[i], 0))
 
     # ---- streams ----
     def _on(self, k):
@@ -360,26 +408,31 @@ class PairModel:
         x = self._buf("enc_x", (M, E), F32)
         o.gemm(patches, W.patch_w, x, M, E, 3 * a.patch * a.patch, bias=W.patch_b,
                flags=_lib.EPI_OUT_F32)
-        xn = self._buf("enc_xn", (M, E), BF16)
+        adt = U8 if self.fp8 else BF16   # GEMM A operands: e4m3 bytes in fp8 mode
+        xn = self._buf("enc_xn", (M, E), adt)
         qkv = self._buf("enc_qkv", (M, 3 * E), BF16)
-        att = self._buf("enc_att", (M, E), BF16)
-        hid = self._buf("enc_hid", (M, a.mlp_ratio * E), BF16)
+        att = self._buf("enc_att", (M, E), adt)
+        hid = self._buf("enc_hid", (M, a.mlp_ratio * E), adt)
         pos = self.positions(B, gh, gw)
         rt = self.rope_tab(gh, gw)
-        P = W.enc
+        P, P8 = W.enc, W.enc8
         for i in range(a.enc_depth):
             o.ln(x, P["ln1_g"][i], P["ln1_b"][i], xn, M, E)
             # qkv projection with RoPE2D on q and k fused into the epilogue
-            o.gemm(xn, P["qkv_w"][i], qkv, M, 3 * E, E, bias=P["qkv_b"][i], rope=(rt, 2 * E, S))
+            w, kw = self._wt(P, P8, "qkv_w", i)
+            o.gemm(xn, w, qkv, M, 3 * E, E, bias=P["qkv_b"][i], rope=(rt, 2 * E, S), **kw)
             o.attn(qkv, 3 * E, S * 3 * E, qkv[:, E:], qkv[:, 2 * E:], 3 * E, S * 3 * E, att, E,
                    S * E, B, a.enc_heads, S, S)
-            o.gemm(att, P["proj_w"][i], x, M, E, E, bias=P["proj_b"][i], R=x,
-                   flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32)
+            w, kw = self._wt(P, P8, "proj_w", i)
+            o.gemm(att, w, x, M, E, E, bias=P["proj_b"][i], R=x,
+                   flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, **kw)
             o.ln(x, P["ln2_g"][i], P["ln2_b"][i], xn, M, E)
-            o.gemm(xn, P["fc1_w"][i], hid, M, a.mlp_ratio * E, E, bias=P["fc1_b"][i],
-                   flags=_lib.EPI_GELU)
-            o.gemm(hid, P["fc2_w"][i], x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][i], R=x,
-                   flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32)
+            w, kw = self._wt(P, P8, "fc1_w", i)
+            o.gemm(xn, w, hid, M, a.mlp_ratio * E, E, bias=P["fc1_b"][i],
+                   flags=_lib.EPI_GELU, out_fp8=self.fp8, **kw)
+            w, kw = self._wt(P, P8, "fc2_w", i)
+            o.gemm(hid, w, x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][i], R=x,
+                   flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, **kw)
         feat = out if out is not None else torch.empty((B, S, E), dtype=BF16, device=self.dev)
         o.ln(x, W.enc_norm_g, W.enc_norm_b, feat, M, E)
         return feat, pos
@@ -407,62 +460,72 @@ class PairModel:
         x = self._buf("dec_x", (Z, S, D), F32)
         o.gemm(h0, W.dec_embed_w, x, S, D, E, Z, sA=S * E, sB=D * E, sC=S * D,
                bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32, wmod=4)
-        xn = self._buf("dec_xn", (Z, S, D), BF16)
-        yn = self._buf("dec_yn", (Z, S, D), BF16)
+        adt = U8 if self.fp8 else BF16
+        xn = self._buf("dec_xn", (Z, S, D), adt)
+        yn = self._buf("dec_yn", (Z, S, D), adt)
         qkv = self._buf("dec_qkv", (Z, S, 3 * D), BF16)
         kv = self._buf("dec_kv", (Z, S, 2 * D), BF16)
         q = self._buf("dec_q", (Z, S, D), BF16)
-        att = self._buf("dec_att", (Z, S, D), BF16)
-        hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), BF16)
+        att = self._buf("dec_att", (Z, S, D), adt)
+        hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), adt)
         hooks = {"h0": h0}
         rt = self.rope_tab(gh, gw)
         hk = set(a.hooks[1:3])
         R32 = _lib.EPI_OUT_F32 | _lib.EPI_RES_F32
+        Dm = a.mlp_ratio * D
         for i in range(a.dec_depth):
             P = W.dec[i]
+            P8 = W.dec8[i] if self.fp8 else None
+            wt = lambda key, n: self._wt(P, P8, key, None, n)  # noqa: E731
             # y_ = norm_y(previous output of the other side), then its k/v projection: on a
             # side stream, overlapping the self-attention half of the layer (the side chain
             # must read x before this layer's first residual update writes it)
+            w, kw = wt("kv_w", 2 * D)
             if self.serial:
                 # norm1(x) and norm_y(other side's x) share the row statistics: one pass
                 o.ln_dual(x, P["ln1_g"], P["ln1_b"], xn, P["lny_g"], P["lny_b"], yn, S, D, Z,
                           S * D, S * D, D, pmod=4)
-                o.gemm(yn, P["kv_w"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
-                       sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4)
+                o.gemm(yn, w, kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
+                       sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4, **kw)
                 ev_lny = ev_kv = None
             else:
                 with self._on(0):
                     o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1, pmod=4)
                     ev_lny = self._event()
-                    o.gemm(yn, P["kv_w"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
-                           sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4)
+                    o.gemm(yn, w, kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
+                           sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4,
+                           **kw)
                     ev_kv = self._event()
                 o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
             # self-attention
-            o.gemm(xn, P["qkv_w"], qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
-                   bias=P["qkv_b"], sBias=3 * D, rope=(rt, 2 * D, S), wmod=4)
+            w, kw = wt("qkv_w", 3 * D)
+            o.gemm(xn, w, qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
+                   bias=P["qkv_b"], sBias=3 * D, rope=(rt, 2 * D, S), wmod=4, **kw)
             o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,
                    D, S * D, Z, a.dec_heads, S, S)
             self._wait(ev_lny)
-            o.gemm(att, P["proj_w"], x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["proj_b"],
-                   sBias=D, R=x, sR=S * D, flags=R32, wmod=4)
+            w, kw = wt("proj_w", D)
+            o.gemm(att, w, x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["proj_b"],
+                   sBias=D, R=x, sR=S * D, flags=R32, wmod=4, **kw)
             # cross-attention: q from norm2(x), k/v from y_
             o.ln(x, P["ln2_g"], P["ln2_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
-            o.gemm(xn, P["q_w"], q, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["q_b"],
-                   sBias=D, rope=(rt, D, S), wmod=4)
+            w, kw = wt("q_w", D)
+            o.gemm(xn, w, q, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["q_b"],
+                   sBias=D, rope=(rt, D, S), wmod=4, **kw)
             self._wait(ev_kv)
             o.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, att, D, S * D, Z, a.dec_heads,
                    S, S)
-            o.gemm(att, P["cproj_w"], x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D,
-                   bias=P["cproj_b"], sBias=D, R=x, sR=S * D, flags=R32, wmod=4)
+            w, kw = wt("cproj_w", D)
+            o.gemm(att, w, x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D,
+                   bias=P["cproj_b"], sBias=D, R=x, sR=S * D, flags=R32, wmod=4, **kw)
             # MLP
             o.ln(x, P["ln3_g"], P["ln3_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
-            o.gemm(xn, P["fc1_w"], hid, S, a.mlp_ratio * D, D, Z, sA=S * D,
-                   sB=a.mlp_ratio * D * D, sC=S * a.mlp_ratio * D, bias=P["fc1_b"],
-                   sBias=a.mlp_ratio * D, flags=_lib.EPI_GELU, wmod=4)
-            o.gemm(hid, P["fc2_w"], x, S, D, a.mlp_ratio * D, Z, sA=S * a.mlp_ratio * D,
-                   sB=a.mlp_ratio * D * D, sC=S * D, bias=P["fc2_b"], sBias=D, R=x, sR=S * D,
-                   flags=R32, wmod=4)
+            w, kw = wt("fc1_w", Dm)
+            o.gemm(xn, w, hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm, bias=P["fc1_b"],
+                   sBias=Dm, flags=_lib.EPI_GELU, wmod=4, out_fp8=self.fp8, **kw)
+            w, kw = wt("fc2_w", D)
+            o.gemm(hid, w, x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D, bias=P["fc2_b"],
+                   sBias=D, R=x, sR=S * D, flags=R32, wmod=4, **kw)
             if (i + 1) in hk:
                 hb = self._buf(f"h{i + 1}", (Z, S, D), BF16)
                 hb.copy_(x)

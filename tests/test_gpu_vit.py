@@ -349,3 +349,81 @@ def test_gemm_fp8(ops, dev, M, N, K, batch, mode):
         C = torch.empty(batch, M, N, device=dev, dtype=torch.bfloat16)
         ops.gemm(A.view(torch.uint8), B.view(torch.uint8), C, M, N, K, batch, **kw)
         assert _rel(C, ref) < 1e-2
+
+
+def _e4m3_close(out8, ref, extra=0.0):
+    """out8: e4m3 bytes; ref f32.  Every value within one e4m3 step of the e4m3 rounding
+    of ref (RNE of slightly different f32 inputs may land on the neighbouring code), and
+    at most 2 % of the codes differ."""
+    out = out8.view(torch.float8_e4m3fn).float()
+    refq = _fp8(ref).float()
+    tol = 0.125 * refq.abs() + 2.0 ** -9 + extra
+    assert bool(((out - refq).abs() <= tol).all()), float(((out - refq).abs() - tol).max())
+    frac = float((out != refq).float().mean())
+    assert frac < 0.02, frac
+
+
+def test_layernorm_fp8_out(ops, dev):
+    """LayerNorm emitting the e4m3 A operand of the fp8 GEMMs (single and dual)."""
+    g = torch.Generator(device=dev).manual_seed(15)
+    x = torch.randn(4, 768, 1024, device=dev, generator=g) * 2 + 0.5
+    gam = torch.randn(4, 1024, device=dev, generator=g)
+    bet = torch.randn(4, 1024, device=dev, generator=g)
+    y = torch.empty(4, 768, 1024, device=dev, dtype=torch.uint8)
+    ops.ln(x, gam, bet, y, 768, 1024, 4, 768 * 1024, 768 * 1024, 1024)
+    ref = torch.stack([F.layer_norm(x[b], (1024,), gam[b], bet[b], 1e-6) for b in range(4)])
+    _e4m3_close(y, ref)
+    y2 = torch.empty_like(y)
+    ops.ln_dual(x, gam, bet, y, bet, gam, y2, 768, 1024, 4, 768 * 1024, 768 * 1024, 1024, pmod=4)
+    ref2 = torch.stack([F.layer_norm(x[b ^ 1], (1024,), bet[b], gam[b], 1e-6) for b in range(4)])
+    _e4m3_close(y, ref)
+    _e4m3_close(y2, ref2)
+
+
+@pytest.mark.parametrize("splits", ["1", "3"])
+def test_attention_fp8_out(ops, dev, monkeypatch, splits):
+    """bf16 attention whose output is stored as e4m3 (direct and through the split combine);
+    tolerance: one e4m3 step plus the bf16 probability rounding of the bf16 path (2e-2)."""
+    monkeypatch.setenv("M3S_ATTN_SPLITS", splits)
+    g = torch.Generator(device=dev).manual_seed(16)
+    S, heads, batch = 300, 4, 2
+    C = heads * 64
+    qkv = torch.randn(batch, S, 3 * C, device=dev, generator=g).bfloat16()
+    o = torch.empty(batch, S, C, device=dev, dtype=torch.uint8)
+    ops.attn(qkv, 3 * C, S * 3 * C, qkv[:, :, C:], qkv[:, :, 2 * C:], 3 * C, S * 3 * C, o, C, S * C,
+             batch, heads, S, S)
+    q, k, v = qkv.float().reshape(batch, S, 3, heads, 64).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(q @ k.transpose(-1, -2) / 8.0, -1) @ v).transpose(1, 2).reshape(batch, S, C)
+    out = o.view(torch.float8_e4m3fn).float()
+    assert bool(((out - _fp8(ref).float()).abs() <= 0.13 * ref.abs() + 0.02).all())
+    assert _rel(out, ref) < 0.05
+
+
+def test_fp8_model_vs_fp32_restatement_512(dev):
+    """the fp8 transformer path (e4m3 activations + per-row weight scales on
+    the scaled MFMA; heads in bf16) at 512x512 against the fp32 restatement.  Stated fp8
+    tolerances (looser than the bf16 path's in _compare_pair): pointmap median relative
+    error < 8 %, conf median < 8 %, descriptor median cosine > 0.97."""
+    from monst3r_slam_amd import model as Mdl
+    from oracle import vit_ref as V
+    m, (sdm, am, sdM, aM) = Mdl.build(dev)
+    m.set_fp8(True)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    img_i = torch.rand(1, 3, 512, 512, device=dev, generator=gen) * 2 - 1
+    img_j = torch.rand(1, 3, 512, 512, device=dev, generator=gen) * 2 - 1
+    out = m.pair(img_i, img_j=img_j)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    sdm = {k: v.to(dev) for k, v in sdm.items()}
+    sdM = {k: v.to(dev) for k, v in sdM.items()}
+    X, C, D, Q, _, _ = V.asymmetric_inference(sdm, am, sdM, aM, img_i, img_j)
+    rel_X = ((out["X"] - X).norm(dim=-1) / X.norm(dim=-1).clamp_min(1e-6))
+    rel_C = ((out["C"] - C).abs() / C.abs())
+    cos_D = _cos(out["D"], D)
+    rel_Q = ((out["Q"] - Q).abs() / Q.abs())
+    stats = dict(X_med=float(rel_X.median()), X_p99=float(rel_X.quantile(0.99)),
+                 C_med=float(rel_C.median()), D_cos_med=float(cos_D.median()),
+                 D_cos_min=float(cos_D.min()), Q_med=float(rel_Q.median()))
+    print("fp8-512-vs-fp32", stats)
+    assert stats["X_med"] < 0.08 and stats["C_med"] < 0.08, stats
+    assert stats["D_cos_med"] > 0.97 and stats["Q_med"] < 0.15, stats
+    m.set_fp8(False)
