@@ -39,6 +39,7 @@ import torch  # noqa: E402
 H, W = 384, 512
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BF16_DENSE_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (spec, no sparsity)
+FP8_DENSE_TFLOPS = 5000.0    # MI355X dense fp8 MFMA (spec, no sparsity; scaled 32x32x64)
 METRIC = "tracking frames/sec @512x384 + pairwise pointmap-inference ms, 1/8 MI355X"
 
 
@@ -51,6 +52,7 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="no HIP graph (debug)")
     ap.add_argument("--no-graph", action="store_true", help="skip the keyframe-graph (C4) leg")
     ap.add_argument("--graph-steps", type=int, default=2)
+    ap.add_argument("--no-c5", action="store_true", help="skip the fp8 512x512 dyn-mask leg")
     ap.add_argument("--streams", action="store_true",
                     help="overlap independent chains on side streams (measured slower)")
     return ap.parse_args()
@@ -106,8 +108,8 @@ def gemm_roofline(model, img, feat_k, dev):
     torch.cuda.synchronize(dev)
     probe, model.ops.probe = model.ops.probe, None
     model.serial = serial
-    t_ms = sum(a.elapsed_time(b) for a, b, _ in probe)
-    flops = sum(f for _, _, f in probe)
+    t_ms = sum(a.elapsed_time(b) for a, b, _, _ in probe)
+    flops = sum(f for _, _, f, _ in probe)
     return dict(launches=len(probe), gemm_ms=t_ms, gemm_flops=flops,
                 avg_launch_us=t_ms / len(probe) * 1e3,
                 tflops=flops / (t_ms * 1e-3) / 1e12)
@@ -190,6 +192,67 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
             "gflop_per_pair": 3603.6, "tflops_achieved": len(ii) * 3603.6e9 * steps / el / 1e12,
             "allgather_bytes_per_rank": int(-(-len(ii) // world) * P.record_bytes(n)),
             "sharding": f"edges round-robin over {world} rank(s), RCCL all-gather"}
+
+
+def c5_bench(model, dev, steps):
+    """configs[4], one GPU: the per-frame inference of dynamic-mask tracking
+    at 512x512 with the fp8 transformer path — MonST3R encoder (new frame), MonST3R-only
+    mono decode + both heads (depth for the ego flow), ego flow + flow-error mask (the RAFT
+    flow is an input: synthetic here, RAFT is absent code), MonST3R+MASt3R pair decode + 4
+    heads + local features vs the cached keyframe, apply_dynamic_mask on C/Q/D.  Graph
+    captured; timed for fp8 and for the bf16 path on the same inputs.  Multi-GPU: frames
+    are sequential per sequence → replicas (the 1→8 curve is the replica sweep)."""
+    from monst3r_slam_amd import monst3r_utils as U
+    from monst3r_slam_amd import synthetic as syn
+    H5 = W5 = 512
+    gh = gw = H5 // 16
+    g = torch.Generator(device=dev).manual_seed(55)
+    img = torch.rand(1, 3, H5, W5, device=dev, generator=g) * 2 - 1
+    img_k = torch.rand(1, 3, H5, W5, device=dev, generator=g) * 2 - 1
+    K = torch.from_numpy(syn.intrinsics(H5, W5)).to(dev)
+    Ti = torch.tensor([0.05, 0.0, 0.01, 0, 0, 0, 1, 1.0], device=dev)
+    Tk = torch.tensor([0.0, 0.0, 0.0, 0, 0, 0, 1, 1.0], device=dev)
+    flow = torch.randn(2, H5, W5, device=dev, generator=g)
+    res = {}
+    for mode in ("fp8", "bf16"):
+        model.set_fp8(mode == "fp8")
+        feat_k = model.encode(img_k)[0].clone()
+
+        def step():
+            feat_i, pos = model.encode(img)
+            Xm, _ = model.mono(feat_i, H5, W5)
+            sR, t = U.sim3_relative_matrix(Ti, Tk)
+            ego = U.ego_flow(Xm[0], sR, t, K, K)
+            mask = U.dynamic_mask_from_flow(flow, ego, 0.35)
+            hooks = model.decode(feat_i[0], feat_k[0], pos, gh, gw)
+            pts, conf, d16, d32, dq = model.heads(hooks, gh, gw, H5, W5)
+            return U.apply_dynamic_mask_to_pointmaps(pts[0:2], conf[0:2], mask, d16, dq)
+
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize(dev)
+        gph = capture(step, dev)
+        res[mode] = time_replays(gph, dev, steps)
+        if mode == "fp8":
+            model.ops.probe = []
+            step()
+            torch.cuda.synchronize(dev)
+            probe, model.ops.probe = model.ops.probe, None
+            fp8_ms = sum(a.elapsed_time(b) for a, b, _, in8 in probe if in8)
+            fp8_fl = sum(f for _, _, f, in8 in probe if in8)
+            all_ms = sum(a.elapsed_time(b) for a, b, _, _ in probe)
+        del gph
+    model.set_fp8(False)
+    return {"workload": "configs[4]: 512x512 frame, fp8 encoder+decoders, mono decode + ego "
+                        "flow + flow-error mask + pair decode/heads + apply_dynamic_mask",
+            "ms_per_frame_fp8": res["fp8"], "ms_per_frame_bf16": res["bf16"],
+            "frames_per_s_fp8": 1e3 / res["fp8"], "speedup_vs_bf16": res["bf16"] / res["fp8"],
+            "fp8_gemm": {"launches": sum(1 for p in probe if p[3]), "ms": fp8_ms,
+                         "gflop": fp8_fl / 1e9, "tflops": fp8_fl / (fp8_ms * 1e-3) / 1e12,
+                         "peak": FP8_DENSE_TFLOPS,
+                         "frac": fp8_fl / (fp8_ms * 1e-3) / 1e12 / FP8_DENSE_TFLOPS},
+            "all_gemm_ms": all_ms,
+            "tolerance": "tests/test_gpu_vit.py::test_fp8_model_vs_fp32_restatement_512"}
 
 
 def pmc_traffic():
@@ -325,6 +388,8 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline()
+    if not args.no_c5 and rank == 0:
+        line["fp8_dynmask_512"] = c5_bench(model, dev, max(5, args.steps // 2))
     if not args.no_graph:
         kg = keyframe_graph_bench(model, dev, world, args.graph_steps)
         if rank == 0:

@@ -310,6 +310,16 @@ int m3s_vit_local_features(const float* d_feats, float* d_desc, uint16_t* d_desc
 int m3s_flow_error_mask(const float* d_flow, const float* d_ego_flow, int64_t n,
                         float threshold, uint8_t* d_mask, float* d_workspace, void* stream);
 
+/* Ego-motion flow of get_dynamic_mask (monst3r_utils.py:566-614): pixel (x, y) of frame i
+ * at depth pts[p].z (the mono decode's res_i pts3d, f32 [h][w][3]; inv_depth =
+ * 1/(z + 1e-6) as :586) maps to K_j (R_ji d K_i^-1 [x y 1]^T + t_ji) in frame j.
+ * params (device, 30 f32): R_ji row-major 9, t_ji 3, K_j 9, K_i^-1 9.  Out ego f32 [3][h*w]:
+ * flow x, flow y (projection - pixel), valid (projected depth > 1e-6; flow 0 otherwise).
+ * DepthBasedWarping itself is absent from the reference checkout: restated, parity
+ * unpinned. */
+int m3s_ego_flow(const float* d_pts, const float* d_params, int64_t h, int64_t w,
+                 float* d_ego, void* stream);
+
 /* apply_dynamic_mask_to_pointmaps (monst3r_utils.py:300-341), in place: where mask[p]
  * (u8 [hw], shared by the batch) C[b][p] = value, Q[b][p] = value (Q optional) and
  * D[b][p][:] = 0 (D optional, f32 or f16 [b][hw][fdim]).  The reference zeroes D whenever

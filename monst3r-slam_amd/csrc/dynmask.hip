@@ -2,6 +2,7 @@
 //   m3s_flow_error_mask   get_dynamic_mask's error map → min-max normalisation → threshold
 //                         (mast3r_slam/monst3r_utils.py:625-637)
 //   m3s_apply_dynamic_mask apply_dynamic_mask_to_pointmaps (monst3r_utils.py:300-341)
+//   m3s_ego_flow          ego-motion flow of get_dynamic_mask (:566-614) from the mono depth
 #include "common.h"
 
 namespace {
@@ -77,7 +78,50 @@ __global__ __launch_bounds__(256) void apply_mask_kernel(const uint8_t* __restri
   }
 }
 
+// Ego-motion flow: pixel (x, y) of frame i with depth z = pts[p].z (mono res_i pts3d)
+// lands at K_j (R_ji d K_i^-1 [x y 1]^T + t_ji) in frame j; flow = projection - (x, y).
+// prm: R_ji (9, row-major), t_ji (3), K_j (9), K_i^-1 (9) = 30 floats in device memory
+// (so a captured graph reads the current pose).  Out: [3][n] (flow x, flow y, valid).
+__global__ __launch_bounds__(256) void ego_flow_kernel(const float* __restrict__ pts,
+                                                       const float* __restrict__ prm, int w,
+                                                       int64_t n, float* __restrict__ ego) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float x = (float)(i % w), y = (float)(i / w);
+  const float z = pts[3 * i + 2];
+  // inv_depth = 1 / (depth + 1e-6) (:586), then depth = 1 / inv_depth inside the warp
+  const float inv_depth = 1.0f / (z + 1e-6f);
+  const float d = 1.0f / inv_depth;
+  const float* R = prm;
+  const float* t = prm + 9;
+  const float* Kj = prm + 12;
+  const float* Ki = prm + 21;
+  const float cx = d * (Ki[0] * x + Ki[1] * y + Ki[2]);
+  const float cy = d * (Ki[3] * x + Ki[4] * y + Ki[5]);
+  const float cz = d * (Ki[6] * x + Ki[7] * y + Ki[8]);
+  const float qx = R[0] * cx + R[1] * cy + R[2] * cz + t[0];
+  const float qy = R[3] * cx + R[4] * cy + R[5] * cz + t[1];
+  const float qz = R[6] * cx + R[7] * cy + R[8] * cz + t[2];
+  const float px = Kj[0] * qx + Kj[1] * qy + Kj[2] * qz;
+  const float py = Kj[3] * qx + Kj[4] * qy + Kj[5] * qz;
+  const float pz = Kj[6] * qx + Kj[7] * qy + Kj[8] * qz;
+  const bool ok = pz > 1e-6f;
+  ego[i] = ok ? px / pz - x : 0.f;
+  ego[n + i] = ok ? py / pz - y : 0.f;
+  ego[2 * n + i] = ok ? 1.f : 0.f;
+}
+
 }  // namespace
+
+extern "C" int m3s_ego_flow(const float* d_pts, const float* d_params, int64_t h, int64_t w,
+                            float* d_ego, void* stream) {
+  if (!d_pts || !d_params || !d_ego || h <= 0 || w <= 0) return M3S_ERR_INVALID_ARG;
+  const int64_t n = h * w;
+  hipLaunchKernelGGL(ego_flow_kernel, dim3(m3s_div_up(n, 256)), dim3(256), 0,
+                     m3s_stream(stream), d_pts, d_params, (int)w, n, d_ego);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
 
 extern "C" int m3s_flow_error_mask(const float* d_flow, const float* d_ego_flow, int64_t n,
                                    float threshold, uint8_t* d_mask, float* d_workspace,

@@ -1091,7 +1091,12 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   const int64_t tiles128 = (int64_t)((d->M + 127) / 128) * ((d->N + 127) / 128) * d->batch;
   const int nk = (int)((eK + 63) / 64);     // K-tiles of 128 bytes per row
   int cfg = forced_tile();
-  if (cfg == 0) {
+  if (cfg == 0 && f8) {
+    // fp8 (tools/fp8_tune.py, S = 768 / 1024 shapes): a K-tile holds 128 e4m3 values, so
+    // the short-K latency regime comes sooner; 64x128 tiles at 2/CU win below ~1.5 waves
+    // of 128^2 tiles, 2 x 128^2 per CU above (1.96 PFLOP/s on 4096^3)
+    cfg = tiles128 >= 400 ? T128O2 : T64;
+  } else if (cfg == 0) {
     // measured on the pair shapes (tools/gemm_tune.py): 2 x 128^2 blocks per CU win for
     // wide convs with several waves of tiles, for one-to-two waves of short-K GEMM tiles,
     // and for large square-ish GEMMs

@@ -56,6 +56,7 @@ SIGNATURES = {
     "m3s_vit_upsample2x": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "m3s_vit_dpt_out": (_I, [_P, _P, _P, _P, _P, _I64, _F, _I64, _I64, _I64, _I64, _P]),
     "m3s_vit_local_features": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P]),
+    "m3s_ego_flow": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "m3s_flow_error_mask": (_I, [_P, _P, _I64, _F, _P, _P, _P]),
     "m3s_apply_dynamic_mask": (_I, [_P, _P, _P, _P, _I, _I64, _I64, _I64, _F, _I, _P]),
 }

@@ -52,7 +52,7 @@ class Ops:
     def __init__(self, dev):
         self.lib = _lib.load()
         self.dev = dev
-        self.probe = None  # list → (start_event, end_event, flops) per GEMM (bench roofline)
+        self.probe = None  # list → (start_event, end_event, flops, fp8) per GEMM (bench roofline)
         # f32 split-K / attention-split scratch, one per stream (the M = 768 GEMMs split K
         # when their grid cannot fill 256 CUs; concurrent streams must not share it)
         self._ws = {}
@@ -111,7 +111,7 @@ class Ops:
             e0.record(st)
             _lib.check(self.lib.m3s_vit_gemm(ctypes.byref(d), self._s()), "vit_gemm")
             e1.record(st)
-            self.probe.append((e0, e1, 2.0 * M * N * K * batch))
+            self.probe.append((e0, e1, 2.0 * M * N * K * batch, fp8 is not None))
             return
         _lib.check(self.lib.m3s_vit_gemm(ctypes.byref(d), self._s()), "vit_gemm")
 
@@ -444,22 +444,25 @@ class PairModel:
         S, E = gh * gw, self.a.enc_dim
         return self.decode_multi(feat_i.reshape(1, S, E), feat_j.reshape(1, S, E), gh, gw)
 
-    def decode_multi(self, feat1, feat2, gh, gw):
+    def decode_multi(self, feat1, feat2, gh, gw, models=2):
         """G directed pairs at once: feat1/feat2 bf16 [G,S,E] are the first / second view of
         each pair (d3r/model.py:171-190 `_decoder(f1, pos1, f2, pos2)`), decoded by BOTH
-        models.  Problems z = (g*2 + model)*2 + side; every launch covers all 4G of them and
-        reads the weight stack of z % 4 (weight_mod).  Returns hooks [4G,S,*]."""
+        models (models=2) or by MonST3R alone (models=1, the dynamic-mask mono decode).
+        Problems z = (g*models + model)*2 + side; every launch covers all of them and reads
+        the weight stack of z % (2*models) (weight_mod).  Returns hooks [2*models*G,S,*]."""
         o, a, W = self.ops, self.a, self.w
         S, E, D = gh * gw, a.enc_dim, a.dec_dim
         G = feat1.shape[0]
-        Z = 4 * G
+        wm = 2 * models
+        self._wm = wm
+        Z = wm * G
         h0 = self._buf("h0", (Z, S, E), BF16)
-        hv = h0.view(G, 2, 2, S, E)
-        hv[:, :, 0].copy_(feat1.reshape(G, 1, S, E).expand(G, 2, S, E))
-        hv[:, :, 1].copy_(feat2.reshape(G, 1, S, E).expand(G, 2, S, E))
+        hv = h0.view(G, models, 2, S, E)
+        hv[:, :, 0].copy_(feat1.reshape(G, 1, S, E).expand(G, models, S, E))
+        hv[:, :, 1].copy_(feat2.reshape(G, 1, S, E).expand(G, models, S, E))
         x = self._buf("dec_x", (Z, S, D), F32)
         o.gemm(h0, W.dec_embed_w, x, S, D, E, Z, sA=S * E, sB=D * E, sC=S * D,
-               bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32, wmod=4)
+               bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32, wmod=wm)
         adt = U8 if self.fp8 else BF16
         xn = self._buf("dec_xn", (Z, S, D), adt)
         yn = self._buf("dec_yn", (Z, S, D), adt)
@@ -484,54 +487,54 @@ class PairModel:
             if self.serial:
                 # norm1(x) and norm_y(other side's x) share the row statistics: one pass
                 o.ln_dual(x, P["ln1_g"], P["ln1_b"], xn, P["lny_g"], P["lny_b"], yn, S, D, Z,
-                          S * D, S * D, D, pmod=4)
+                          S * D, S * D, D, pmod=wm)
                 o.gemm(yn, w, kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
-                       sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4, **kw)
+                       sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=wm, **kw)
                 ev_lny = ev_kv = None
             else:
                 with self._on(0):
-                    o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1, pmod=4)
+                    o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1, pmod=wm)
                     ev_lny = self._event()
                     o.gemm(yn, w, kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
-                           sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=4,
+                           sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=wm,
                            **kw)
                     ev_kv = self._event()
-                o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
+                o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D, pmod=wm)
             # self-attention
             w, kw = wt("qkv_w", 3 * D)
             o.gemm(xn, w, qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
-                   bias=P["qkv_b"], sBias=3 * D, rope=(rt, 2 * D, S), wmod=4, **kw)
+                   bias=P["qkv_b"], sBias=3 * D, rope=(rt, 2 * D, S), wmod=wm, **kw)
             o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,
                    D, S * D, Z, a.dec_heads, S, S)
             self._wait(ev_lny)
             w, kw = wt("proj_w", D)
             o.gemm(att, w, x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["proj_b"],
-                   sBias=D, R=x, sR=S * D, flags=R32, wmod=4, **kw)
+                   sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
             # cross-attention: q from norm2(x), k/v from y_
-            o.ln(x, P["ln2_g"], P["ln2_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
+            o.ln(x, P["ln2_g"], P["ln2_b"], xn, S, D, Z, S * D, S * D, D, pmod=wm)
             w, kw = wt("q_w", D)
             o.gemm(xn, w, q, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["q_b"],
-                   sBias=D, rope=(rt, D, S), wmod=4, **kw)
+                   sBias=D, rope=(rt, D, S), wmod=wm, **kw)
             self._wait(ev_kv)
             o.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, att, D, S * D, Z, a.dec_heads,
                    S, S)
             w, kw = wt("cproj_w", D)
             o.gemm(att, w, x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D,
-                   bias=P["cproj_b"], sBias=D, R=x, sR=S * D, flags=R32, wmod=4, **kw)
+                   bias=P["cproj_b"], sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
             # MLP
-            o.ln(x, P["ln3_g"], P["ln3_b"], xn, S, D, Z, S * D, S * D, D, pmod=4)
+            o.ln(x, P["ln3_g"], P["ln3_b"], xn, S, D, Z, S * D, S * D, D, pmod=wm)
             w, kw = wt("fc1_w", Dm)
             o.gemm(xn, w, hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm, bias=P["fc1_b"],
-                   sBias=Dm, flags=_lib.EPI_GELU, wmod=4, out_fp8=self.fp8, **kw)
+                   sBias=Dm, flags=_lib.EPI_GELU, wmod=wm, out_fp8=self.fp8, **kw)
             w, kw = wt("fc2_w", D)
             o.gemm(hid, w, x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D, bias=P["fc2_b"],
-                   sBias=D, R=x, sR=S * D, flags=R32, wmod=4, **kw)
+                   sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
             if (i + 1) in hk:
                 hb = self._buf(f"h{i + 1}", (Z, S, D), BF16)
                 hb.copy_(x)
                 hooks[f"h{i + 1}"] = hb
         h12 = self._buf("h12", (Z, S, D), BF16)
-        o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=4)
+        o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
         hooks["h12"] = h12
         return hooks
 
@@ -545,7 +548,7 @@ class PairModel:
                sB=cout * 9 * cin, sC=hout * wout * cout,
                bias=H[bias_key] if bias_key else None, sBias=cout, R=R,
                sR=hout * wout * cout, flags=flags, conv=(hin, win, cin, hout, wout, stride),
-               wmod=4, dpt=dpt)
+               wmod=self._wm, dpt=dpt)
         return hout, wout
 
     def _rcu(self, x, k, u, b, h, w, out, addend_res=None):
@@ -574,24 +577,14 @@ class PairModel:
         self._rcu(s1, k, 2, b, h, w, s2)
         oc = self._buf(("fus_oc", h, w), (b, h, w, F), BF16)
         o.gemm(s2, H[f"r{k}_out_w"], oc, h * w, F, F, b, sA=h * w * F, sB=F * F, sC=h * w * F,
-               bias=H[f"r{k}_out_b"], sBias=F, wmod=4)
+               bias=H[f"r{k}_out_b"], sBias=F, wmod=self._wm)
         oh, ow = next_hw
         o.up2(oc, out, b, h, w, F, oh, ow, add=next_skip)
 
-    def heads(self, hooks, gh, gw, H, W):
-        """DPT heads of all 4G problems (z = (g*2 + model)*2 + side, head weights z % 4) +
-        MASt3R local features of the model-1 problems.
-        Returns pts3d f32 [4G,H,W,3], conf f32 [4G,H,W], desc16 f16 [2G,H,W,24],
-        desc f32 [2G,H,W,24], desc_conf f32 [2G,H,W] (the latter three: (g, side) of model 1)."""
-        o, a, Hw = self.ops, self.a, self.w.h
-        Z = hooks["h0"].shape[0]
-        G = Z // 4
-        S, E, D = gh * gw, a.enc_dim, a.dec_dim
-        Ld = a.layer_dims
-        F = a.feature_dim
-        # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle, on
-        # side stream 1 (independent of the DPT: overlaps all of it)
-        aM = self.w.arch_mast3r
+    def _local_features(self, hooks, G, S, E, D, H, W):
+        """MASt3R local features (z = 2, 3 of each pair): cat(enc, dec_last) → MLP → pixel
+        shuffle, on side stream 1 (independent of the DPT: overlaps all of it)."""
+        o, aM = self.ops, self.w.arch_mast3r
         idim = E + D
         hidd = 4 * idim
         odim = (aM.desc_dim + 1) * aM.patch ** 2
@@ -613,6 +606,27 @@ class PairModel:
                    flags=_lib.EPI_OUT_F32, wmod=2)
             o.local_features(lo, desc, desc16, dconf, 2 * G, H, W)
             ev_lf = self._event()
+        return desc, desc16, dconf, ev_lf
+
+    def heads(self, hooks, gh, gw, H, W, models=2):
+        """DPT heads of all 2*models*G problems (z = (g*models + model)*2 + side, head weights
+        z % (2*models)) + MASt3R local features of the model-1 problems (models=2 only).
+        Returns pts3d f32 [Z,H,W,3], conf f32 [Z,H,W], desc16 f16 [2G,H,W,24],
+        desc f32 [2G,H,W,24], desc_conf f32 [2G,H,W] (the latter three: (g, side) of model 1;
+        None with models=1)."""
+        o, a, Hw = self.ops, self.a, self.w.h
+        Z = hooks["h0"].shape[0]
+        wm = 2 * models
+        self._wm = wm
+        G = Z // wm
+        S, E, D = gh * gw, a.enc_dim, a.dec_dim
+        Ld = a.layer_dims
+        F = a.feature_dim
+        # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle, on
+        # side stream 1 (independent of the DPT: overlaps all of it)
+        desc = desc16 = dconf = ev_lf = None
+        if models == 2:
+            desc, desc16, dconf, ev_lf = self._local_features(hooks, G, S, E, D, H, W)
         # act_postprocess + layer_rn (3x3, no bias → F channels): branches 1-3 on side
         # stream 0, branch 0 (the largest) on the current stream
         g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
@@ -621,30 +635,30 @@ class PairModel:
         with self._on(0):
             t1 = self._buf("ap_t1", (Z, S, Ld[1]), BF16)
             o.gemm(hooks["h6"], Hw["ap1_w"], t1, S, Ld[1], D, Z, sA=S * D, sB=Ld[1] * D,
-                   sC=S * Ld[1], bias=Hw["ap1_b"], sBias=Ld[1], wmod=4)
+                   sC=S * Ld[1], bias=Hw["ap1_b"], sBias=Ld[1], wmod=wm)
             L1 = self._buf("ap_L1", (Z, 2 * gh, 2 * gw, Ld[1]), BF16)
             o.gemm(t1, Hw["ap1t_w"], L1, S, 4 * Ld[1], Ld[1], Z, sA=S * Ld[1],
                    sB=4 * Ld[1] * Ld[1], sC=4 * S * Ld[1], bias=Hw["ap1t_b"], sBias=Ld[1],
-                   convt=(2, Ld[1], gw), wmod=4)
+                   convt=(2, Ld[1], gw), wmod=wm)
             self._conv3(L1, "rn1_w", R[1], Z, dims[1][0], dims[1][1], Ld[1], F)
             L2 = self._buf("ap_L2", (Z, gh, gw, Ld[2]), BF16)
             o.gemm(hooks["h9"], Hw["ap2_w"], L2, S, Ld[2], D, Z, sA=S * D, sB=Ld[2] * D,
-                   sC=S * Ld[2], bias=Hw["ap2_b"], sBias=Ld[2], wmod=4)
+                   sC=S * Ld[2], bias=Hw["ap2_b"], sBias=Ld[2], wmod=wm)
             self._conv3(L2, "rn2_w", R[2], Z, gh, gw, Ld[2], F)
             t3 = self._buf("ap_t3", (Z, gh, gw, Ld[3]), BF16)
             o.gemm(hooks["h12"], Hw["ap3_w"], t3, S, Ld[3], D, Z, sA=S * D, sB=Ld[3] * D,
-                   sC=S * Ld[3], bias=Hw["ap3_b"], sBias=Ld[3], wmod=4)
+                   sC=S * Ld[3], bias=Hw["ap3_b"], sBias=Ld[3], wmod=wm)
             L3 = self._buf("ap_L3", (Z, g3h, g3w, Ld[3]), BF16)
             self._conv3(t3, "ap3c_w", L3, Z, gh, gw, Ld[3], Ld[3], stride=2, bias_key="ap3c_b")
             self._conv3(L3, "rn3_w", R[3], Z, g3h, g3w, Ld[3], F)
             ev_ap = self._event()
         t0 = self._buf("ap_t0", (Z, S, Ld[0]), BF16)
         o.gemm(hooks["h0"], Hw["ap0_w"], t0, S, Ld[0], E, Z, sA=S * E, sB=Ld[0] * E,
-               sC=S * Ld[0], bias=Hw["ap0_b"], sBias=Ld[0], wmod=4)
+               sC=S * Ld[0], bias=Hw["ap0_b"], sBias=Ld[0], wmod=wm)
         L0 = self._buf("ap_L0", (Z, 4 * gh, 4 * gw, Ld[0]), BF16)
         o.gemm(t0, Hw["ap0t_w"], L0, S, 16 * Ld[0], Ld[0], Z, sA=S * Ld[0],
                sB=16 * Ld[0] * Ld[0], sC=16 * S * Ld[0], bias=Hw["ap0t_b"], sBias=Ld[0],
-               convt=(4, Ld[0], gw), wmod=4)
+               convt=(4, Ld[0], gw), wmod=wm)
         self._conv3(L0, "rn0_w", R[0], Z, dims[0][0], dims[0][1], Ld[0], F)
         self._wait(ev_ap)
         # refinenets: path_k = up2(out_conv(RCU2(path_{k+1} + RCU1(R_k)))) with the next
@@ -699,15 +713,15 @@ class PairModel:
 
     # ---- monst3r_inference_mono (monst3r_utils.py:187-211) ----
     def mono(self, feat, H, W):
-        """Self-pair decode of one frame's features feat bf16 [1,S,E].  Returns X [2,H,W,3]
-        (res11, res21), C [2,H,W] of the MonST3R heads (the MASt3R half of the batched
-        problem set runs too and is ignored, as its outputs are in the reference)."""
+        """Self-pair decode of one frame's features feat bf16 [1,S,E] by MonST3R alone (2
+        problems: both sides, both heads).  Returns X [2,H,W,3] (res11, res21), C [2,H,W]
+        (views of persistent buffers, overwritten by the next mono call)."""
         a = self.a
         gh, gw = H // a.patch, W // a.patch
         f = feat.reshape(1, gh * gw, a.enc_dim)
-        hooks = self.decode_multi(f, f, gh, gw)
-        pts, conf, _, _, _ = self.heads(hooks, gh, gw, H, W)
-        return pts[0:2], conf[0:2]
+        hooks = self.decode_multi(f, f, gh, gw, models=1)
+        pts, conf, _, _, _ = self.heads(hooks, gh, gw, H, W, models=1)
+        return pts, conf
 
     # ---- monst3r_decode_symmetric_batch (monst3r_utils.py:141-184) ----
     def symmetric(self, feat_i, feat_j, H, W, chunk=4):

@@ -12,8 +12,10 @@ glue (tracker2.py, global_opt2.py, main_monster_slam.py) reads the same:
   monst3r_match_symmetric                 :214-252
   monst3r_inference_mono                  :187-211
   apply_dynamic_mask_to_pointmaps         :300-341   (HIP kernel m3s_apply_dynamic_mask)
-  dynamic_mask_from_flow                  :625-637   (the mask arithmetic of get_dynamic_mask;
-                                                      RAFT / ego-flow / SAM2 are absent code)
+  get_dynamic_mask                        :512-704   (caller's RAFT callable; mono decode,
+                                                      ego flow, error mask on the GPU;
+                                                      SAM2 refinement not provided)
+  ego_flow / dynamic_mask_from_flow       :566-637   (DepthBasedWarping restated: unpinned)
   resize_img / create_frame / Frame       monst3r_utils.py:739-782, frame.py:14-141
 
 Model handles: the reference keeps two nn.Modules; here both weight sets live in ONE
@@ -317,8 +319,89 @@ def monst3r_inference_mono(monst3r, frame):
 
 
 # ---------------------------------------------------------------------------------------
-# dynamic mask (monst3r_utils.py:300-341, 625-637)
+# dynamic mask (monst3r_utils.py:300-341, 512-704)
 # ---------------------------------------------------------------------------------------
+def _quat_rot(q):
+    x, y, z, w = q.unbind(-1)
+    return torch.stack([
+        torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)], -1),
+        torch.stack([2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)], -1),
+        torch.stack([2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)], -1)], -2)
+
+
+def sim3_relative_matrix(T_WC_i, T_WC_j):
+    """lietorch (T_WC_j.inv() * T_WC_i).matrix()[:3] for data tensors [..., 8] (t, q xyzw,
+    s): returns (sR [3,3], t [3]) of T_ji (:566-578), device tensors, no host sync."""
+    Ti, Tj = T_WC_i.reshape(8).float(), T_WC_j.reshape(8).float()
+    Ri, Rj = _quat_rot(Ti[3:7]), _quat_rot(Tj[3:7])
+    si, sj = Ti[7], Tj[7]
+    # T_j^-1 T_i: x → (Rj^T (si Ri x + ti - tj)) / sj
+    sR = (si / sj) * (Rj.t() @ Ri)
+    t = (Rj.t() @ (Ti[:3] - Tj[:3])) / sj
+    return sR, t
+
+
+def _inv3(K):
+    """3x3 inverse by the adjugate (elementwise torch ops: no solver call, graph-capturable)."""
+    a, b, c, d, e, f, g, h, i = K.reshape(9).unbind()
+    co = torch.stack([e * i - f * h, c * h - b * i, b * f - c * e,
+                      f * g - d * i, a * i - c * g, c * d - a * f,
+                      d * h - e * g, b * g - a * h, a * e - b * d]).reshape(3, 3)
+    return co / (a * co[0, 0] + b * co[1, 0] + c * co[2, 0])
+
+
+def ego_flow(pts_i, R_ji, t_ji, K_j, K_i):
+    """Ego-motion flow of frame i's pixels into frame j (the DepthBasedWarping call of
+    :597-604) from the mono pointmap pts_i [..,H,W,3] (depth = z): ego f32 [3,H,W]
+    (flow x, flow y, valid).  HIP kernel m3s_ego_flow; the warp is restated (its source is
+    not in the reference checkout: parity unpinned)."""
+    H, W = pts_i.shape[-3:-1]
+    p = pts_i.reshape(H, W, 3).float().contiguous()
+    _lib.require_cuda(p, names=("pts_i",))
+    prm = torch.cat([R_ji.reshape(9).float(), t_ji.reshape(3).float(),
+                     K_j.reshape(9).float(), _inv3(K_i.reshape(3, 3).float()).reshape(9)
+                     ]).to(p.device).contiguous()
+    ego = torch.empty((3, H, W), dtype=torch.float32, device=p.device)
+    _lib.check(_lib.load().m3s_ego_flow(_lib.ptr(p), _lib.ptr(prm), H, W, _lib.ptr(ego),
+                                        _lib.stream(p.device)), "ego_flow")
+    return ego
+
+
+@torch.inference_mode()
+def get_dynamic_mask(monst3r, raft_model, frame_i, frame_j, threshold=0.35,
+                     refine_with_sam2=True, sam2_predictor=None):
+    """:512-704.  raft_model: the caller's RAFT (called as the reference does,
+    raft_model(img_i_255, img_j_255, iters=20, test_mode=True)[1] → flow [1,2,H,W]); the
+    depth comes from the MonST3R-only mono decode of frame i (res_i pts3d z, :580-587).
+    Returns bool [H,W]; an all-False mask when K is missing or the flow call fails, like
+    the reference.  SAM2 refinement needs the absent SAM2 predictor: requesting it with
+    a predictor raises NotImplementedError (the unrefined mask is what the reference
+    returns when no predictor is given)."""
+    H, W = _hw(frame_i)
+    dev = frame_i.img.device
+    empty = torch.zeros((H, W), dtype=torch.bool, device=dev)
+    if getattr(frame_i, "K", None) is None or getattr(frame_j, "K", None) is None:
+        return empty
+    try:
+        img_i = frame_i.img if frame_i.img.dim() == 4 else frame_i.img[None]
+        img_j = frame_j.img if frame_j.img.dim() == 4 else frame_j.img[None]
+        flow = raft_model((img_i * 0.5 + 0.5) * 255.0, (img_j * 0.5 + 0.5) * 255.0, iters=20,
+                          test_mode=True)[1].reshape(2, H, W)
+    except Exception as e:  # the reference prints and returns the empty mask
+        print(f"Error computing optical flow: {e}")
+        return empty
+    sR, t = sim3_relative_matrix(frame_i.T_WC, frame_j.T_WC)
+    pm = monst3r.pair_model()
+    f = _ensure_feat(pm, frame_i)
+    X, _ = pm.mono(f, H, W)
+    ego = ego_flow(X[0], sR, t, frame_j.K, frame_i.K)
+    mask = dynamic_mask_from_flow(flow, ego, threshold)
+    if refine_with_sam2 and sam2_predictor is not None:
+        raise NotImplementedError("SAM2 refinement (:640-700) needs the SAM2 predictor, "
+                                  "which is not part of this package")
+    return mask
+
+
 def dynamic_mask_from_flow(flow_ij, ego_flow_ij, threshold=0.35):
     """The mask arithmetic of get_dynamic_mask (:625-637): err = |flow - ego_flow[:2]|,
     min-max normalised, > threshold.  flow f32 [2,H,W], ego [>=2,H,W] → bool [H,W].

@@ -34,3 +34,20 @@ def test_square_ok_keeps_square():
     from monst3r_slam_amd.monst3r_utils import resize_img
     img = np.zeros((600, 600, 3), np.float32)
     assert resize_img(img, 512, square_ok=True)["img"].shape == (1, 3, 512, 512)
+
+
+def test_sim3_relative_matrix_matches_lietorch_composition():
+    """T_ji = T_WC_j^-1 T_WC_i as a scaled-rotation matrix + translation (the
+    lietorch .matrix() of monst3r_utils.py:574-578), against the numpy Sim3 algebra."""
+    import numpy as np
+    import torch
+    from monst3r_slam_amd import monst3r_utils as U
+    from monst3r_slam_amd import synthetic as syn
+    Ti = np.array([0.3, -0.2, 0.5, *syn.quat_from_axis_angle([1, 2, 3], 0.4), 1.3], np.float32)
+    Tj = np.array([-0.1, 0.4, 0.2, *syn.quat_from_axis_angle([0, 1, -1], -0.7), 0.8], np.float32)
+    sR, t = U.sim3_relative_matrix(torch.from_numpy(Ti), torch.from_numpy(Tj))
+    Tji = syn.sim3_mul(syn.sim3_inv(Tj), Ti)
+    X = np.random.default_rng(0).normal(size=(50, 3)).astype(np.float32)
+    ref = syn.sim3_act(Tji, X)
+    got = X @ sR.numpy().T + t.numpy()
+    assert np.allclose(got, ref, atol=1e-5)

@@ -182,3 +182,55 @@ def test_dynamic_mask_kernels(dev):
     Dr[e[..., None].expand_as(Dr)] = 0.0
     assert torch.equal(Co, Cr) and torch.equal(Qo, Qr) and torch.equal(Do, Dr)
     assert torch.equal(Xo, X)
+
+
+def test_ego_flow_and_get_dynamic_mask(small, dev):
+    """Ego-motion flow kernel against a float64 torch statement of the same warp (parity
+    with DepthBasedWarping itself is unpinned: its source is absent), then get_dynamic_mask
+    end to end with a stand-in RAFT whose flow is the ego flow plus a moving block: the
+    block (and only it) is flagged."""
+    from monst3r_slam_amd import monst3r_utils as U
+    from monst3r_slam_amd import synthetic as syn
+    m, _ = small
+    H, W = 96, 128
+    g = torch.Generator(device=dev).manual_seed(11)
+    pts = torch.rand(H, W, 3, device=dev, generator=g) + 0.5
+    K = torch.from_numpy(syn.intrinsics(H, W)).to(dev)
+    Ti = torch.tensor([0.1, -0.05, 0.02, *syn.quat_from_axis_angle([0, 1, 0.2], 0.05), 1.1],
+                      dtype=torch.float32, device=dev)
+    Tj = torch.tensor([0.0, 0.0, 0.0, 0, 0, 0, 1, 1.0], dtype=torch.float32, device=dev)
+    sR, t = U.sim3_relative_matrix(Ti, Tj)
+    ego = U.ego_flow(pts, sR, t, K, K)
+    yy, xx = torch.meshgrid(torch.arange(H, device=dev, dtype=torch.float64),
+                            torch.arange(W, device=dev, dtype=torch.float64), indexing="ij")
+    pix = torch.stack([xx, yy, torch.ones_like(xx)], -1)
+    d = 1.0 / (1.0 / (pts[..., 2].double() + 1e-6))
+    cam = (pix @ torch.linalg.inv(K.double()).t()) * d[..., None]
+    proj = (cam @ sR.double().t() + t.double()) @ K.double().t()
+    ref = torch.stack([proj[..., 0] / proj[..., 2] - xx, proj[..., 1] / proj[..., 2] - yy])
+    assert torch.allclose(ego[:2].double(), ref, atol=2e-3, rtol=1e-4)
+    assert bool((ego[2] == 1).all())
+    # end to end: frames with K and poses, RAFT stand-in = ego flow of the mono depth + block
+    fr_i = U.Frame(0, torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1,
+                   torch.tensor([[H, W]]), torch.tensor([[H, W]]), None, T_WC=Ti[None], K=K)
+    fr_j = U.Frame(1, torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1,
+                   torch.tensor([[H, W]]), torch.tensor([[H, W]]), None, T_WC=Tj[None], K=K)
+
+    class Handle:
+        def pair_model(self):
+            return m
+
+    Xm, _ = m.mono(m.encode(fr_i.img)[0], H, W)
+    ego_i = U.ego_flow(Xm[0], sR, t, K, K)
+
+    def raft(a, b, iters=20, test_mode=True):
+        f = ego_i[:2].clone()
+        f[:, 20:40, 30:60] += 25.0
+        return None, f[None]
+
+    fr_i.feat = None
+    mask = U.get_dynamic_mask(Handle(), raft, fr_i, fr_j, threshold=0.35, sam2_predictor=None)
+    assert mask.shape == (H, W) and bool(mask[20:40, 30:60].all())
+    assert int(mask.sum()) == 20 * 30
+    fr_j.K = None
+    assert not bool(U.get_dynamic_mask(Handle(), raft, fr_i, fr_j).any())

@@ -1,0 +1,15 @@
+"""Run only bench.py's configs[4] leg (fp8 512x512 dyn-mask frame), for rocprofv3."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "monst3r-slam_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from monst3r_slam_amd import model as Mdl  # noqa: E402
+
+dev = torch.device("cuda:0")
+m, _ = Mdl.build(dev)
+print(json.dumps(bench.c5_bench(m, dev, int(sys.argv[1]) if len(sys.argv) > 1 else 10)))
