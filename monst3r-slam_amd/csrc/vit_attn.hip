@@ -119,19 +119,33 @@ constexpr int STAGE_BYTES = 2 * TILE_BYTES;
 constexpr uint32_t OOB = 0x80000000u;
 constexpr int PART_LD = HD + 4;            // split partial row: O[64], m, l, pad
 
-// AW waves per block (QT query rows each) share one K/V ring: AW = 4 when the grid has
-// blocks to spare, fewer when (S / 128) x heads x batch would leave CUs idle.
-template <int AW>
-__global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
+// A block is AW query waves (QT query rows each) x KS key splits.  The AW waves of one
+// key split share a K/V ring and walk key tiles ks, ks + KS, ...; at the end the KS
+// partial (O, max, sum) sets of each query wave merge through LDS (no extra launch, no
+// HBM partials).  KS > 1 puts 2-4 waves on every SIMD at the 768-1024-token shapes,
+// whose (S / 128) x heads x batch grids would otherwise leave most SIMDs with one wave
+// (or none) and no second wave to run MFMA while another does the softmax.
+constexpr int RED_FLOATS = 8 * 64 * 4 + 64 * 2;  // one wave's partial: O^T 32x64, m, l
+
+template <int AW, int KS>
+__global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, void* __restrict__ o,
     int64_t ldo, int64_t so_b, int o_fp8, int Sq, int Sk, int heads, float c_log2, int splits,
     int tiles_per_split, float* __restrict__ part) {
-  constexpr int ACH = TILE_BYTES / 16 / (AW * 64);  // DMA chunks per thread per operand
-  __shared__ __attribute__((aligned(16))) char lds[ASTAGES * STAGE_BYTES];
+  constexpr int GT = AW * 64;                        // threads of one key-split group
+  constexpr int ACH = TILE_BYTES / 16 / GT;          // DMA chunks per thread per operand
+  constexpr int NST = KS == 1 ? ASTAGES : 2;         // ring depth per key split
+  static_assert(KS == 1 || (KS - 1) * AW * RED_FLOATS * 4 <= KS * NST * STAGE_BYTES,
+                "partials must fit in the ring");
+  __shared__ __attribute__((aligned(16))) char lds[KS * NST * STAGE_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wall = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wid = wall % AW;          // query wave
+  const int ksp = wall / AW;          // key split inside the block
+  const int gtid = tid - ksp * GT;
+  char* const ring = lds + ksp * NST * STAGE_BYTES;
   const int r = lane & 31, hh = lane >> 5;
   // 1-D grid (query tile fastest, then head, then batch x split) remapped so that each
   // XCD gets a contiguous id range: the query tiles of one head share an XCD and its L2
@@ -174,7 +188,7 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
   uint32_t k_off[ACH], v_off[ACH];
 #pragma unroll
   for (int i = 0; i < ACH; i++) {
-    const int c = i * AW * 64 + tid;
+    const int c = i * GT + gtid;
     const int row = c >> 3, slot = c & 7;
     k_row[i] = row;
     k_off[i] = (uint32_t)(((int64_t)row * ldkv + (slot ^ k_swz(row)) * 8) * 2);
@@ -183,15 +197,18 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
   const int nkt_all = (Sk + AKT - 1) / AKT;
   const int kt0 = sp * tiles_per_split;
   const int nkt = max(0, min(nkt_all - kt0, tiles_per_split));  // tiles of this split
-  auto issue = [&](int ktl, int stage) {
-    const int kt = kt0 + ktl;
-    char* sb = lds + stage * STAGE_BYTES;
+  const int nkt_g = nkt > ksp ? (nkt - ksp + KS - 1) / KS : 0;     // ... of this key split
+  const int nj = (nkt + KS - 1) / KS;                             // uniform trip count
+  // j-th tile of this key split: kt0 + ksp + KS j
+  auto issue = [&](int j, int stage) {
+    const int kt = kt0 + ksp + KS * j;
+    char* sb = ring + stage * STAGE_BYTES;
     const uint32_t t0 = (uint32_t)((int64_t)kt * AKT * ldkv * 2);
 #pragma unroll
     for (int i = 0; i < ACH; i++) {
       const bool ok = kt * AKT + k_row[i] < Sk;
-      glds16(rK, sb + (i * AW * 64 + wid * 64) * 16, ok ? t0 + k_off[i] : OOB);
-      glds16(rV, sb + TILE_BYTES + (i * AW * 64 + wid * 64) * 16, ok ? t0 + v_off[i] : OOB);
+      glds16(rK, sb + (i * GT + wid * 64) * 16, ok ? t0 + k_off[i] : OOB);
+      glds16(rV, sb + TILE_BYTES + (i * GT + wid * 64) * 16, ok ? t0 + v_off[i] : OOB);
     }
   };
 
@@ -205,19 +222,15 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
   const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gsel = (lane >> 4) & 1;
 
 #pragma unroll
-  for (int st = 0; st < ASTAGES - 1; st++)
-    if (st < nkt) issue(st, st);
+  for (int st = 0; st < NST - 1; st++)
+    if (st < nkt_g) issue(st, st);
 
   // one key tile; TAIL (the last, partial tile only) masks keys >= Sk — a separate
   // instantiation, so full tiles carry no per-score masking code
-  auto tile = [&](int ktl, auto tail_tag) {
+  auto tile = [&](int j, auto tail_tag) {
     constexpr bool TAIL = decltype(tail_tag)::value;
-    const int kt = kt0 + ktl;
-    if (ktl + 1 < nkt) vm_wait<2 * ACH>();
-    else vm_wait<0>();
-    block_sync_lds();
-    if (ktl + ASTAGES - 1 < nkt) issue(ktl + ASTAGES - 1, (ktl + ASTAGES - 1) % ASTAGES);
-    const char* sK = lds + (ktl % ASTAGES) * STAGE_BYTES;
+    const int kt = kt0 + ksp + KS * j;
+    const char* sK = ring + (j % NST) * STAGE_BYTES;
     const char* sV = sK + TILE_BYTES;
 
     // S^T (keys x queries), two 32-key halves
@@ -307,9 +320,53 @@ __global__ __launch_bounds__(AW * 64, 2) void attn_kernel(
     }
 #undef M3S_VT
   };
-  for (int ktl = 0; ktl < nkt; ktl++) {
-    if ((kt0 + ktl + 1) * AKT > Sk) tile(ktl, std::true_type{});
-    else tile(ktl, std::false_type{});
+  // every wave runs nj trips (s_barrier is block-wide); a key split with fewer tiles
+  // idles through its last trip
+  for (int j = 0; j < nj; j++) {
+    if (NST >= 3 && j + 1 < nkt_g) vm_wait<2 * ACH>();
+    else vm_wait<0>();
+    block_sync_lds();
+    if (j + NST - 1 < nkt_g) issue(j + NST - 1, (j + NST - 1) % NST);
+    if (j < nkt_g) {
+      if ((kt0 + ksp + KS * j + 1) * AKT > Sk) tile(j, std::true_type{});
+      else tile(j, std::false_type{});
+    }
+  }
+  if constexpr (KS > 1) {
+    // merge the key splits of each query wave: lane-aligned (same accumulator layout)
+    block_sync_lds();  // ring reads done (the last trip waited for all DMA)
+    float* red = reinterpret_cast<float*>(lds);
+    if (ksp > 0) {
+      float* P = red + ((ksp - 1) * AW + wid) * RED_FLOATS;
+#pragma unroll
+      for (int i4 = 0; i4 < 8; i4++)
+        reinterpret_cast<float4*>(P)[i4 * 64 + lane] =
+            make_float4(oacc[i4 >> 2][(i4 & 3) * 4], oacc[i4 >> 2][(i4 & 3) * 4 + 1],
+                        oacc[i4 >> 2][(i4 & 3) * 4 + 2], oacc[i4 >> 2][(i4 & 3) * 4 + 3]);
+      reinterpret_cast<float2*>(P + 2048)[lane] = make_float2(m, l);
+    }
+    block_sync_lds();
+    if (ksp > 0) return;
+#pragma unroll
+    for (int s2 = 1; s2 < KS; s2++) {
+      const float* P = red + ((s2 - 1) * AW + wid) * RED_FLOATS;
+      const float2 ml = reinterpret_cast<const float2*>(P + 2048)[lane];
+      const float M = fmaxf(m, ml.x);
+      // a split that saw no keys has m = -inf and l = 0: weight 0, never inf - inf
+      const float a0 = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - M) * c_log2);
+      const float a1 = ml.x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((ml.x - M) * c_log2);
+#pragma unroll
+      for (int i4 = 0; i4 < 8; i4++) {
+        const float4 w = reinterpret_cast<const float4*>(P)[i4 * 64 + lane];
+        const int d = i4 >> 2, e = (i4 & 3) * 4;
+        oacc[d][e] = oacc[d][e] * a0 + w.x * a1;
+        oacc[d][e + 1] = oacc[d][e + 1] * a0 + w.y * a1;
+        oacc[d][e + 2] = oacc[d][e + 2] * a0 + w.z * a1;
+        oacc[d][e + 3] = oacc[d][e + 3] * a0 + w.w * a1;
+      }
+      l = l * a0 + ml.y * a1;
+      m = M;
+    }
   }
   if (qrow >= Sq) return;
   if (part) {  // split: unnormalised O, running max m and sum l → [split][b][h][q][68] f32
@@ -435,13 +492,23 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   if (sk * ld_kv * 2 >= 0x7ffffff0) return M3S_ERR_TOO_LARGE;  // 31-bit buffer offsets
   if (((uintptr_t)d_o) % 8 || ld_o % 4 || stride_o % 4) return M3S_ERR_INVALID_ARG;
   const float c_log2 = 0.125f * 1.4426950408889634f;  // head_dim^-0.5 * log2(e)
-  // AW waves per block share each K/V tile; AW = 2 (tuning override only) doubles the
-  // grid.  Key splits (flash-decoding; partials merged by attn_combine_kernel) are
+  // Grid-level key splits (flash-decoding; partials merged by attn_combine_kernel) are
   // available through M3S_ATTN_SPLITS: measured on the 768-token shapes, the combine
-  // pass costs what the wider grid saves, so the default is one split.
-  int aw = 4;
+  // pass costs what the wider grid saves, so the default is one split; the in-block
+  // splits below get the parallelism without the extra pass.
+  // In-block key splits by the size of the plain grid (tools/attn_ks_tune.py, 768 / 1024
+  // tokens): <= 128 blocks of 4 query waves (the encoder) → 2 query waves x 4 key splits
+  // (16.8 → 9.8 us at 768 tokens); <= 256 (mono decode) → 4 x 2; <= 768 (pair decode) →
+  // 2 x 2; larger grids (keyframe-graph batches) fill the chip without splitting.
   const int64_t hb = heads * batch;
+  const int64_t b4 = m3s_div_up(sq, 4 * QT) * hb;
+  int aw = 4, ks = 1;
+  if (b4 <= 128) aw = 2, ks = 4;
+  else if (b4 <= 256) aw = 4, ks = 2;
+  else if (b4 <= 768) aw = 2, ks = 2;
   if (const char* e = getenv("M3S_ATTN_AW")) aw = atoi(e) == 2 ? 2 : 4;
+  if (const char* e = getenv("M3S_ATTN_KS")) ks = atoi(e) >= 4 ? 4 : atoi(e) >= 2 ? 2 : 1;
+  if (ks == 4) aw = 2;   // 8 waves per block at most
   const int nkt = (int)m3s_div_up(sk, AKT);
   int splits = 1;
   if (const char* e = getenv("M3S_ATTN_SPLITS")) splits = std::max(1, std::min(nkt, atoi(e)));
@@ -453,16 +520,19 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   if ((int64_t)m3s_div_up(sq, 2 * QT) * hb * splits >= (1ll << 31)) return M3S_ERR_TOO_LARGE;
   float* part = splits > 1 ? reinterpret_cast<float*>(d_workspace) : nullptr;
   hipStream_t s = m3s_stream(stream);
-#define M3S_ATTN_LAUNCH(AWV)                                                                 \
-  hipLaunchKernelGGL(attn_kernel<AWV>,                                                      \
+#define M3S_ATTN_LAUNCH(AWV, KSV)                                                            \
+  hipLaunchKernelGGL((attn_kernel<AWV, KSV>),                                               \
                      dim3((unsigned)(m3s_div_up(sq, AWV * QT) * heads * batch * splits)),    \
-                     dim3(AWV * 64), 0, s,                                                   \
+                     dim3(AWV * KSV * 64), 0, s,                                             \
                      reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,                   \
                      reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
                      ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,          \
                      (int)sk, (int)heads, c_log2, splits, tps, part)
-  if (aw == 2) M3S_ATTN_LAUNCH(2);
-  else M3S_ATTN_LAUNCH(4);
+  if (ks == 4) M3S_ATTN_LAUNCH(2, 4);
+  else if (ks == 2 && aw == 2) M3S_ATTN_LAUNCH(2, 2);
+  else if (ks == 2) M3S_ATTN_LAUNCH(4, 2);
+  else if (aw == 2) M3S_ATTN_LAUNCH(2, 1);
+  else M3S_ATTN_LAUNCH(4, 1);
   if (splits > 1) {
     M3S_LAUNCH_CHECK();
     const int64_t rows = hb * sq;

@@ -121,8 +121,10 @@ def test_convtranspose_scatter(ops, dev, s):
     assert _rel(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("S,heads,batch", [(768, 16, 1), (196, 12, 4), (12, 4, 2)])
-def test_attention(ops, dev, S, heads, batch):
+@pytest.mark.parametrize("S,heads,batch", [(768, 16, 1), (196, 12, 4), (12, 4, 2), (1024, 12, 2)])
+@pytest.mark.parametrize("ks", ["1", "2", "4"])
+def test_attention(ops, dev, monkeypatch, S, heads, batch, ks):
+    monkeypatch.setenv("M3S_ATTN_KS", ks)
     g = torch.Generator(device=dev).manual_seed(4)
     C = heads * 64
     qkv = torch.randn(batch, S, 3 * C, device=dev, generator=g).bfloat16()
@@ -232,11 +234,15 @@ def test_full_model_vs_fp32_restatement(dev):
     _compare_pair(out, X, C, D, Q, "full-vs-fp32")
 
 
-@pytest.mark.parametrize("splits", ["1", "3", "5"])
-def test_attention_key_splits(ops, dev, monkeypatch, splits):
-    """Flash-decoding key splits (partial O, max, sum merged by the combine kernel) with a
-    ragged last key tile and a ragged last split: Sk = 300 = 4 x 64 + 44."""
+@pytest.mark.parametrize("splits,ks", [("1", "1"), ("3", "1"), ("5", "1"), ("1", "2"),
+                                       ("1", "4"), ("3", "2"), ("1", "8")])
+def test_attention_key_splits(ops, dev, monkeypatch, splits, ks):
+    """Flash-decoding key splits (partial O, max, sum merged by the combine kernel) and
+    in-block key splits (merged through LDS; ks=8 clamps to 4) with a ragged last key tile
+    and a ragged last split: Sk = 300 = 4 x 64 + 44 (ks=4 x splits=3: a key split with no
+    tile)."""
     monkeypatch.setenv("M3S_ATTN_SPLITS", splits)
+    monkeypatch.setenv("M3S_ATTN_KS", ks)
     g = torch.Generator(device=dev).manual_seed(9)
     Sq, Sk, heads = 200, 300, 2
     D = heads * 64
