@@ -63,10 +63,11 @@ class Tracker:
         captured graph sees the previous frame's matches."""
         self.idx_f2k = torch.arange(n, device=device, dtype=torch.int64)[None].contiguous()
 
-    def track(self, img, T_WCf_init=None):
+    def track(self, img, T_WCf_init=None, feat_i=None):
         """One frame.  Returns dict(new_kf, lost, T_WCf, idx_f2k, match_frac, info, ...);
-        the scalar flags are device tensors."""
-        out = self.model.pair(img, feat_j=self.kf.feat)
+        the scalar flags are device tensors.  feat_i: the frame's encoder features if
+        already computed (FramePipeline)."""
+        out = self.model.pair(img, feat_j=self.kf.feat, feat_i=feat_i)
         return self.track_outputs(out, T_WCf_init)
 
     def track_outputs(self, out, T_WCf_init=None):
@@ -122,3 +123,35 @@ class Tracker:
         return dict(new_kf=new_kf, lost=lost, T_WCf=T_WCf, T_CkCf=T_CkCf, idx_f2k=idx,
                     valid_match=valid_match, match_frac=match_frac, info=info,
                     feat_i=out.get("feat_i"), pair=out)
+
+
+class FramePipeline:
+    """Streaming tracking with the next frame's encoder prefetched: the MonST3R encoder of
+    frame t+1 depends only on its image, so it runs on a side stream concurrently with
+    frame t's decoders, heads, matching and pose solve (which leave most CUs idle at 768
+    tokens).  Per-frame work and results are those of Tracker.track; only the schedule
+    changes.  Features are double-buffered: step(k) tracks the frame encoded by the
+    previous step into buffer k % 2 and encodes the next frame into buffer (k + 1) % 2."""
+
+    def __init__(self, tracker, shape_hw):
+        self.tr = tracker
+        m = tracker.model
+        H, W = shape_hw
+        S = (H // m.a.patch) * (W // m.a.patch)
+        self.feat = [torch.empty((1, S, m.a.enc_dim), dtype=torch.bfloat16, device=m.dev)
+                     for _ in range(2)]
+        self.side = torch.cuda.Stream(m.dev)
+
+    def prime(self, img, k=0):
+        """Encode the first frame into buffer k % 2 (on the current stream)."""
+        self.tr.model.encode(img, out=self.feat[k % 2])
+
+    def step(self, img_cur, img_next, k, T_WCf_init=None):
+        main = torch.cuda.current_stream(self.tr.model.dev)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self.tr.model.encode(img_next, out=self.feat[(k + 1) % 2])
+        res = self.tr.track(img_cur, T_WCf_init, feat_i=self.feat[k % 2])
+        main.wait_stream(self.side)
+        return res
+

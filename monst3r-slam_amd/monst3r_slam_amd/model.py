@@ -52,7 +52,7 @@ class Ops:
     def __init__(self, dev):
         self.lib = _lib.load()
         self.dev = dev
-        self.probe = None  # list → (start_event, end_event, flops, fp8) per GEMM (bench roofline)
+        self.record = None  # list → (descriptor, flops, fp8) per GEMM launch (bench roofline)
         # f32 split-K / attention-split scratch, one per stream (the M = 768 GEMMs split K
         # when their grid cannot fill 256 CUs; concurrent streams must not share it)
         self._ws = {}
@@ -105,15 +105,15 @@ class Ops:
         if rope is not None:  # (cos/sin table, rotated columns, tokens per image)
             d.flags |= _lib.EPI_ROPE
             d.rope_table, d.rope_cols, d.rope_tokens = _p(rope[0]), rope[1], rope[2]
-        if self.probe is not None:
-            st = torch.cuda.current_stream(self.dev)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            _lib.check(self.lib.m3s_vit_gemm(ctypes.byref(d), self._s()), "vit_gemm")
-            e1.record(st)
-            self.probe.append((e0, e1, 2.0 * M * N * K * batch, fp8 is not None))
-            return
+        if self.record is not None:  # (descriptor copy, flops, fp8) for the bench replay
+            dc = _lib.GemmDesc()
+            ctypes.memmove(ctypes.byref(dc), ctypes.byref(d), ctypes.sizeof(d))
+            self.record.append((dc, 2.0 * M * N * K * batch, fp8 is not None))
         _lib.check(self.lib.m3s_vit_gemm(ctypes.byref(d), self._s()), "vit_gemm")
+
+    def replay_gemm(self, desc):
+        """Re-issue a recorded GEMM descriptor on the current stream (bench roofline)."""
+        _lib.check(self.lib.m3s_vit_gemm(ctypes.byref(desc), self._s()), "vit_gemm")
 
     def ln(self, x, g, b, y, rows, dim, batch=1, sx=0, sy=0, sp=0, y_f32=False, xor=0, pmod=0):
         """y dtype picks the output: bf16, f32 (or y_f32) or uint8/float8_e4m3fn (e4m3)."""
@@ -695,8 +695,10 @@ class PairModel:
         self._fusion(k, sp, skip, b, h, w, next_hw, None, out)
 
     # ---- monst3r_asymmetric_inference ----
-    def pair(self, img_i, feat_j=None, img_j=None):
+    def pair(self, img_i, feat_j=None, img_j=None, feat_i=None):
         """Frame i vs keyframe j (keyframe features cached as in monst3r_utils.py:262-269).
+        feat_i: frame i's encoder features when already computed (the prefetched encode of
+        frontend.FramePipeline); img_i then only gives the size.
         Returns dict X [2,H,W,3] (ii, ji), C [2,H,W], D16 f16 [2,H,W,24], D f32, Q [2,H,W],
         feat_i (to cache when the frame becomes a keyframe)."""
         a = self.a
@@ -705,7 +707,10 @@ class PairModel:
         if feat_j is None:
             feat_j, _ = self.encode(img_j)
             feat_j = feat_j.clone()
-        feat_i, pos = self.encode(img_i)
+        if feat_i is None:
+            feat_i, pos = self.encode(img_i)
+        else:
+            pos = self.positions(1, gh, gw)
         hooks = self.decode(feat_i[0], feat_j.reshape(-1, a.enc_dim), pos, gh, gw)
         pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W)
         return dict(X=pts[0:2], C=conf[0:2], D16=desc16, D=desc, Q=dconf, feat_i=feat_i,

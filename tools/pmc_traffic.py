@@ -2,7 +2,8 @@
 (tools/gpu_cmd_r1z.sh): FETCH_SIZE and WRITE_SIZE in separate passes, KiB units; on gfx950
 FETCH_SIZE reports half the bytes of 16-B-per-lane streaming reads (MI355X_MICROARCH.md
 §HBM), so reads are doubled.  The last eager pair inference of the run is used (the
-bench's serial roofline probe: patchify_kernel .. local_feat_kernel).
+bench's serial roofline probe: patchify_kernel .. the head.2 conv with the fused DPT tail,
+gemm_kernel<..., 517, ...> = BIAS|RELU|DPT_OUT; run the bench with --no-c5 --no-graph).
 Writes profiles/<out>.json: per-launch and per-pair GEMM bytes, plus the L2 hit rate.
 Usage: python tools/pmc_traffic.py gpurun_out/prof profiles/r01_pmc_gemm_traffic.json"""
 import collections
@@ -26,9 +27,9 @@ def load(path, counters):
 def last_pair(meta):
     ids = sorted(meta)
     starts = [d for d in ids if "patchify_kernel" in meta[d]]
-    ends = [d for d in ids if "dpt_out_kernel" in meta[d]]
-    e = ends[-1]
-    s = max(d for d in starts if d < e)
+    ends = [d for d in ids if "gemm_kernel" in meta[d] and ", 517," in meta[d]]
+    s = starts[-1]                       # the eager pair of the roofline replay recording
+    e = min(d for d in ends if d > s)    # (its GEMM-only replay graph follows)
     return [d for d in ids if s <= d <= e]
 
 
