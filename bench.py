@@ -53,6 +53,10 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="skip the keyframe-graph (C4) leg")
     ap.add_argument("--graph-steps", type=int, default=2)
     ap.add_argument("--no-c5", action="store_true", help="skip the fp8 512x512 dyn-mask leg")
+    ap.add_argument("--main-priority", type=int, default=0, help="tracking-chain stream priority")
+    ap.add_argument("--side-priority", type=int, default=0, help="prefetch stream priority")
+    ap.add_argument("--no-split-heads", action="store_true",
+                    help="run the MASt3R DPT heads batched on the tracking chain")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="encode each frame inside its own step (no next-frame encoder overlap)")
     ap.add_argument("--streams", action="store_true",
@@ -61,27 +65,47 @@ def parse():
 
 
 def setup(dev, seed):
+    """Model (seeded random weights), the synthetic frame / keyframe images, and the
+    tracking inputs.  The ViT runs on the images; its random-weight pointmaps carry no
+    geometry (no valid matches: every frame would be 'lost' after one GN iteration), so
+    matching, the Sim3 GN and the keyframe fusion run on the analytic 384x512 pointmaps /
+    descriptors of the synthetic scene (synthetic.pair) against a keyframe displaced by a
+    known Sim3 — the tracker does its real iterations every frame."""
+    import numpy as np
     from monst3r_slam_amd import model as Mdl
+    from monst3r_slam_amd import synthetic as syn
     from monst3r_slam_amd.frontend import Tracker
     model, _ = Mdl.build(dev)
     g = torch.Generator(device=dev).manual_seed(100 + seed)
     img_k = torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1
     img_f = torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1
+    rng = np.random.default_rng(seed)
+    X11, X21, D11, D21 = syn.pair(H, W, seed=seed, shift_px=(1.5, -0.75))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    glue = dict(X=t(np.stack([X11, X21])),
+                C=t((1.0 + np.exp(rng.normal(1.0, 0.5, size=(2, H, W)))).astype(np.float32)),
+                D16=t(np.stack([D11, D21]).astype(np.float16)),
+                Q=t((1.0 + np.exp(rng.normal(1.0, 0.5, size=(2, H, W)))).astype(np.float32)))
+    T_true = np.array([0.02, -0.01, 0.03, *syn.quat_from_axis_angle([0.3, 1.0, 0.2], 0.02), 1.0],
+                      np.float32)
+    Xk = t(syn.sim3_act(T_true, X21).reshape(-1, 3))
+    Ck = torch.full((H * W, 1), 2.0, device=dev)
     tr = Tracker(model)
     T0 = torch.tensor([0, 0, 0, 0, 0, 0, 1, 1], dtype=torch.float32, device=dev)
-    tr.add_keyframe(img_k, T0)
-    return model, tr, img_f
+    feat_k = model.encode(img_k)[0].clone()
+    tr.add_keyframe(img_k, T0, X=Xk, C=Ck, feat=feat_k)
+    return model, tr, img_f, glue
 
 
-def capture(fn, dev):
-    s = torch.cuda.Stream(dev)
+def capture(fn, dev, priority=0):
+    s = torch.cuda.Stream(dev, priority=priority)
     s.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s):
         fn()
     torch.cuda.current_stream(dev).wait_stream(s)
     torch.cuda.synchronize(dev)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, stream=s):
         fn()
     torch.cuda.synchronize(dev)
     return g
@@ -332,16 +356,31 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
-    model, tr, img_f = setup(dev, rank)
+    model, tr, img_f, glue = setup(dev, rank)
     model.serial = not args.streams
+    tr.split_heads = not args.no_split_heads
 
     from monst3r_slam_amd.frontend import FramePipeline
-    pipe = None if args.no_prefetch else FramePipeline(tr, (H, W))
+    pipe = None if args.no_prefetch else FramePipeline(tr, (H, W), args.side_priority)
 
     def step(k=0):
-        if pipe is None:
-            return tr.track(img_f)
-        return pipe.step(img_f, img_f, k)   # synthetic stream: every frame is img_f
+        """One tracked frame: pair inference on the frame image (encoder output prefetched
+        by the previous step unless --no-prefetch; this step encodes the next frame on the
+        side stream), then matching + GN + fusion on the synthetic scene's pointmaps."""
+        main = torch.cuda.current_stream(dev)
+        feat_i = None
+        if pipe is not None:
+            pipe.side.wait_stream(main)
+            with torch.cuda.stream(pipe.side):
+                model.encode(img_f, out=pipe.feat[(k + 1) % 2])   # every frame is img_f
+            feat_i = pipe.feat[k % 2]
+        out = model.pair(img_f, feat_j=tr.kf.feat, feat_i=feat_i, split_heads=tr.split_heads)
+        res = tr.track_outputs(glue)
+        model.join()
+        if pipe is not None:
+            main.wait_stream(pipe.side)
+        res["pair"] = out
+        return res
 
     if pipe is not None:
         pipe.prime(img_f, 0)
@@ -349,8 +388,8 @@ def main():
         step(2 * w)
     torch.cuda.synchronize(dev)
     # two graphs with the feature double-buffer parities swapped, replayed alternately
-    g_steps = None if args.eager else [capture(lambda: step(0), dev),
-                                       capture(lambda: step(1), dev)]
+    g_steps = None if args.eager else [capture(lambda: step(0), dev, args.main_priority),
+                                       capture(lambda: step(1), dev, args.main_priority)]
     g_pair = None if args.eager else capture(lambda: model.pair(img_f, feat_j=tr.kf.feat), dev)
 
     if world > 1:
@@ -372,6 +411,8 @@ def main():
         elapsed = float(t.item())
 
     if rank == 0:
+        res = step(0)
+        gn_info = [int(v) for v in res["info"].tolist()]   # iterations, fail, converged
         pair_ms = time_replays(g_pair, dev, max(5, args.steps // 2)) if g_pair else None
         roof = gemm_roofline(model, img_f, tr.kf.feat, dev)
         pmc = pmc_traffic()
@@ -388,14 +429,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (seeded random images and weights; no checkpoints offline)",
+            "data": "synthetic (seeded random images and weights, no checkpoints offline; "
+                    "matching/GN/fusion on the analytic pointmaps of the synthetic scene)",
             "config": {"workload": "tracking step 384x512: MonST3R+MASt3R pair inference + "
                                    "projective matching + Sim3 ray GN (configs[1]+[2])",
-                       "schedule": "serial" if pipe is None else
-                                   "next frame's encoder prefetched on a side stream",
+                       "schedule": ("serial" if pipe is None else
+                                    "next frame's encoder prefetched on a side stream") +
+                                   ("" if args.no_split_heads else
+                                    "; MASt3R DPT heads on a side stream"),
                        "h": H, "w": W, "models": "MonST3R ViT-L/B dpt + MASt3R ViT-L/B catmlp+dpt",
                        "parallelism": f"replicas{world}"},
             "pair_inference_ms": pair_ms,
+            "tracker_gn": {"iterations": gn_info[0], "fail": gn_info[1], "converged": gn_info[2]},
             "roofline": {"bound": "mfma", "achieved": roof["tflops"], "peak": BF16_DENSE_TFLOPS,
                          "unit": "TFLOP/s", "frac": roof["tflops"] / BF16_DENSE_TFLOPS,
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,

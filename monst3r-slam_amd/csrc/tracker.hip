@@ -7,8 +7,10 @@
 //     cdna_hip_programming.md §6 G16): f64 reduction of the partials in fixed block order
 //     (deterministic), 7x7 Cholesky, tau = H^-1 g, T <- Exp(tau) * T (lietorch retr),
 //     check_convergence (nonlinear_optimizer.py:5-25, NaN-aware on iteration 0), done flag.
-// All max_iters iterations are enqueued without a host sync; once the flag is set the
-// remaining launches return at entry.
+// Default: all iterations in one persistent launch (track_persistent_kernel, grid
+// barrier per iteration, every workgroup takes the same step); M3S_TRACK_PERSISTENT=0
+// enqueues one launch per iteration instead (the remaining ones return at entry once
+// the done flag is set).
 #include "common.h"
 #include "sim3.h"
 
@@ -16,6 +18,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kBlocks = 512;
+constexpr int kPersistentBlocks = 256;  // one per CU: co-resident next to other kernels
 constexpr int kAcc = 36;  // 28 H upper, 7 g, 1 cost
 
 enum : int { TRACK_RAYS = 0, TRACK_CALIB = 1 };
@@ -90,27 +93,16 @@ __global__ void track_init_kernel(const float* __restrict__ Twc_k, const float* 
 __device__ void track_solve(TrackState* st, const float* partial, int nblocks, float rel_error,
                             float delta_norm);
 
+// per-point residuals / Jacobians of the points k = first, first + stride, ... into acc
 template <int MODE>
-__global__ __launch_bounds__(kThreads) void track_iter_kernel(
-    TrackState* __restrict__ st, TrackParams prm, const float* __restrict__ K,
-    const float* __restrict__ Xf, const float* __restrict__ Xk, const float* __restrict__ Qk,
-    const uint8_t* __restrict__ valid, const float* __restrict__ meas_k,
-    const uint8_t* __restrict__ valid_meas, int64_t n, float* __restrict__ partial,
-    float rel_error, float delta_norm) {
-  if (st->done) return;
-  if (MODE == TRACK_CALIB) {
-    prm.fx = K[0];
-    prm.fy = K[4];
-    prm.cx = K[2];
-    prm.cy = K[5];
-  }
-  float T[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) T[i] = st->T[i];
-  float acc[kAcc];
-#pragma unroll
-  for (int l = 0; l < kAcc; l++) acc[l] = 0.f;
-
+__device__ __forceinline__ void track_points(const float* T, const TrackParams& prm,
+                                             const float* __restrict__ Xf,
+                                             const float* __restrict__ Xk,
+                                             const float* __restrict__ Qk,
+                                             const uint8_t* __restrict__ valid,
+                                             const float* __restrict__ meas_k,
+                                             const uint8_t* __restrict__ valid_meas, int64_t n,
+                                             float* acc) {
   for (int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x; k < n;
        k += (int64_t)gridDim.x * kThreads) {
     const float X[3] = {Xf[3 * k], Xf[3 * k + 1], Xf[3 * k + 2]};
@@ -177,6 +169,10 @@ __global__ __launch_bounds__(kThreads) void track_iter_kernel(
       }
     }
   }
+}
+
+// wave butterfly + LDS: the workgroup's 36 sums → out[0..35] (threads < kAcc write)
+__device__ __forceinline__ void block_partial(const float* acc, float* out) {
   __shared__ float red[kThreads / M3S_WAVE][kAcc];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -189,8 +185,33 @@ __global__ __launch_bounds__(kThreads) void track_iter_kernel(
     float v = red[0][threadIdx.x];
 #pragma unroll
     for (int w = 1; w < kThreads / M3S_WAVE; w++) v += red[w][threadIdx.x];
-    partial[blockIdx.x * kAcc + threadIdx.x] = v;
+    out[threadIdx.x] = v;
   }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void track_iter_kernel(
+    TrackState* __restrict__ st, TrackParams prm, const float* __restrict__ K,
+    const float* __restrict__ Xf, const float* __restrict__ Xk, const float* __restrict__ Qk,
+    const uint8_t* __restrict__ valid, const float* __restrict__ meas_k,
+    const uint8_t* __restrict__ valid_meas, int64_t n, float* __restrict__ partial,
+    float rel_error, float delta_norm) {
+  if (st->done) return;
+  if (MODE == TRACK_CALIB) {
+    prm.fx = K[0];
+    prm.fy = K[4];
+    prm.cx = K[2];
+    prm.cy = K[5];
+  }
+  float T[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) T[i] = st->T[i];
+  float acc[kAcc];
+#pragma unroll
+  for (int l = 0; l < kAcc; l++) acc[l] = 0.f;
+
+  track_points<MODE>(T, prm, Xf, Xk, Qk, valid, meas_k, valid_meas, n, acc);
+  block_partial(acc, partial + blockIdx.x * kAcc);
   // publish this workgroup's partial row; the last to arrive reduces and solves
   __shared__ unsigned s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -212,10 +233,9 @@ __global__ __launch_bounds__(kThreads) void track_iter_kernel(
   track_solve(st, partial, (int)gridDim.x, rel_error, delta_norm);
 }
 
-__device__ void track_solve(TrackState* st, const float* partial, int nblocks, float rel_error,
-                            float delta_norm) {
-  __shared__ double sacc[kAcc];
-  // f64 reduction of the partials: lane-per-(accumulator, block-slice), then fixed order
+// f64 reduction of nblocks partial rows in fixed order (deterministic): every thread of
+// the workgroup takes part; the 36 sums land in sacc (shared)
+__device__ void reduce_partials(const float* partial, int nblocks, double* sacc) {
   const int tid = threadIdx.x;
   __shared__ double tmp[kThreads / M3S_WAVE][kAcc];
   for (int l = 0; l < kAcc; l++) {
@@ -231,7 +251,14 @@ __device__ void track_solve(TrackState* st, const float* partial, int nblocks, f
     sacc[tid] = v;
   }
   __syncthreads();
-  if (tid != 0) return;
+}
+
+// One Gauss-Newton step on the reduced sums (one thread): 7x7 Cholesky (failure → the
+// reference's CholeskyError, frame lost), tau = H^-1 g, T <- Exp(tau) * T (lietorch retr),
+// check_convergence (nonlinear_optimizer.py:5-25; rel_dec is NaN on iteration 0).
+// Returns 0 = continue, 1 = converged, 2 = Cholesky failure.
+__device__ int gn_step(const double* sacc, float* T, double* old_cost, float rel_error,
+                       float delta_norm) {
   double H[7][7], g[7];
   int l = 0;
   for (int n = 0; n < 7; n++)
@@ -242,28 +269,17 @@ __device__ void track_solve(TrackState* st, const float* partial, int nblocks, f
     }
   for (int n = 0; n < 7; n++) g[n] = sacc[28 + n];
   const double new_cost = sacc[35];
-  // Cholesky H = L L^T (torch.linalg.cholesky raises on failure → frame lost)
   double L[7][7] = {};
-  bool ok = true;
-  for (int j = 0; j < 7 && ok; j++) {
+  for (int j = 0; j < 7; j++) {
     double s = H[j][j];
     for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
-    if (!(s > 0.0)) {
-      ok = false;
-      break;
-    }
+    if (!(s > 0.0)) return 2;
     L[j][j] = sqrt(s);
     for (int i = j + 1; i < 7; i++) {
       double t = H[i][j];
       for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
       L[i][j] = t / L[j][j];
     }
-  }
-  st->ticket = 0;  // next iteration (next launch) counts from zero again
-  if (!ok) {
-    st->fail = 1;
-    st->done = 1;
-    return;
   }
   double y[7], x[7];
   for (int i = 0; i < 7; i++) {
@@ -279,22 +295,128 @@ __device__ void track_solve(TrackState* st, const float* partial, int nblocks, f
   float tau[7];
   for (int i = 0; i < 7; i++) tau[i] = (float)x[i];
   float t1[3], q1[4], s1;
-  m3s_retr_sim3<float>(tau, st->T, st->T + 3, st->T[7], t1, q1, &s1);
-  for (int i = 0; i < 3; i++) st->T[i] = t1[i];
-  for (int i = 0; i < 4; i++) st->T[3 + i] = q1[i];
-  st->T[7] = s1;
-  // check_convergence: rel_dec = |(old - new) / old| (NaN on iteration 0: inf/inf)
-  const double old_cost = st->old_cost;
-  const double rel_dec = fabs((old_cost - new_cost) / old_cost);
+  m3s_retr_sim3<float>(tau, T, T + 3, T[7], t1, q1, &s1);
+  for (int i = 0; i < 3; i++) T[i] = t1[i];
+  for (int i = 0; i < 4; i++) T[3 + i] = q1[i];
+  T[7] = s1;
+  const double rel_dec = fabs((*old_cost - new_cost) / *old_cost);
   float dn = 0.f;
   for (int i = 0; i < 7; i++) dn += tau[i] * tau[i];
   dn = sqrtf(dn);
+  *old_cost = new_cost;
+  return (rel_dec < (double)rel_error || dn < delta_norm) ? 1 : 0;
+}
+
+__device__ void track_solve(TrackState* st, const float* partial, int nblocks, float rel_error,
+                            float delta_norm) {
+  __shared__ double sacc[kAcc];
+  reduce_partials(partial, nblocks, sacc);
+  if (threadIdx.x != 0) return;
+  st->ticket = 0;  // next iteration (next launch) counts from zero again
+  float T[8];
+  for (int i = 0; i < 8; i++) T[i] = st->T[i];
+  double oc = st->old_cost;
+  const int r = gn_step(sacc, T, &oc, rel_error, delta_norm);
+  if (r == 2) {
+    st->fail = 1;
+    st->done = 1;
+    return;
+  }
+  for (int i = 0; i < 8; i++) st->T[i] = T[i];
+  st->old_cost = oc;
   st->iters += 1;
-  if (rel_dec < (double)rel_error || dn < delta_norm) {
+  if (r == 1) {
     st->conv = 1;
     st->done = 1;
   }
-  st->old_cost = new_cost;
+}
+
+// All Gauss-Newton iterations in ONE launch: nb co-resident workgroups (nb <= 256, a few
+// registers' worth of occupancy, so they fit beside whatever else runs) accumulate their
+// points' partial rows, meet at a grid barrier (monotonic agent-scope counter), then EVERY
+// workgroup reduces the same partials in the same order and takes the same step — the
+// pose never needs a broadcast and the next iteration starts straight away.  Partials
+// are double-buffered by iteration parity (a workgroup can be at most one barrier ahead).
+// Exit: convergence, Cholesky failure, max_iters, or a barrier wait beyond ~0.2 s
+// (st->fail = 3: co-residency broken), reached by every wave.
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void track_persistent_kernel(
+    TrackState* __restrict__ st, TrackParams prm, const float* __restrict__ K,
+    const float* __restrict__ Xf, const float* __restrict__ Xk, const float* __restrict__ Qk,
+    const uint8_t* __restrict__ valid, const float* __restrict__ meas_k,
+    const uint8_t* __restrict__ valid_meas, int64_t n, float* __restrict__ partial,
+    int max_iters, float rel_error, float delta_norm) {
+  if (MODE == TRACK_CALIB) {
+    prm.fx = K[0];
+    prm.fy = K[4];
+    prm.cx = K[2];
+    prm.cy = K[5];
+  }
+  __shared__ float sT[8];
+  __shared__ int s_status;
+  __shared__ double sacc[kAcc];
+  const int nb = gridDim.x;
+  unsigned* bar = &st->ticket;
+  float T[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) T[i] = st->T[i];
+  double old_cost = st->old_cost;
+  int it = 0, status = 0;
+  for (; it < max_iters; it++) {
+    float acc[kAcc];
+#pragma unroll
+    for (int l = 0; l < kAcc; l++) acc[l] = 0.f;
+    track_points<MODE>(T, prm, Xf, Xk, Qk, valid, meas_k, valid_meas, n, acc);
+    float* slot = partial + (size_t)(it & 1) * nb * kAcc;
+    block_partial(acc, slot + blockIdx.x * kAcc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (unsigned)(it + 1) * (unsigned)nb;
+      int timeout = 0;
+      for (long spins = 0;
+           __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; spins++) {
+        __builtin_amdgcn_s_sleep(2);
+        if (spins > (1l << 22)) {
+          timeout = 1;
+          break;
+        }
+      }
+      s_status = timeout ? 3 : 0;
+    }
+    __syncthreads();
+    if (s_status == 3) {
+      status = 3;
+      break;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    reduce_partials(slot, nb, sacc);
+    if (threadIdx.x == 0) {
+      const int r = gn_step(sacc, T, &old_cost, rel_error, delta_norm);
+      s_status = r;
+      if (r != 2)
+        for (int i = 0; i < 8; i++) sT[i] = T[i];
+    }
+    __syncthreads();
+    status = s_status;
+    if (status == 2) break;
+#pragma unroll
+    for (int i = 0; i < 8; i++) T[i] = sT[i];
+    if (status == 1) {
+      it++;
+      break;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (int i = 0; i < 8; i++) st->T[i] = T[i];
+    st->old_cost = old_cost;
+    st->iters = it;
+    st->fail = status == 3 ? 3 : (status == 2 ? 1 : 0);
+    st->conv = status == 1 ? 1 : 0;
+    st->done = 1;
+  }
 }
 
 __global__ void track_finish_kernel(const float* __restrict__ Twc_k, const TrackState* st,
@@ -344,12 +466,23 @@ int run_track(const float* Twc_k, const float* Twc_f, const float* Xf, const flo
   float* partial = reinterpret_cast<float*>(w + L.partial);
   hipLaunchKernelGGL(track_init_kernel, dim3(1), dim3(64), 0, s, Twc_k, Twc_f, st);
   M3S_LAUNCH_CHECK();
-  int nb = (int)((n + kThreads - 1) / kThreads);
-  if (nb > kBlocks) nb = kBlocks;
-  for (int it = 0; it < max_iters; it++) {
-    hipLaunchKernelGGL(track_iter_kernel<MODE>, dim3(nb), dim3(kThreads), 0, s, st, prm, K, Xf,
-                       Xk, Qk, valid, meas_k, valid_meas, n, partial, rel_error, delta_norm);
-    M3S_LAUNCH_CHECK();
+  const char* e = getenv("M3S_TRACK_PERSISTENT");  // A/B: 0 = one launch per iteration
+  if (!e || atoi(e) != 0) {
+    int nb = (int)((n + kThreads - 1) / kThreads);
+    if (nb > kPersistentBlocks) nb = kPersistentBlocks;
+    if (max_iters > 0)
+      hipLaunchKernelGGL(track_persistent_kernel<MODE>, dim3(nb), dim3(kThreads), 0, s, st, prm,
+                         K, Xf, Xk, Qk, valid, meas_k, valid_meas, n, partial, max_iters,
+                         rel_error, delta_norm);
+  } else {
+    int nb = (int)((n + kThreads - 1) / kThreads);
+    if (nb > kBlocks) nb = kBlocks;
+    for (int it = 0; it < max_iters; it++) {
+      hipLaunchKernelGGL(track_iter_kernel<MODE>, dim3(nb), dim3(kThreads), 0, s, st, prm, K,
+                         Xf, Xk, Qk, valid, meas_k, valid_meas, n, partial, rel_error,
+                         delta_norm);
+      M3S_LAUNCH_CHECK();
+    }
   }
   hipLaunchKernelGGL(track_finish_kernel, dim3(1), dim3(64), 0, s, Twc_k, st, T_WCf, T_CkCf,
                      info);

@@ -45,6 +45,7 @@ class Tracker:
         self.cfg = cfg or _config
         self.idx_f2k = None
         self.kf = None
+        self.split_heads = False   # measured: no gain
 
     def add_keyframe(self, img, T_WC, X=None, C=None, feat=None):
         if feat is None:
@@ -67,8 +68,13 @@ class Tracker:
         """One frame.  Returns dict(new_kf, lost, T_WCf, idx_f2k, match_frac, info, ...);
         the scalar flags are device tensors.  feat_i: the frame's encoder features if
         already computed (FramePipeline)."""
-        out = self.model.pair(img, feat_j=self.kf.feat, feat_i=feat_i)
-        return self.track_outputs(out, T_WCf_init)
+        # the MASt3R DPT heads (outputs the tracking never reads) overlap the MonST3R
+        # heads, matching and the pose solve on a side stream; joined before returning
+        out = self.model.pair(img, feat_j=self.kf.feat, feat_i=feat_i,
+                              split_heads=self.split_heads)
+        res = self.track_outputs(out, T_WCf_init)
+        self.model.join()
+        return res
 
     def track_outputs(self, out, T_WCf_init=None):
         """tracker2.py:127-270 on the pair-inference outputs X [2,H,W,3] (ii, ji), C [2,H,W],
@@ -133,14 +139,14 @@ class FramePipeline:
     changes.  Features are double-buffered: step(k) tracks the frame encoded by the
     previous step into buffer k % 2 and encodes the next frame into buffer (k + 1) % 2."""
 
-    def __init__(self, tracker, shape_hw):
+    def __init__(self, tracker, shape_hw, side_priority=0):
         self.tr = tracker
         m = tracker.model
         H, W = shape_hw
         S = (H // m.a.patch) * (W // m.a.patch)
         self.feat = [torch.empty((1, S, m.a.enc_dim), dtype=torch.bfloat16, device=m.dev)
                      for _ in range(2)]
-        self.side = torch.cuda.Stream(m.dev)
+        self.side = torch.cuda.Stream(m.dev, priority=side_priority)
 
     def prime(self, img, k=0):
         """Encode the first frame into buffer k % 2 (on the current stream)."""

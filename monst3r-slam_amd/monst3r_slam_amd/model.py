@@ -324,6 +324,10 @@ class PairModel:
         self.side = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
         self.serial = True
         self.fp8 = False
+        self._tag = None      # buffer-key prefix of the head set being issued (split heads)
+        self._wbase = 0       # first head-weight stack of that set
+        self._wm = 4
+        self._ev_heads = None
 
     def set_fp8(self, on=True):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
@@ -369,7 +373,7 @@ class PairModel:
     def _buf(self, key, shape, dtype):
         """Persistent scratch per (name, shape, dtype): a buffer is never freed or
         reallocated, so HIP graphs captured over it stay valid when other batch sizes run."""
-        k = (key, tuple(shape), dtype)
+        k = (self._tag, key, tuple(shape), dtype)
         t = self._bufs.get(k)
         if t is None:
             t = torch.empty(shape, dtype=dtype, device=self.dev)
@@ -541,12 +545,12 @@ class PairModel:
     # ---- DPT heads (batched over z) ----
     def _conv3(self, x, wkey, out, b, hin, win, cin, cout, stride=1, bias_key=None, R=None,
                flags=0, dpt=None):
-        o, H = self.ops, self.w.h
+        o, H = self.ops, self._hw
         hout = (hin + 2 - 3) // stride + 1
         wout = (win + 2 - 3) // stride + 1
-        o.gemm(x, H[wkey], out, hout * wout, cout, 9 * cin, b, sA=hin * win * cin,
+        o.gemm(x, H(wkey), out, hout * wout, cout, 9 * cin, b, sA=hin * win * cin,
                sB=cout * 9 * cin, sC=hout * wout * cout,
-               bias=H[bias_key] if bias_key else None, sBias=cout, R=R,
+               bias=H(bias_key) if bias_key else None, sBias=cout, R=R,
                sR=hout * wout * cout, flags=flags, conv=(hin, win, cin, hout, wout, stride),
                wmod=self._wm, dpt=dpt)
         return hout, wout
@@ -565,7 +569,7 @@ class PairModel:
         """FeatureFusionBlock (dpt_block.py:185-218) at resolution (h, w):
         s = path + RCU1(skip) (path given; skip None for refinenet4); s = RCU2(s);
         out = up2(out_conv(s)) (+ next_skip)  — out_conv commuted before the upsample."""
-        o, H = self.ops, self.w.h
+        o, H = self.ops, self._hw
         F = self.a.feature_dim
         s1 = self._buf(("fus_s1", h, w), (b, h, w, F), BF16)
         if skip is not None:
@@ -576,8 +580,8 @@ class PairModel:
         s2 = self._buf(("fus_s2", h, w), (b, h, w, F), BF16)
         self._rcu(s1, k, 2, b, h, w, s2)
         oc = self._buf(("fus_oc", h, w), (b, h, w, F), BF16)
-        o.gemm(s2, H[f"r{k}_out_w"], oc, h * w, F, F, b, sA=h * w * F, sB=F * F, sC=h * w * F,
-               bias=H[f"r{k}_out_b"], sBias=F, wmod=self._wm)
+        o.gemm(s2, H(f"r{k}_out_w"), oc, h * w, F, F, b, sA=h * w * F, sB=F * F, sC=h * w * F,
+               bias=H(f"r{k}_out_b"), sBias=F, wmod=self._wm)
         oh, ow = next_hw
         o.up2(oc, out, b, h, w, F, oh, ow, add=next_skip)
 
@@ -608,25 +612,66 @@ class PairModel:
             ev_lf = self._event()
         return desc, desc16, dconf, ev_lf
 
-    def heads(self, hooks, gh, gw, H, W, models=2):
+    def _hw(self, key):
+        """Head weight stack `key` from the current set's first stack (split heads)."""
+        t = self.w.h[key]
+        return t[self._wbase:] if self._wbase else t
+
+    def heads(self, hooks, gh, gw, H, W, models=2, split=False):
         """DPT heads of all 2*models*G problems (z = (g*models + model)*2 + side, head weights
         z % (2*models)) + MASt3R local features of the model-1 problems (models=2 only).
+        split (one pair, G = 1): the MASt3R DPT heads — whose pts3d/conf the tracking never
+        reads (monst3r_utils.py:290) — are issued on side stream 0 as their own 2-problem
+        set, concurrent with the MonST3R heads, the local features and the caller's
+        matching / pose solve; the caller joins with `join()` before the next frame.
         Returns pts3d f32 [Z,H,W,3], conf f32 [Z,H,W], desc16 f16 [2G,H,W,24],
         desc f32 [2G,H,W,24], desc_conf f32 [2G,H,W] (the latter three: (g, side) of model 1;
         None with models=1)."""
-        o, a, Hw = self.ops, self.a, self.w.h
+        a = self.a
         Z = hooks["h0"].shape[0]
         wm = 2 * models
-        self._wm = wm
         G = Z // wm
+        S, E, D = gh * gw, a.enc_dim, a.dec_dim
+        pts = self._buf("pts3d", (Z, H, W, 3), F32)
+        conf = self._buf("conf", (Z, H, W), F32)
+        split = split and models == 2 and G == 1
+        if split:
+            main = torch.cuda.current_stream(self.dev)
+            side = self.side[0]
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                sub = {k: v[2:4] for k, v in hooks.items()}
+                self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4])
+                self._ev_heads = torch.cuda.Event()
+                self._ev_heads.record(side)
+        # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle
+        desc = desc16 = dconf = ev_lf = None
+        if models == 2:
+            self._wm = wm
+            desc, desc16, dconf, ev_lf = self._local_features(hooks, G, S, E, D, H, W)
+        if split:
+            sub = {k: v[0:2] for k, v in hooks.items()}
+            self._dpt(sub, gh, gw, H, W, 2, 0, 2, None, pts[0:2], conf[0:2])
+        else:
+            self._dpt(hooks, gh, gw, H, W, Z, 0, wm, None, pts, conf)
+        self._wait(ev_lf)
+        return pts, conf, desc16, desc, dconf
+
+    def join(self):
+        """Current stream waits for the split MASt3R heads (heads(split=True))."""
+        if self._ev_heads is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self._ev_heads)
+            self._ev_heads = None
+
+    def _dpt(self, hooks, gh, gw, H, W, Z, wbase, wm, tag, pts, conf):
+        """act_postprocess + refinenets + head of Z problems whose hooks are given (views),
+        head weights from stack wbase with weight_mod wm, scratch keyed by tag."""
+        o, a = self.ops, self.a
+        self._tag, self._wbase, self._wm = tag, wbase, wm
+        Hw = self._hw
         S, E, D = gh * gw, a.enc_dim, a.dec_dim
         Ld = a.layer_dims
         F = a.feature_dim
-        # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle, on
-        # side stream 1 (independent of the DPT: overlaps all of it)
-        desc = desc16 = dconf = ev_lf = None
-        if models == 2:
-            desc, desc16, dconf, ev_lf = self._local_features(hooks, G, S, E, D, H, W)
         # act_postprocess + layer_rn (3x3, no bias → F channels): branches 1-3 on side
         # stream 0, branch 0 (the largest) on the current stream
         g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
@@ -634,30 +679,30 @@ class PairModel:
         R = [self._buf(f"rn{k}", (Z, dims[k][0], dims[k][1], F), BF16) for k in range(4)]
         with self._on(0):
             t1 = self._buf("ap_t1", (Z, S, Ld[1]), BF16)
-            o.gemm(hooks["h6"], Hw["ap1_w"], t1, S, Ld[1], D, Z, sA=S * D, sB=Ld[1] * D,
-                   sC=S * Ld[1], bias=Hw["ap1_b"], sBias=Ld[1], wmod=wm)
+            o.gemm(hooks["h6"], Hw("ap1_w"), t1, S, Ld[1], D, Z, sA=S * D, sB=Ld[1] * D,
+                   sC=S * Ld[1], bias=Hw("ap1_b"), sBias=Ld[1], wmod=wm)
             L1 = self._buf("ap_L1", (Z, 2 * gh, 2 * gw, Ld[1]), BF16)
-            o.gemm(t1, Hw["ap1t_w"], L1, S, 4 * Ld[1], Ld[1], Z, sA=S * Ld[1],
-                   sB=4 * Ld[1] * Ld[1], sC=4 * S * Ld[1], bias=Hw["ap1t_b"], sBias=Ld[1],
+            o.gemm(t1, Hw("ap1t_w"), L1, S, 4 * Ld[1], Ld[1], Z, sA=S * Ld[1],
+                   sB=4 * Ld[1] * Ld[1], sC=4 * S * Ld[1], bias=Hw("ap1t_b"), sBias=Ld[1],
                    convt=(2, Ld[1], gw), wmod=wm)
             self._conv3(L1, "rn1_w", R[1], Z, dims[1][0], dims[1][1], Ld[1], F)
             L2 = self._buf("ap_L2", (Z, gh, gw, Ld[2]), BF16)
-            o.gemm(hooks["h9"], Hw["ap2_w"], L2, S, Ld[2], D, Z, sA=S * D, sB=Ld[2] * D,
-                   sC=S * Ld[2], bias=Hw["ap2_b"], sBias=Ld[2], wmod=wm)
+            o.gemm(hooks["h9"], Hw("ap2_w"), L2, S, Ld[2], D, Z, sA=S * D, sB=Ld[2] * D,
+                   sC=S * Ld[2], bias=Hw("ap2_b"), sBias=Ld[2], wmod=wm)
             self._conv3(L2, "rn2_w", R[2], Z, gh, gw, Ld[2], F)
             t3 = self._buf("ap_t3", (Z, gh, gw, Ld[3]), BF16)
-            o.gemm(hooks["h12"], Hw["ap3_w"], t3, S, Ld[3], D, Z, sA=S * D, sB=Ld[3] * D,
-                   sC=S * Ld[3], bias=Hw["ap3_b"], sBias=Ld[3], wmod=wm)
+            o.gemm(hooks["h12"], Hw("ap3_w"), t3, S, Ld[3], D, Z, sA=S * D, sB=Ld[3] * D,
+                   sC=S * Ld[3], bias=Hw("ap3_b"), sBias=Ld[3], wmod=wm)
             L3 = self._buf("ap_L3", (Z, g3h, g3w, Ld[3]), BF16)
             self._conv3(t3, "ap3c_w", L3, Z, gh, gw, Ld[3], Ld[3], stride=2, bias_key="ap3c_b")
             self._conv3(L3, "rn3_w", R[3], Z, g3h, g3w, Ld[3], F)
             ev_ap = self._event()
         t0 = self._buf("ap_t0", (Z, S, Ld[0]), BF16)
-        o.gemm(hooks["h0"], Hw["ap0_w"], t0, S, Ld[0], E, Z, sA=S * E, sB=Ld[0] * E,
-               sC=S * Ld[0], bias=Hw["ap0_b"], sBias=Ld[0], wmod=wm)
+        o.gemm(hooks["h0"], Hw("ap0_w"), t0, S, Ld[0], E, Z, sA=S * E, sB=Ld[0] * E,
+               sC=S * Ld[0], bias=Hw("ap0_b"), sBias=Ld[0], wmod=wm)
         L0 = self._buf("ap_L0", (Z, 4 * gh, 4 * gw, Ld[0]), BF16)
-        o.gemm(t0, Hw["ap0t_w"], L0, S, 16 * Ld[0], Ld[0], Z, sA=S * Ld[0],
-               sB=16 * Ld[0] * Ld[0], sC=16 * S * Ld[0], bias=Hw["ap0t_b"], sBias=Ld[0],
+        o.gemm(t0, Hw("ap0t_w"), L0, S, 16 * Ld[0], Ld[0], Z, sA=S * Ld[0],
+               sB=16 * Ld[0] * Ld[0], sC=16 * S * Ld[0], bias=Hw("ap0t_b"), sBias=Ld[0],
                convt=(4, Ld[0], gw), wmod=wm)
         self._conv3(L0, "rn0_w", R[0], Z, dims[0][0], dims[0][1], Ld[0], F)
         self._wait(ev_ap)
@@ -679,13 +724,10 @@ class PairModel:
         o.up2(hd0, hup, Z, h2, w2, F // 2, H, W)
         # conv3x3 → last_dim + ReLU with the 1x1 (last_dim → 4) + reg_dense_depth / conf
         # fused into its epilogue: the 128-channel map never reaches HBM
-        pts = self._buf("pts3d", (Z, H, W, 3), F32)
-        conf = self._buf("conf", (Z, H, W), F32)
         self._conv3(hup, "head2_w", pts, Z, H, W, F // 2, a.last_dim, bias_key="head2_b",
                     flags=_lib.EPI_RELU,
-                    dpt=(Hw["head4_w"], Hw["head4_b"], pts, conf, a.conf_min))
-        self._wait(ev_lf)
-        return pts, conf, desc16, desc, dconf
+                    dpt=(Hw("head4_w"), Hw("head4_b"), pts, conf, a.conf_min))
+        self._tag, self._wbase = None, 0
 
     def _fusion_skip(self, k, path, skip, b, h, w, next_hw, out):
         """refinenet_k(path, skip): s = path + RCU1(skip) = conv2(...) + (skip + path)."""
@@ -695,12 +737,14 @@ class PairModel:
         self._fusion(k, sp, skip, b, h, w, next_hw, None, out)
 
     # ---- monst3r_asymmetric_inference ----
-    def pair(self, img_i, feat_j=None, img_j=None, feat_i=None):
+    def pair(self, img_i, feat_j=None, img_j=None, feat_i=None, split_heads=False):
         """Frame i vs keyframe j (keyframe features cached as in monst3r_utils.py:262-269).
         feat_i: frame i's encoder features when already computed (the prefetched encode of
         frontend.FramePipeline); img_i then only gives the size.
         Returns dict X [2,H,W,3] (ii, ji), C [2,H,W], D16 f16 [2,H,W,24], D f32, Q [2,H,W],
-        feat_i (to cache when the frame becomes a keyframe)."""
+        feat_i (to cache when the frame becomes a keyframe).  split_heads: the MASt3R DPT
+        heads (mast3r_X / mast3r_C) finish asynchronously on a side stream — call join()
+        before reading them or starting the next pair."""
         a = self.a
         H, W = img_i.shape[-2:]
         gh, gw = H // a.patch, W // a.patch
@@ -712,7 +756,7 @@ class PairModel:
         else:
             pos = self.positions(1, gh, gw)
         hooks = self.decode(feat_i[0], feat_j.reshape(-1, a.enc_dim), pos, gh, gw)
-        pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W)
+        pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W, split=split_heads)
         return dict(X=pts[0:2], C=conf[0:2], D16=desc16, D=desc, Q=dconf, feat_i=feat_i,
                     mast3r_X=pts[2:4], mast3r_C=conf[2:4])
 

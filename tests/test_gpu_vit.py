@@ -433,3 +433,23 @@ def test_fp8_model_vs_fp32_restatement_512(dev):
     assert stats["X_med"] < 0.08 and stats["C_med"] < 0.08, stats
     assert stats["D_cos_med"] > 0.97 and stats["Q_med"] < 0.15, stats
     m.set_fp8(False)
+
+
+def test_split_heads_match_batched(dev):
+    """pair(split_heads=True): MASt3R DPT heads as their own 2-problem set on a side stream
+    (joined), MonST3R heads as another — same outputs as the 4-problem batched heads up
+    to the bf16 GEMM tiling (tile shapes may differ with the batch), descriptors exact."""
+    from monst3r_slam_amd import model as Mdl
+    m, _ = Mdl.build(dev, small=True)
+    g = torch.Generator(device=dev).manual_seed(41)
+    img_i = torch.rand(1, 3, 96, 128, device=dev, generator=g) * 2 - 1
+    img_j = torch.rand(1, 3, 96, 128, device=dev, generator=g) * 2 - 1
+    a = {k: v.clone() for k, v in m.pair(img_i, img_j=img_j).items() if torch.is_tensor(v)}
+    b = m.pair(img_i, img_j=img_j, split_heads=True)
+    m.join()
+    b = {k: v.clone() for k, v in b.items() if torch.is_tensor(v)}
+    for k in ("X", "mast3r_X"):
+        assert _rel(b[k], a[k]) < 1e-2, k
+    for k in ("C", "mast3r_C"):
+        assert _rel(b[k], a[k]) < 1e-2, k
+    assert torch.equal(b["D16"], a["D16"]) and torch.equal(b["Q"], a["Q"])
