@@ -185,7 +185,17 @@ enum {
   M3S_IN_FP8 = 1024,      /* A and B are OCP fp8 e4m3 (1 byte; K, lda, ldb, strides % 16
                              == 0; GEMM mode only): scaled-MFMA 32x32x64 path; the f32
                              accumulator is multiplied by col_scale[n] before the epilogue */
-  M3S_EPI_OUT_FP8 = 2048  /* store C as OCP fp8 e4m3 (saturated to ±448)           */
+  M3S_EPI_OUT_FP8 = 2048, /* store C as OCP fp8 e4m3 (saturated to ±448)           */
+  M3S_EPI_LN_STATS = 4096, /* producer of a LayerNorm input (the f32 residual stream; GEMM
+                             mode, N % 128 == 0, f32 out): also stores a bf16 copy of C to
+                             C2 and, per row and 128-column group, (mean, M2) of the stored
+                             values to stats — the row statistics a LN_FOLD consumer needs */
+  M3S_EPI_LN_FOLD = 8192  /* consumer: A is the bf16 copy of LayerNorm's INPUT x and B the
+                             weight with gamma folded in (B[n][k] = W[n][k] gamma[k]); the
+                             epilogue forms LN(x) W^T + b = rstd (acc - mean c1[n]) + c2[n]
+                             with mean / rstd from the producer's stats (Chan's combination
+                             of the groups, fixed order), c1 = ln_c1 (row sums of B) and
+                             bias = c2 = b + W beta.  GEMM mode; no split-K, no fp8 */
 };
 
 typedef struct {
@@ -213,6 +223,14 @@ typedef struct {
   const float* col_scale;                  /* IN_FP8: f32 [N] per weight batch (dequant of
                                               A·B: activation scale x weight row scale) */
   int64_t stride_col_scale;                /* IN_FP8: elements between batches (weight_mod) */
+  void* C2;                                /* LN_STATS: bf16 copy of C (ldc / strideC)  */
+  float* stats;                            /* LN_STATS out / LN_FOLD in: f32 [batch][M][groups][2]
+                                              (mean, M2) per 128-column group of a row     */
+  int32_t stats_groups;                    /* LN_FOLD: groups per row (LayerNorm dim / 128, ≤ 8) */
+  int32_t a_batch_xor;                     /* LN_FOLD: batch g reads A and stats of g ^ this
+                                              (the decoder's norm_y of the other side)     */
+  const float* ln_c1;                      /* LN_FOLD: f32 [N] per weight batch (strideBias) */
+  float ln_eps;                            /* LN_FOLD: LayerNorm eps                       */
 } m3s_gemm_desc;
 
 /* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 8 == 0; conv: Cin % 32 == 0.

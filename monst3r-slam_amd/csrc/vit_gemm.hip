@@ -66,7 +66,81 @@ struct Args {
   float dpt_conf_min;
   const float* cscale;     // IN_FP8: per-column dequant scale, batch stride sCscale
   int64_t sCscale;
+  bf16_t* C2;              // LN_STATS: bf16 copy of C
+  float* stats;            // LN_STATS out / LN_FOLD in: [batch][M][groups] x (mean, M2)
+  int a_xor;               // LN_FOLD: A and stats of batch g ^ a_xor
+  const float* ln_c1;      // LN_FOLD: row sums of the gamma-folded weight (stride sBias)
+  float ln_eps;
 };
+
+// Row statistics of a LN_FOLD consumer from the producer's per-128-column (mean_t, M2_t)
+// groups (all of equal size, so no pairwise weights): mean = Σ mean_t / G,
+// M2 = Σ M2_t + 128 Σ (mean_t − mean)², biased variance M2 / (128 G) as nn.LayerNorm.
+// Fixed order → deterministic.  mu / rstd of row m of batch gs; groups ≤ 8.
+__device__ __forceinline__ void ln_row_stats(const Args& a, int64_t gs, int m, int groups,
+                                             float& mu, float& rs) {
+  const float2* st = reinterpret_cast<const float2*>(a.stats) + (gs * a.M + m) * groups;
+  float2 s[8];
+#pragma unroll
+  for (int t = 0; t < 8; t++) s[t] = t < groups ? st[t] : make_float2(0.f, 0.f);
+  float sm = 0.f, m2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; t++) sm += s[t].x;
+  const float mean = sm / (float)groups;
+#pragma unroll
+  for (int t = 0; t < 8; t++) {
+    const float d = t < groups ? s[t].x - mean : 0.f;
+    m2 += fmaf(128.f * d, d, s[t].y);
+  }
+  mu = mean;
+  rs = 1.0f / sqrtf(m2 / (128.f * (float)groups) + a.ln_eps);
+}
+
+// Sum over the 16 lanes of a DPP row (xor 1, xor 2 in the quad, then half-row and row
+// mirrors pair every lane with the other half): 4 VALU ops with DPP operands.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float sum16(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  return v;
+}
+
+// LN_STATS producer: (mean, M2) of the 128 columns [n, n + 128) of row m held by 16
+// consecutive lanes (8 values each; n = 8·(lane % 16) + group base), written by the
+// group's first lane.  All 16 lanes of a group are active together (rows are uniform).
+__device__ __forceinline__ void ln_group_stats(const Args& a, int64_t g, int m, int n,
+                                               const float* x) {
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; t++) s += x[t];
+  s = sum16(s);
+  const float mean = s * (1.0f / 128.0f);
+  float q = 0.f;
+#pragma unroll
+  for (int t = 0; t < 8; t++) {
+    const float d = x[t] - mean;
+    q = fmaf(d, d, q);
+  }
+  q = sum16(q);
+  if ((threadIdx.x & 15) == 0) {
+    const int groups = a.N >> 7;
+    reinterpret_cast<float2*>(a.stats)[(g * a.M + m) * groups + (n >> 7)] = make_float2(mean, q);
+  }
+}
+
+__device__ __forceinline__ void store_bf16x8(bf16_t* p, const float* x) {
+  bf16x8 o;
+#pragma unroll
+  for (int t = 0; t < 8; t++) o[t] = f2bf(x[t]);
+  *reinterpret_cast<bf16x8*>(p) = o;
+}
 
 // ---------------------------------------------------------------------------------------
 // epilogue
@@ -320,7 +394,7 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
   const int wm = wid / WN, wn = wid % WN;
 
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(a.A + (int64_t)g * a.sA), (short)0, NUM_RECORDS, 0x00020000);
+      const_cast<bf16_t*>(a.A + (int64_t)(g ^ a.a_xor) * a.sA), (short)0, NUM_RECORDS, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>(a.B + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sB), (short)0,
       NUM_RECORDS, 0x00020000);
@@ -479,11 +553,16 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
       }
   };
   auto stage_of = [&](int t) { return lds + (t % STAGES) * C::ST_BYTES; };
-  if (nk > 0) {
-    const int ahead = min(nk - 1, STAGES - 2);
-    if (STAGES >= 4 && ahead >= 2) vm_wait<C::L * 2>();
+  // retire the oldest DMA tile, leaving `ahead` (≤ STAGES - 2) younger tiles in flight
+  auto wait_ahead = [&](int ahead) {
+    if (STAGES >= 6 && ahead >= 4) vm_wait<C::L * (STAGES >= 6 ? 4 : 0)>();
+    else if (STAGES >= 5 && ahead >= 3) vm_wait<C::L * (STAGES >= 5 ? 3 : 0)>();
+    else if (STAGES >= 4 && ahead >= 2) vm_wait<C::L * 2>();
     else if (ahead >= 1) vm_wait<C::L>();
     else vm_wait<0>();
+  };
+  if (nk > 0) {
+    wait_ahead(min(nk - 1, STAGES - 2));
     block_sync_lds();
     read_frags(0, lds, 0);
   }
@@ -517,9 +596,7 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
         mfmas(cur);
         __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
         // retire tile kt+1: tiles kt+2 .. kt+STAGES-1 (STAGES-2 of them) stay in flight
-        if (STAGES >= 4) vm_wait<C::L * 2>();
-        else if (STAGES == 3) vm_wait<C::L>();
-        else vm_wait<0>();
+        vm_wait<C::L * (STAGES - 2)>();
         block_sync_lds();
         read_frags(cur ^ 1, stage_of(kt + 1), 0);
       }
@@ -543,9 +620,7 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
       } else {
         mfmas(cur);
         if (kt + 1 < nk) {
-          if (STAGES >= 4 && nk - 2 - kt >= 2) vm_wait<C::L * 2>();
-          else if (STAGES >= 3 && nk - 2 - kt >= 1) vm_wait<C::L>();
-          else vm_wait<0>();
+          wait_ahead(min(nk - 2 - kt, STAGES - 2));
           block_sync_lds();
           read_frags(cur ^ 1, stage_of(kt + 1), 0);
         }
@@ -581,6 +656,14 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
   const bool vec = EPI >= 0 ? true : (a.vec != 0);
   const bool vec_path = !SPLIT && vec && en < a.N;
   float e_b[8], e_pb[8], e_x[EG][16];
+  float e_c1[8], e_pc1[8], e_mu[EG], e_rs[EG];  // LN_FOLD: c1 columns, row mean / rstd
+  // LN_FOLD: the 16 lanes of a row group own rows er0 + v·RSTEP (v < NV ≤ 16); lane v
+  // combines the statistics of row v once, the others read it by lane shuffle
+  float ln_mu = 0.f, ln_rs = 0.f;
+  static_assert(NV <= 16, "one row per lane of the group");
+  if ((fl & M3S_EPI_LN_FOLD) && !SPLIT && (lane & 15) < NV)
+    ln_row_stats(a, g ^ a.a_xor, min(m0 + er0 + (lane & 15) * RSTEP, a.M - 1), a.K >> 7, ln_mu,
+                 ln_rs);
   Epi e = make_epi(a, g);
   e.flags = fl;
   const bool e_rope = (fl & M3S_EPI_ROPE) && en < a.rope_cols;
@@ -588,6 +671,11 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
 #pragma unroll
     for (int u = 0; u < EG; u++) {
       const int m = min(m0 + er0 + (v0 + u) * RSTEP, a.M - 1);  // rows ≥ M are not stored
+      if (fl & M3S_EPI_LN_FOLD) {  // row v0 + u's statistics, held by lane v0 + u of the row group
+        const int src = (lane & ~15) | (v0 + u);
+        e_mu[u] = __shfl(ln_mu, src, 64);
+        e_rs[u] = __shfl(ln_rs, src, 64);
+      }
 #pragma unroll
       for (int t = 0; t < 16; t++) e_x[u][t] = 0.f;
       if (fl & M3S_EPI_RES_F32) {
@@ -621,6 +709,16 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
         *reinterpret_cast<float4*>(&e_pb[0]) = *reinterpret_cast<const float4*>(e.bias + (en ^ 16));
         *reinterpret_cast<float4*>(&e_pb[4]) =
             *reinterpret_cast<const float4*>(e.bias + (en ^ 16) + 4);
+      }
+    }
+    if (fl & M3S_EPI_LN_FOLD) {
+      const float* c1 = a.ln_c1 + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sBias;
+      *reinterpret_cast<float4*>(&e_c1[0]) = *reinterpret_cast<const float4*>(c1 + en);
+      *reinterpret_cast<float4*>(&e_c1[4]) = *reinterpret_cast<const float4*>(c1 + en + 4);
+      if (e_rope) {
+        *reinterpret_cast<float4*>(&e_pc1[0]) = *reinterpret_cast<const float4*>(c1 + (en ^ 16));
+        *reinterpret_cast<float4*>(&e_pc1[4]) =
+            *reinterpret_cast<const float4*>(c1 + (en ^ 16) + 4);
       }
     }
     e_prefetch(0);
@@ -748,8 +846,22 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
         const int m = m0 + er0 + (v0 + u) * RSTEP;
         if (m >= a.M) continue;
         float* x = xv[u];
+        if (fl & M3S_EPI_LN_FOLD) {  // LN(x) W^T + b = rstd (acc - mean c1) + c2
 #pragma unroll
-        for (int t = 0; t < 8; t++) x[t] += e_b[t];
+          for (int t = 0; t < 8; t++) x[t] = fmaf(e_rs[u], fmaf(-e_mu[u], e_c1[t], x[t]), e_b[t]);
+          if (rope_now) {  // the partner columns' final values
+#pragma unroll
+            for (int t = 0; t < 8; t++)
+              pv[u][t] = fmaf(e_rs[u], fmaf(-e_mu[u], e_pc1[t], pv[u][t]), e_pb[t]);
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 8; t++) x[t] += e_b[t];
+          if (rope_now) {
+#pragma unroll
+            for (int t = 0; t < 8; t++) pv[u][t] += e_pb[t];
+          }
+        }
         if (fl & M3S_EPI_GELU) {
 #pragma unroll
           for (int t = 0; t < 8; t++) x[t] = gelu_erf(x[t]);
@@ -757,7 +869,7 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
         if (rope_now) {
 #pragma unroll
           for (int t = 0; t < 8; t++)
-            x[t] = x[t] * e_x[u][t] + sg * (pv[u][t] + e_pb[t]) * e_x[u][8 + t];
+            x[t] = x[t] * e_x[u][t] + sg * pv[u][t] * e_x[u][8 + t];
         }
         if (has_res) {
 #pragma unroll
@@ -773,6 +885,10 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
           float* cp = reinterpret_cast<float*>(e.C) + off;
           *reinterpret_cast<float4*>(cp) = make_float4(x[0], x[1], x[2], x[3]);
           *reinterpret_cast<float4*>(cp + 4) = make_float4(x[4], x[5], x[6], x[7]);
+          if (fl & M3S_EPI_LN_STATS) {  // the next LayerNorm's input: bf16 copy + row stats
+            store_bf16x8(a.C2 + (int64_t)g * a.sC + off, x);
+            ln_group_stats(a, g, m, en, x);
+          }
         } else if (fl & M3S_EPI_OUT_FP8) {
           *reinterpret_cast<uint2*>(e.C + off) = make_uint2(pack4_fp8(x[0], x[1], x[2], x[3]),
                                                             pack4_fp8(x[4], x[5], x[6], x[7]));
@@ -845,7 +961,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
         p[4] += w1.x; p[5] += w1.y; p[6] += w1.z; p[7] += w1.w;
       }
     }
-    epi_vec8(e, x, p, m, n);
+    epi_vec8(e, x, p, m, n);  // x now holds the stored values
+    if (a.flags & M3S_EPI_LN_STATS) {
+      store_bf16x8(a.C2 + (int64_t)g * a.sC + (int64_t)m * a.ldc + n, x);
+      ln_group_stats(a, g, m, n, x);
+    }
   } else {
     for (int t = 0; t < 8 && n + t < a.N; t++) {
       float s = 0.f, ps = 0.f;
@@ -861,6 +981,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
 // ---------------------------------------------------------------------------------------
 // tile configurations
 // ---------------------------------------------------------------------------------------
+// (4- and 5-stage 128x128 / 6-stage 64x128 rings were measured on the M = 768 shapes at
+// ±3 % of these — tools/gemm_depth.py — and dropped: the first-tile latency, not the ring
+// depth, bounds those blocks)
 enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7, T96 = 8, T96O2 = 9 };
 
 // Epilogue flag sets compiled as straight-line variants (8-wide vector path), per mode:
@@ -882,6 +1005,15 @@ bool try_epi(Args& a, dim3 grid, hipStream_t s, int key) {
     return true;
   }
   return false;
+}
+
+// the same, biased set only (the LayerNorm-fold sets always carry a bias)
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, int E>
+bool try_epi_b(Args& a, dim3 grid, hipStream_t s, int key) {
+  if (key != (E | M3S_EPI_BIAS)) return false;
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, E | M3S_EPI_BIAS>),
+                     grid, dim3(NT), 0, s, a);
+  return true;
 }
 
 // fp8 operands (GEMM mode): the epilogue sets the ViT uses — qkv / q / kv (+RoPE), fc1
@@ -915,6 +1047,20 @@ void launch_main(Args& a, dim3 grid, hipStream_t s) {
               a, grid, s, key))
         return;
       if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_OUT_F32>(a, grid, s, key)) return;
+      // LayerNorm fold (the ViT blocks' norm → projection pairs): consumers qkv / q / kv
+      // (+RoPE) and fc1 (+GELU), producers the residual GEMMs and the embeddings
+      if constexpr (BN == 128 && BK == 64 && (BM == 64 || BM == 128)) {
+        constexpr int LF = M3S_EPI_LN_FOLD, LS = M3S_EPI_LN_STATS;
+        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_ROPE>(a, grid, s, key))
+          return;
+        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_GELU>(a, grid, s, key))
+          return;
+        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE,
+                      LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32>(a, grid, s, key))
+          return;
+        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LS | M3S_EPI_OUT_F32>(a, grid, s, key))
+          return;
+      }
     } else {
       if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0>(a, grid, s, key)) return;
       if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RES_BF16>(a, grid, s, key)) return;
@@ -1059,6 +1205,29 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   a.dpt_conf_min = d->dpt_conf_min;
   a.cscale = d->col_scale;
   a.sCscale = d->stride_col_scale;
+  a.C2 = reinterpret_cast<bf16_t*>(d->C2);
+  a.stats = d->stats;
+  a.a_xor = 0;
+  a.ln_c1 = d->ln_c1;
+  a.ln_eps = d->ln_eps;
+  const bool ln_stats = d->flags & M3S_EPI_LN_STATS, ln_fold = d->flags & M3S_EPI_LN_FOLD;
+  if (ln_stats || ln_fold) {
+    // GEMM mode, bf16 operands, biased, 128-column groups, 16-B aligned row vectors
+    if (d->mode != 0 || f8 || !d->stats || !d->bias || !(d->flags & M3S_EPI_BIAS) ||
+        (d->flags & (M3S_EPI_CONVT | M3S_EPI_OUT_FP8)) || !aligned16(d->stats))
+      return M3S_ERR_INVALID_ARG;
+  }
+  if (ln_stats && (d->N % 128 || !(d->flags & M3S_EPI_OUT_F32) || !d->C2 || !aligned16(d->C2) ||
+                   (d->flags & (M3S_EPI_GELU | M3S_EPI_ROPE | M3S_EPI_RELU))))
+    return M3S_ERR_INVALID_ARG;
+  if (ln_fold) {
+    if (d->K % 128 || d->K / 128 != d->stats_groups || d->stats_groups > 8 || !d->ln_c1 ||
+        !aligned16(d->ln_c1) || d->a_batch_xor < 0 || d->a_batch_xor > 1 ||
+        (d->a_batch_xor && d->batch % 2) || (d->flags & (M3S_EPI_RES_F32 | M3S_EPI_RES_BF16)) ||
+        !(d->ln_eps > 0.f))
+      return M3S_ERR_INVALID_ARG;
+    a.a_xor = d->a_batch_xor;
+  }
   if (f8) {
     a.K = (int)eK;
     a.lda = elda;
@@ -1074,6 +1243,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
           (!d->R || (d->ldr % 8 == 0 && d->strideR % 8 == 0 && aligned16(d->R)));
   (void)out32;
   if ((d->flags & M3S_EPI_ROPE) && !a.vec) return M3S_ERR_INVALID_ARG;
+  if ((ln_stats || ln_fold) && !a.vec) return M3S_ERR_INVALID_ARG;
   if (d->flags & M3S_EPI_DPT_OUT) {
     // compiled only as the conv variant BIAS? | RELU | DPT_OUT on the 8-wide vector path
     const int rest = d->flags & ~(M3S_EPI_DPT_OUT | M3S_EPI_RELU | M3S_EPI_BIAS);
@@ -1103,6 +1273,10 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     if (conv) cfg = tiles128 < 1536 ? T64 : (d->N >= 256 ? T128O2 : T256);
     else if (nk >= 32) cfg = tiles128 >= 1024 ? T128O2 : T128;
     else if (tiles128 < 64 || nk < 8 || (tiles128 > 512 && nk < 16)) cfg = T64;
+    // under one wave of 128^2 tiles with K ≤ 1024 (the encoder's qkv / fc1, the decoder's
+    // N = 768 projections): 64x128 tiles spread the grid over more CUs (graph-replayed
+    // sweep, tools/gemm_depth.py: enc qkv 18.4 → 15.1 us, enc fc1 18.9 → 16.2 us)
+    else if (tiles128 < 256 && nk <= 16) cfg = T64;
     else if (tiles128 >= 256 && tiles128 <= 512 && nk <= 16) cfg = T128O2;
     else cfg = T128;
   }
@@ -1116,7 +1290,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     if (cfg == T128 || cfg == T128O2)
       while (tiles128 * splits * 2 <= 256 && nk / (splits * 2) >= 8) splits *= 2;
   }
-  const bool can_split = !conv && !(d->flags & M3S_EPI_CONVT) && d->workspace &&
+  const bool can_split = !conv && !(d->flags & M3S_EPI_CONVT) && !ln_fold && d->workspace &&
                          (int64_t)splits * d->batch * d->M * d->N * 4 <= d->workspace_bytes;
   if (splits > 1 && can_split) a.splits = splits;
   if (f8) {

@@ -79,12 +79,14 @@ class GemmDesc(ctypes.Structure):
                 ("rope_tokens", ctypes.c_int32), ("weight_mod", ctypes.c_int32),
                 ("dpt_w4", _P), ("dpt_b4", _P), ("dpt_pts", _P), ("dpt_conf", _P),
                 ("dpt_conf_min", ctypes.c_float), ("col_scale", _P),
-                ("stride_col_scale", _I64)]
+                ("stride_col_scale", _I64), ("C2", _P), ("stats", _P),
+                ("stats_groups", ctypes.c_int32), ("a_batch_xor", ctypes.c_int32),
+                ("ln_c1", _P), ("ln_eps", ctypes.c_float)]
 
 
 (EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT,
- EPI_ROPE, EPI_DPT_OUT, IN_FP8, EPI_OUT_FP8) = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024,
-                                                2048)
+ EPI_ROPE, EPI_DPT_OUT, IN_FP8, EPI_OUT_FP8, EPI_LN_STATS, EPI_LN_FOLD) = (
+    1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192)
 
 _lib = None
 

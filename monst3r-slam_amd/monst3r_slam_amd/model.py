@@ -22,6 +22,7 @@ Weights: seeded random (monst3r_slam_amd.weights) — no checkpoints offline.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -71,10 +72,15 @@ class Ops:
 
     def gemm(self, A, B, C, M, N, K, batch=1, *, lda=None, ldb=None, ldc=None, sA=0, sB=0,
              sC=0, bias=None, sBias=0, R=None, ldr=None, sR=0, flags=0, conv=None, convt=None,
-             rope=None, split_k=0, wmod=0, dpt=None, fp8=None, out_fp8=False):
+             rope=None, split_k=0, wmod=0, dpt=None, fp8=None, out_fp8=False, ln_stats=None,
+             ln_fold=None):
         """fp8 = (col_scale f32 [.., N], stride): A and B are OCP e4m3 bytes (torch
         float8_e4m3fn / uint8), the f32 accumulator is scaled per column; out_fp8: C is
-        stored as e4m3."""
+        stored as e4m3.
+        ln_stats = (C2 bf16, stats f32 [batch, M, N/128, 2]): this f32-out GEMM produces a
+        LayerNorm input — also store its bf16 copy and per-128-column (mean, M2).
+        ln_fold = (stats, c1 f32, a_xor): A is the bf16 copy of a LayerNorm input and B a
+        gamma-folded weight; the epilogue applies the normalisation (bias = c2)."""
         d = _lib.GemmDesc()
         d.A, d.lda, d.strideA = _p(A), lda if lda is not None else K, sA
         d.B, d.ldb, d.strideB = _p(B), ldb if ldb is not None else K, sB
@@ -105,6 +111,13 @@ class Ops:
         if rope is not None:  # (cos/sin table, rotated columns, tokens per image)
             d.flags |= _lib.EPI_ROPE
             d.rope_table, d.rope_cols, d.rope_tokens = _p(rope[0]), rope[1], rope[2]
+        if ln_stats is not None:
+            d.flags |= _lib.EPI_LN_STATS
+            d.C2, d.stats = _p(ln_stats[0]), _p(ln_stats[1])
+        if ln_fold is not None:
+            d.flags |= _lib.EPI_LN_FOLD
+            d.stats, d.ln_c1, d.a_batch_xor = _p(ln_fold[0]), _p(ln_fold[1]), ln_fold[2]
+            d.stats_groups, d.ln_eps = K // 128, LN_EPS
         if self.record is not None:  # (descriptor copy, flops, fp8) for the bench replay
             dc = _lib.GemmDesc()
             ctypes.memmove(ctypes.byref(dc), ctypes.byref(d), ctypes.sizeof(d))
@@ -186,6 +199,20 @@ def quant_e4m3(w):
     return q.contiguous(), sc.contiguous()
 
 
+def ln_fold(w, b, g, beta, dev):
+    """LayerNorm → Linear folded for the LN_FOLD epilogue (croco/blocks.py: norm then
+    projection): LN(x) Wᵀ + b = rstd (x (W∘γ)ᵀ − mean c1) + c2 with W' = bf16(W∘γ) (one
+    rounding from the f32 weight), c1 = Σ_k W'[n,k] (of the rounded W', so the mean term
+    cancels what the MFMA accumulates) and c2 = b + W β.  w [.., N, K], b [.., N],
+    g / beta [.., K] (f32).  Returns (W' bf16, c1 f32, c2 f32) on dev."""
+    w = w.to(device=dev, dtype=torch.float64)
+    wf = (w * g.to(device=dev, dtype=torch.float64).unsqueeze(-2)).to(BF16).contiguous()
+    c1 = wf.double().sum(-1).float().contiguous()
+    c2 = (b.to(device=dev, dtype=torch.float64) +
+          (w @ beta.to(device=dev, dtype=torch.float64).unsqueeze(-1)).squeeze(-1))
+    return wf, c1, c2.float().contiguous()
+
+
 # the transformer GEMMs that run on the fp8 MFMA in fp8 mode (SURVEY §8 C5); patch embed,
 # decoder_embed and the DPT/local-feature heads stay bf16
 ENC_FP8 = ("qkv_w", "proj_w", "fc1_w", "fc2_w")
@@ -218,6 +245,12 @@ class PackedWeights:
             ln2_g=f32(st("norm2.weight")), ln2_b=f32(st("norm2.bias")),
             fc1_w=bf(st("mlp.fc1.weight")), fc1_b=f32(st("mlp.fc1.bias")),
             fc2_w=bf(st("mlp.fc2.weight")), fc2_b=f32(st("mlp.fc2.bias")))
+        # LayerNorm-folded copies of the norm → projection pairs (ln_fold): qkv ← norm1,
+        # fc1 ← norm2 → keys <name>_wf / _c1 / _c2
+        for name, lin, nrm in (("qkv", "attn.qkv", "norm1"), ("fc1", "mlp.fc1", "norm2")):
+            wf, c1, c2 = ln_fold(st(lin + ".weight"), st(lin + ".bias"), st(nrm + ".weight"),
+                                 st(nrm + ".bias"), dev)
+            self.enc.update({name + "_wf": wf, name + "_c1": c1, name + "_c2": c2})
         self.enc_norm_g = f32(sdm["enc_norm.weight"])
         self.enc_norm_b = f32(sdm["enc_norm.bias"])
         # ---- decoders, z = model*2 + side ----
@@ -250,6 +283,16 @@ class PackedWeights:
                 ln3_g=f32(dz("norm3.weight", i)), ln3_b=f32(dz("norm3.bias", i)),
                 fc1_w=bf(dz("mlp.fc1.weight", i)), fc1_b=f32(dz("mlp.fc1.bias", i)),
                 fc2_w=bf(dz("mlp.fc2.weight", i)), fc2_b=f32(dz("mlp.fc2.bias", i))))
+            # LayerNorm-folded copies: qkv ← norm1, kv ← norm_y (of the other side's x),
+            # q ← norm2, fc1 ← norm3
+            P = self.dec[-1]
+            for name, w, b, nrm in (
+                    ("qkv", dz("attn.qkv.weight", i), dz("attn.qkv.bias", i), "norm1"),
+                    ("kv", kv_w, kv_b, "norm_y"),
+                    ("q", dz("cross_attn.projq.weight", i), dz("cross_attn.projq.bias", i), "norm2"),
+                    ("fc1", dz("mlp.fc1.weight", i), dz("mlp.fc1.bias", i), "norm3")):
+                wf, c1, c2 = ln_fold(w, b, dz(nrm + ".weight", i), dz(nrm + ".bias", i), dev)
+                P.update({name + "_wf": wf, name + "_c1": c1, name + "_c2": c2})
         self.dec_norm_g = f32(dz("dec_norm.weight"))
         self.dec_norm_b = f32(dz("dec_norm.bias"))
         # ---- DPT heads, z = model*2 + side ----
@@ -324,6 +367,9 @@ class PairModel:
         self.side = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
         self.serial = True
         self.fp8 = False
+        # bf16 path: the blocks' LayerNorms folded into the following projections (ln_fold;
+        # LN_STATS / LN_FOLD epilogues) instead of separate LayerNorm launches
+        self.lnfold = os.environ.get("M3S_LNFOLD", "1") != "0"
         self._tag = None      # buffer-key prefix of the head set being issued (split heads)
         self._wbase = 0       # first head-weight stack of that set
         self._wm = 4
@@ -410,8 +456,15 @@ class PairModel:
         patches = self._buf("enc_patch", (M, 3 * a.patch * a.patch), BF16)
         o.patchify(img, patches, B, H, Wd)
         x = self._buf("enc_x", (M, E), F32)
+        fold = self.lnfold and not self.fp8 and E % 128 == 0
+        if fold:
+            # LayerNorm folded into the projections (ln_fold): every residual-stream
+            # producer also writes x in bf16 + row statistics; no LayerNorm launches
+            xb = self._buf("enc_xb", (M, E), BF16)
+            st = self._buf("enc_stats", (M, E // 128, 2), F32)
+            R32S = dict(flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, ln_stats=(xb, st))
         o.gemm(patches, W.patch_w, x, M, E, 3 * a.patch * a.patch, bias=W.patch_b,
-               flags=_lib.EPI_OUT_F32)
+               flags=_lib.EPI_OUT_F32, ln_stats=(xb, st) if fold else None)
         adt = U8 if self.fp8 else BF16   # GEMM A operands: e4m3 bytes in fp8 mode
         xn = self._buf("enc_xn", (M, E), adt)
         qkv = self._buf("enc_qkv", (M, 3 * E), BF16)
@@ -420,7 +473,18 @@ class PairModel:
         pos = self.positions(B, gh, gw)
         rt = self.rope_tab(gh, gw)
         P, P8 = W.enc, W.enc8
-        for i in range(a.enc_depth):
+        if fold:
+            for i in range(a.enc_depth):
+                o.gemm(xb, P["qkv_wf"][i], qkv, M, 3 * E, E, bias=P["qkv_c2"][i],
+                       rope=(rt, 2 * E, S), ln_fold=(st, P["qkv_c1"][i], 0))
+                o.attn(qkv, 3 * E, S * 3 * E, qkv[:, E:], qkv[:, 2 * E:], 3 * E, S * 3 * E, att,
+                       E, S * E, B, a.enc_heads, S, S)
+                o.gemm(att, P["proj_w"][i], x, M, E, E, bias=P["proj_b"][i], R=x, **R32S)
+                o.gemm(xb, P["fc1_wf"][i], hid, M, a.mlp_ratio * E, E, bias=P["fc1_c2"][i],
+                       flags=_lib.EPI_GELU, ln_fold=(st, P["fc1_c1"][i], 0))
+                o.gemm(hid, P["fc2_w"][i], x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][i], R=x,
+                       **R32S)
+        for i in range(a.enc_depth if not fold else 0):
             o.ln(x, P["ln1_g"][i], P["ln1_b"][i], xn, M, E)
             # qkv projection with RoPE2D on q and k fused into the epilogue
             w, kw = self._wt(P, P8, "qkv_w", i)
@@ -465,8 +529,15 @@ class PairModel:
         hv[:, :, 0].copy_(feat1.reshape(G, 1, S, E).expand(G, models, S, E))
         hv[:, :, 1].copy_(feat2.reshape(G, 1, S, E).expand(G, models, S, E))
         x = self._buf("dec_x", (Z, S, D), F32)
+        fold = self.lnfold and not self.fp8 and self.serial and D % 128 == 0
+        if fold:
+            xb = self._buf("dec_xb", (Z, S, D), BF16)
+            st = self._buf("dec_stats", (Z, S, D // 128, 2), F32)
         o.gemm(h0, W.dec_embed_w, x, S, D, E, Z, sA=S * E, sB=D * E, sC=S * D,
-               bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32, wmod=wm)
+               bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32, wmod=wm,
+               ln_stats=(xb, st) if fold else None)
+        if fold:
+            return self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm)
         adt = U8 if self.fp8 else BF16
         xn = self._buf("dec_xn", (Z, S, D), adt)
         yn = self._buf("dec_yn", (Z, S, D), adt)
@@ -537,6 +608,61 @@ class PairModel:
                 hb = self._buf(f"h{i + 1}", (Z, S, D), BF16)
                 hb.copy_(x)
                 hooks[f"h{i + 1}"] = hb
+        h12 = self._buf("h12", (Z, S, D), BF16)
+        o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
+        hooks["h12"] = h12
+        return hooks
+
+    def _decode_folded(self, x, xb, st, h0, Z, S, E, D, gh, gw, wm):
+        """decode_multi's blocks (croco/blocks.py:172-195 DecoderBlock) with every LayerNorm
+        folded into the projection that consumes it (ln_fold): the residual GEMMs write x
+        (f32), its bf16 copy and row statistics; qkv (norm1), kv (norm_y of the other side:
+        A / stats of problem z ^ 1), q (norm2) and fc1 (norm3) normalise in the epilogue.
+        The hook layers' bf16 copies are written straight into the hook buffers."""
+        o, a, W = self.ops, self.a, self.w
+        qkv = self._buf("dec_qkv", (Z, S, 3 * D), BF16)
+        kv = self._buf("dec_kv", (Z, S, 2 * D), BF16)
+        q = self._buf("dec_q", (Z, S, D), BF16)
+        att = self._buf("dec_att", (Z, S, D), BF16)
+        hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), BF16)
+        hooks = {"h0": h0}
+        rt = self.rope_tab(gh, gw)
+        hk = set(a.hooks[1:3])
+        Dm = a.mlp_ratio * D
+        xc = xb                                  # the current bf16 copy of x
+        zs = dict(sA=S * D, sC=S * D, wmod=wm)   # the per-problem strides of a [Z,S,D] A
+        for i in range(a.dec_depth):
+            P = W.dec[i]
+            R32S = dict(R=x, sR=S * D, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32,
+                        ln_stats=(xb, st))
+            # cross-attention k/v from norm_y(other side's x): issued first (reads x of
+            # the layer's start, as the reference's y_ = norm_y(y) before x changes)
+            o.gemm(xc, P["kv_wf"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D, sC=S * 2 * D,
+                   bias=P["kv_c2"], sBias=2 * D, rope=(rt, D, S), wmod=wm,
+                   ln_fold=(st, P["kv_c1"], 1))
+            o.gemm(xc, P["qkv_wf"], qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
+                   bias=P["qkv_c2"], sBias=3 * D, rope=(rt, 2 * D, S), wmod=wm,
+                   ln_fold=(st, P["qkv_c1"], 0))
+            o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,
+                   D, S * D, Z, a.dec_heads, S, S)
+            o.gemm(att, P["proj_w"], x, S, D, D, Z, sB=D * D, bias=P["proj_b"], sBias=D, **zs,
+                   **R32S)
+            o.gemm(xb, P["q_wf"], q, S, D, D, Z, sB=D * D, bias=P["q_c2"], sBias=D,
+                   rope=(rt, D, S), ln_fold=(st, P["q_c1"], 0), **zs)
+            o.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, att, D, S * D, Z, a.dec_heads,
+                   S, S)
+            o.gemm(att, P["cproj_w"], x, S, D, D, Z, sB=D * D, bias=P["cproj_b"], sBias=D, **zs,
+                   **R32S)
+            o.gemm(xb, P["fc1_wf"], hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm,
+                   bias=P["fc1_c2"], sBias=Dm, flags=_lib.EPI_GELU, wmod=wm,
+                   ln_fold=(st, P["fc1_c1"], 0))
+            xc = xb
+            if (i + 1) in hk:
+                xc = self._buf(f"h{i + 1}", (Z, S, D), BF16)
+                hooks[f"h{i + 1}"] = xc
+            o.gemm(hid, P["fc2_w"], x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D,
+                   bias=P["fc2_b"], sBias=D, wmod=wm,
+                   **dict(R32S, ln_stats=(xc, st)))
         h12 = self._buf("h12", (Z, S, D), BF16)
         o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
         hooks["h12"] = h12

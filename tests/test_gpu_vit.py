@@ -453,3 +453,83 @@ def test_split_heads_match_batched(dev):
     for k in ("C", "mast3r_C"):
         assert _rel(b[k], a[k]) < 1e-2, k
     assert torch.equal(b["D16"], a["D16"]) and torch.equal(b["Q"], a["Q"])
+
+
+def _ln_stats_ref(x):
+    """(mean, M2) per 128-column group of the rows of x [.., M, N]."""
+    g = x.float().reshape(*x.shape[:-1], x.shape[-1] // 128, 128)
+    mean = g.mean(-1)
+    return torch.stack([mean, ((g - mean[..., None]) ** 2).sum(-1)], -1)
+
+
+@pytest.mark.parametrize("M,N,K,batch,split_k", [(768, 768, 3072, 4, 1), (768, 1024, 1024, 1, 2),
+                                                 (768, 1024, 4096, 1, 0), (200, 256, 96, 2, 1)])
+def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k):
+    """LN_STATS: the residual GEMM also stores bf16(x) and per-128-column (mean, M2) of the
+    stored f32 rows — in the main epilogue and in the split-K reduce (split_k 2 / auto)."""
+    from monst3r_slam_amd import _lib
+    g = torch.Generator(device=dev).manual_seed(11)
+    A = torch.randn(batch, M, K, device=dev, generator=g).bfloat16()
+    B = (torch.randn(batch, N, K, device=dev, generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(batch, N, device=dev, generator=g)
+    x = torch.randn(batch, M, N, device=dev, generator=g) + 3.0
+    ref = x + torch.bmm(A.float(), B.float().transpose(1, 2)) + bias[:, None]
+    xb = torch.empty(batch, M, N, device=dev, dtype=torch.bfloat16)
+    st = torch.full((batch, M, N // 128, 2), float("nan"), device=dev)
+    ops.gemm(A, B, x, M, N, K, batch, sA=M * K, sB=N * K, sC=M * N, bias=bias, sBias=N, R=x,
+             sR=M * N, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, ln_stats=(xb, st),
+             split_k=split_k)
+    assert _rel(x, ref) < 1e-3
+    assert torch.equal(xb, x.bfloat16())                      # the bf16 copy of what x holds
+    sr = _ln_stats_ref(x)
+    assert float((st[..., 0] - sr[..., 0]).abs().max()) < 1e-5 * float(x.abs().max())
+    assert float(((st[..., 1] - sr[..., 1]).abs() / sr[..., 1]).max()) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K,batch,axor,epi", [(768, 2304, 768, 4, 0, "rope"),
+                                                  (768, 1536, 768, 4, 1, "rope"),
+                                                  (768, 3072, 768, 4, 0, "gelu"),
+                                                  (768, 4096, 1024, 1, 0, "gelu"),
+                                                  (200, 384, 256, 2, 1, "none")])
+def test_gemm_ln_fold_consumer(ops, dev, M, N, K, batch, axor, epi):
+    """LN_FOLD: LN(x) Wᵀ + b computed as rstd (bf16(x) (W∘γ)ᵀ − mean c1) + c2 from the
+    producer's statistics, vs torch fp32 LayerNorm → Linear (→ RoPE / GELU) on x of
+    problem g ^ axor; x carries a mean offset (the cancellation the fold must survive).
+    Tolerance 1e-2 of the output scale (bf16 operands, as the unfolded GEMM tests)."""
+    from monst3r_slam_amd import _lib
+    from monst3r_slam_amd.model import ln_fold, LN_EPS
+    from oracle import vit_ref as V
+    g = torch.Generator(device=dev).manual_seed(12)
+    x = torch.randn(batch, M, K, device=dev, generator=g) * 1.5 + 0.7
+    gam = 1.0 + 0.3 * torch.randn(batch, K, device=dev, generator=g)
+    bet = 0.2 * torch.randn(batch, K, device=dev, generator=g)
+    W = torch.randn(batch, N, K, device=dev, generator=g) / K ** 0.5
+    b = torch.randn(batch, N, device=dev, generator=g)
+    wf, c1, c2 = ln_fold(W, b, gam, bet, dev)
+    xb = x.bfloat16()  # what the producer's LN_STATS epilogue stores (checked above)
+    st = _ln_stats_ref(x).contiguous()
+    out = torch.empty(batch, M, N, device=dev, dtype=torch.bfloat16)
+    kw = {}
+    flags = 0
+    S = M
+    if epi == "rope":
+        gh, gw = 24, 32
+        assert gh * gw == M
+        pos = V.positions(1, gh, gw, dev)[0].contiguous()
+        kw["rope"] = (ops.rope_table(pos, 100.0), N // 2 if axor else 2 * N // 3, S)
+    elif epi == "gelu":
+        flags = _lib.EPI_GELU
+    ops.gemm(xb, wf, out, M, N, K, batch, sA=M * K, sB=N * K, sC=M * N, bias=c2, sBias=N,
+             flags=flags, ln_fold=(st, c1, axor), **kw)
+    src = x[torch.arange(batch, device=dev) ^ axor]
+    ln = F.layer_norm(src, (K,), eps=LN_EPS) * gam[:, None] + bet[:, None]
+    ref = torch.bmm(ln, W.transpose(1, 2)) + b[:, None]
+    if epi == "gelu":
+        ref = F.gelu(ref)
+    elif epi == "rope":
+        rc = kw["rope"][1]
+        posb = V.positions(batch, 24, 32, dev)
+        r = ref[..., :rc].reshape(batch, S, rc // 64, 64)
+        r = V.rope2d(r.transpose(1, 2), posb, 100.0).transpose(1, 2)
+        ref = torch.cat([r.reshape(batch, S, rc), ref[..., rc:]], -1)
+    assert _rel(out, ref) < 1e-2

@@ -33,9 +33,11 @@ def gemm(A, B, C, M, N, K, b, tile, split, flags=0, R=None):
     assert st == 0, st
 
 
-shapes = [("enc proj", 768, 1024, 1024, 1, 2, 1), ("enc fc1", 768, 4096, 1024, 1, 2, 1),
-          ("dec fc2", 768, 768, 3072, 4, 1, 1), ("dec fc1", 768, 3072, 768, 4, 2, 1),
-          ("big", 4096, 4096, 4096, 1, 1, 1), ("big T256", 4096, 4096, 4096, 1, 6, 1)]
+shapes = [("enc fc1", 768, 4096, 1024, 1, 1, 1), ("enc fc1 S4", 768, 4096, 1024, 1, 10, 1),
+          ("enc fc1 S5", 768, 4096, 1024, 1, 11, 1),
+          ("dec fc2", 768, 768, 3072, 4, 1, 1), ("dec fc2 S5", 768, 768, 3072, 4, 11, 1),
+          ("dec fc1", 768, 3072, 768, 4, 1, 1), ("dec fc1 S5", 768, 3072, 768, 4, 11, 1),
+          ("big", 4096, 4096, 4096, 1, 1, 1), ("big S5", 4096, 4096, 4096, 1, 11, 1)]
 for name, M, N, K, b, tile, split in shapes:
     A = torch.randn(b, M, K, device=dev).bfloat16()
     B = torch.randn(b, N, K, device=dev).bfloat16()
