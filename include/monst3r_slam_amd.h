@@ -281,13 +281,15 @@ int m3s_vit_rope(void* d_t, int64_t ld, int64_t stride, const int64_t* d_pos,
  * The pos/rope arguments are reserved (must be NULL/0).  With a device workspace (16-B
  * aligned, optional) a small (query tile x head x batch) grid is split along the keys
  * (flash-decoding): per-split unnormalised O, max and sum in f32, merged by a second
- * kernel; up to splits x B x heads x sq x 68 floats of workspace are used. */
+ * kernel; up to splits x B x heads x sq x 68 floats of workspace are used.
+ * kv_batch_xor = 1 (B even): batch b attends to the k / v rows of batch b ^ 1 (the
+ * decoder's cross-attention reading the other side's k / v from a fused projection). */
 int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q, const void* d_k,
                       const void* d_v, int64_t ld_kv, int64_t stride_kv, const int64_t* d_qpos,
                       const int64_t* d_kpos, int64_t stride_pos, void* d_o, int64_t ld_o,
                       int64_t stride_o, int o_fp8, int64_t batch, int64_t heads, int64_t sq,
                       int64_t sk, float rope_base, void* d_workspace, int64_t workspace_bytes,
-                      void* stream);
+                      int kv_batch_xor, void* stream);
 
 /* Patch-embed im2col: img f32 NCHW [B][3][H][W] → bf16 [B][(H/16)(W/16)][3*16*16]
  * with K ordered (c, ky, kx) like the conv weight [1024][3][16][16]. */

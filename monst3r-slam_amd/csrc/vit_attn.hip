@@ -132,7 +132,7 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, void* __restrict__ o,
     int64_t ldo, int64_t so_b, int o_fp8, int Sq, int Sk, int heads, float c_log2, int splits,
-    int tiles_per_split, float* __restrict__ part) {
+    int tiles_per_split, float* __restrict__ part, int kv_xor) {
   constexpr int GT = AW * 64;                        // threads of one key-split group
   constexpr int ACH = TILE_BYTES / 16 / GT;          // DMA chunks per thread per operand
   constexpr int NST = KS == 1 ? ASTAGES : 2;         // ring depth per key split
@@ -180,9 +180,9 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
   for (int ks = 0; ks < 4; ks++) asm volatile("" : "+v"(qf[ks]));
 
   const __amdgpu_buffer_rsrc_t rK = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(k + b * skv_b + h * HD), (short)0, 0x7ffffff0, 0x00020000);
+      const_cast<bf16_t*>(k + (b ^ kv_xor) * skv_b + h * HD), (short)0, 0x7ffffff0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rV = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(v + b * skv_b + h * HD), (short)0, 0x7ffffff0, 0x00020000);
+      const_cast<bf16_t*>(v + (b ^ kv_xor) * skv_b + h * HD), (short)0, 0x7ffffff0, 0x00020000);
   // DMA chunk c = i*256 + tid → tile row c / 8, slot c % 8
   int k_row[ACH];
   uint32_t k_off[ACH], v_off[ACH];
@@ -477,9 +477,11 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
                                  void* d_o, int64_t ld_o, int64_t stride_o, int o_fp8,
                                  int64_t batch, int64_t heads, int64_t sq, int64_t sk,
                                  float rope_base,
-                                 void* d_workspace, int64_t workspace_bytes, void* stream) {
+                                 void* d_workspace, int64_t workspace_bytes, int kv_batch_xor,
+                                 void* stream) {
   if (!d_q || !d_k || !d_v || !d_o || batch <= 0 || heads <= 0 || sq <= 0 || sk <= 0)
     return M3S_ERR_INVALID_ARG;
+  if (kv_batch_xor < 0 || kv_batch_xor > 1 || (kv_batch_xor && batch % 2)) return M3S_ERR_INVALID_ARG;
   if ((((uintptr_t)d_q) | ((uintptr_t)d_k) | ((uintptr_t)d_v)) % 16) return M3S_ERR_INVALID_ARG;
   if (ld_q % 8 || ld_kv % 8 || stride_q % 8 || stride_kv % 8) return M3S_ERR_INVALID_ARG;
   if (batch > 65535 || heads > 65535) return M3S_ERR_TOO_LARGE;
@@ -527,7 +529,7 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
                      reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,                   \
                      reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
                      ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,          \
-                     (int)sk, (int)heads, c_log2, splits, tps, part)
+                     (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor)
   if (ks == 4) M3S_ATTN_LAUNCH(2, 4);
   else if (ks == 2 && aw == 2) M3S_ATTN_LAUNCH(2, 2);
   else if (ks == 2) M3S_ATTN_LAUNCH(4, 2);

@@ -649,7 +649,9 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
   // Vector path: a thread owns columns [n, n+8) of rows r0 + v*RSTEP.  Its bias and, per
   // group of EG vectors, the residual (or RoPE cos/sin) operands are loaded ahead of use —
   // the first group before the LDS round trip — so their latency is overlapped.
-  constexpr int EG = NV < 4 ? NV : 4;
+  // EG must divide NV (96-row tiles have NV = 6: groups of 4 would run past the tile into
+  // the next tile's rows)
+  constexpr int EG = NV % 4 == 0 ? 4 : NV % 3 == 0 ? 3 : NV % 2 == 0 ? 2 : 1;
   const int ec = (tid % VPR) * 8, er0 = tid / VPR;
   const int en = n0 + ec;
   const int fl = EPI >= 0 ? EPI : a.flags;
@@ -1049,7 +1051,8 @@ void launch_main(Args& a, dim3 grid, hipStream_t s) {
       if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_OUT_F32>(a, grid, s, key)) return;
       // LayerNorm fold (the ViT blocks' norm → projection pairs): consumers qkv / q / kv
       // (+RoPE) and fc1 (+GELU), producers the residual GEMMs and the embeddings
-      if constexpr (BN == 128 && BK == 64 && (BM == 64 || BM == 128)) {
+      if constexpr (BN == 128 && BK == 64 && (BM == 64 || BM == 96 || BM == 128) && OCC <= 2 &&
+                    (BM != 96 || OCC == 1)) {
         constexpr int LF = M3S_EPI_LN_FOLD, LS = M3S_EPI_LN_STATS;
         if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_ROPE>(a, grid, s, key))
           return;
@@ -1099,8 +1102,20 @@ int launch(Args& a, int batch, hipStream_t s) {
     a.nmajor = 0;
   }
   if (split) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true, -1, F8>), grid,
-                       dim3(NT), 0, s, a);
+    // split implicit convs: the 64x128 config only (the small DPT levels, host-chosen)
+    constexpr bool CONV_SPLIT = BM == 64 && BN == 128 && STAGES == 3 && OCC == 2 && !F8;
+    if (a.mode != 0 && !CONV_SPLIT) return M3S_ERR_INVALID_ARG;
+    if constexpr (CONV_SPLIT) {
+      if (a.mode != 0 && (a.flags & M3S_PRO_RELU))
+        hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 2, true, -1, F8>), grid,
+                           dim3(NT), 0, s, a);
+      else if (a.mode != 0)
+        hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 1, true, -1, F8>), grid,
+                           dim3(NT), 0, s, a);
+    }
+    if (a.mode == 0)
+      hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true, -1, F8>), grid,
+                         dim3(NT), 0, s, a);
     M3S_LAUNCH_CHECK();
     const int64_t nv = (int64_t)a.M * ((a.N + 7) / 8);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(m3s_div_up(nv, 256), (unsigned)batch),
@@ -1270,7 +1285,9 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     // measured on the pair shapes (tools/gemm_tune.py): 2 x 128^2 blocks per CU win for
     // wide convs with several waves of tiles, for one-to-two waves of short-K GEMM tiles,
     // and for large square-ish GEMMs
-    if (conv) cfg = tiles128 < 1536 ? T64 : (d->N >= 256 ? T128O2 : T256);
+    // (2 x 128^2 per CU beat 256x128 on the 128-channel head convs too: head.2 + DPT tail
+    // 348 → 311 us, tools/gemm_depth.py conv sweep)
+    if (conv) cfg = tiles128 < 1536 ? T64 : T128O2;
     else if (nk >= 32) cfg = tiles128 >= 1024 ? T128O2 : T128;
     else if (tiles128 < 64 || nk < 8 || (tiles128 > 512 && nk < 16)) cfg = T64;
     // under one wave of 128^2 tiles with K ≤ 1024 (the encoder's qkv / fc1, the decoder's
@@ -1279,6 +1296,16 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     else if (tiles128 < 256 && nk <= 16) cfg = T64;
     else if (tiles128 >= 256 && tiles128 <= 512 && nk <= 16) cfg = T128O2;
     else cfg = T128;
+    // 96-row tiles (768 = 8 bands) whose grid is one well-filled round of 256 CUs or whole
+    // rounds: faster launch by launch (graph-replayed sweep, tools/gemm_depth.py: enc qkv
+    // 12.3 → 11.1 us, dec fc1 30.1 → 27.4, dec fc2 25.8 → 23.5) but, filling every CU
+    // with one 86-KB-LDS block, they leave no room for the concurrently prefetched encoder:
+    // the tracking pipeline measured 182 vs 184.6 frames/s (2 x 200 steps, A/B).  Opt-in.
+    const int64_t tiles96 = (int64_t)((d->M + 95) / 96) * ((d->N + 127) / 128) * d->batch;
+    static const bool use96 = getenv("M3S_T96") != nullptr;
+    if (!conv && use96 && d->M % 96 == 0 && nk >= 8 &&
+        ((tiles96 >= 160 && tiles96 <= 256) || tiles96 % 256 == 0))
+      cfg = T96;
   }
   if (cfg < 1 || cfg > 9 || cfg == 4 || cfg == 5) cfg = T128;
   if (conv && d->Cin % 64 != 0) cfg = T128K32;  // tap-uniform K-tiles need Cin % BK == 0
@@ -1287,10 +1314,17 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   int splits = d->split_k;
   if (splits <= 0) {
     splits = 1;
-    if (cfg == T128 || cfg == T128O2)
+    if (!conv && (cfg == T128 || cfg == T128O2))
       while (tiles128 * splits * 2 <= 256 && nk / (splits * 2) >= 8) splits *= 2;
+    // the small DPT levels (24x32, 12x16 convs: 24-96 tiles of 64x128 with K = 2304-6912)
+    // split K while the grid stays within one round of 2 blocks per CU
+    if (conv && cfg == T64 && !(d->flags & M3S_EPI_DPT_OUT)) {
+      const int64_t tiles64 = (int64_t)((d->M + 63) / 64) * ((d->N + 127) / 128) * d->batch;
+      while (tiles64 * splits * 2 <= 512 && nk / (splits * 2) >= 8) splits *= 2;
+    }
   }
-  const bool can_split = !conv && !(d->flags & M3S_EPI_CONVT) && !ln_fold && d->workspace &&
+  const bool can_split = (!conv || (cfg == T64 && !(d->flags & M3S_EPI_DPT_OUT))) &&
+                         !(d->flags & M3S_EPI_CONVT) && !ln_fold && d->workspace &&
                          (int64_t)splits * d->batch * d->M * d->N * 4 <= d->workspace_bytes;
   if (splits > 1 && can_split) a.splits = splits;
   if (f8) {

@@ -50,7 +50,7 @@ SIGNATURES = {
                                     _I64, _I64, _P]),
     "m3s_vit_rope": (_I, [_P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _F, _P]),
     "m3s_vit_attention": (_I, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _I64, _I64,
-                               _I, _I64, _I64, _I64, _I64, _F, _P, _I64, _P]),
+                               _I, _I64, _I64, _I64, _I64, _F, _P, _I64, _I, _P]),
     "m3s_vit_rope_table": (_I, [_P, _I64, _F, _P, _P]),
     "m3s_vit_patchify": (_I, [_P, _P, _I64, _I64, _I64, _P]),
     "m3s_vit_upsample2x": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),

@@ -152,12 +152,14 @@ class Ops:
                                                self._s()), "vit_rope_table")
         return tab
 
-    def attn(self, q, ldq, sq_b, k, v, ldkv, skv_b, o, ldo, so_b, batch, heads, sq, sk):
+    def attn(self, q, ldq, sq_b, k, v, ldkv, skv_b, o, ldo, so_b, batch, heads, sq, sk,
+             kv_xor=0):
+        """kv_xor = 1: batch b reads k / v of batch b ^ 1."""
         ws = self.ws
         _lib.check(self.lib.m3s_vit_attention(_p(q), ldq, sq_b, _p(k), _p(v), ldkv, skv_b, None,
                                               None, 0, _p(o), ldo, so_b,
                                               int(o.element_size() == 1), batch, heads, sq, sk, 0.0,
-                                              _p(ws), ws.numel(), self._s()),
+                                              _p(ws), ws.numel(), kv_xor, self._s()),
                    "vit_attention")
 
     def patchify(self, img, out, b, h, w):
@@ -293,6 +295,17 @@ class PackedWeights:
                     ("fc1", dz("mlp.fc1.weight", i), dz("mlp.fc1.bias", i), "norm3")):
                 wf, c1, c2 = ln_fold(w, b, dz(nrm + ".weight", i), dz(nrm + ".bias", i), dev)
                 P.update({name + "_wf": wf, name + "_c1": c1, name + "_c2": c2})
+            # self-attention qkv of problem z and the cross-attention k/v that problem z ^ 1
+            # takes from z's tokens (norm_y params / weights of z ^ 1) read the same A rows:
+            # one GEMM, output columns [q | k | k' | v | v'] (RoPE on the first 3 blocks)
+            D = am.dec_dim
+            sw = [1, 0, 3, 2]
+
+            def fuse(a, b):
+                b = b[sw]
+                return torch.cat([a[:, :2 * D], b[:, :D], a[:, 2 * D:], b[:, D:]], 1).contiguous()
+            for suf in ("_wf", "_c1", "_c2"):
+                P["qkvkv" + suf] = fuse(P.pop("qkv" + suf), P.pop("kv" + suf))
         self.dec_norm_g = f32(dz("dec_norm.weight"))
         self.dec_norm_b = f32(dz("dec_norm.bias"))
         # ---- DPT heads, z = model*2 + side ----
@@ -616,12 +629,14 @@ class PairModel:
     def _decode_folded(self, x, xb, st, h0, Z, S, E, D, gh, gw, wm):
         """decode_multi's blocks (croco/blocks.py:172-195 DecoderBlock) with every LayerNorm
         folded into the projection that consumes it (ln_fold): the residual GEMMs write x
-        (f32), its bf16 copy and row statistics; qkv (norm1), kv (norm_y of the other side:
-        A / stats of problem z ^ 1), q (norm2) and fc1 (norm3) normalise in the epilogue.
+        (f32), its bf16 copy and row statistics; qkv (norm1), the cross-attention k/v
+        (norm_y of the other side), q (norm2) and fc1 (norm3) normalise in the epilogue.
+        qkv of problem z and the k/v that problem z ^ 1 attends to are one GEMM over z's
+        rows (PackedWeights "qkvkv"); the cross-attention reads them with kv_xor = 1.
         The hook layers' bf16 copies are written straight into the hook buffers."""
         o, a, W = self.ops, self.a, self.w
-        qkv = self._buf("dec_qkv", (Z, S, 3 * D), BF16)
-        kv = self._buf("dec_kv", (Z, S, 2 * D), BF16)
+        F5 = 5 * D                               # fused [q | k | k' | v | v'] columns
+        qkv = self._buf("dec_qkvkv", (Z, S, F5), BF16)
         q = self._buf("dec_q", (Z, S, D), BF16)
         att = self._buf("dec_att", (Z, S, D), BF16)
         hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), BF16)
@@ -635,22 +650,20 @@ class PairModel:
             P = W.dec[i]
             R32S = dict(R=x, sR=S * D, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32,
                         ln_stats=(xb, st))
-            # cross-attention k/v from norm_y(other side's x): issued first (reads x of
-            # the layer's start, as the reference's y_ = norm_y(y) before x changes)
-            o.gemm(xc, P["kv_wf"], kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D, sC=S * 2 * D,
-                   bias=P["kv_c2"], sBias=2 * D, rope=(rt, D, S), wmod=wm,
-                   ln_fold=(st, P["kv_c1"], 1))
-            o.gemm(xc, P["qkv_wf"], qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
-                   bias=P["qkv_c2"], sBias=3 * D, rope=(rt, 2 * D, S), wmod=wm,
-                   ln_fold=(st, P["qkv_c1"], 0))
-            o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,
+            # norm1 → qkv of problem z and norm_y → cross k/v of problem z ^ 1, one GEMM over
+            # x of the layer's start (the reference's y_ = norm_y(y) before x changes)
+            o.gemm(xc, P["qkvkv_wf"], qkv, S, F5, D, Z, sA=S * D, sB=F5 * D, sC=S * F5,
+                   bias=P["qkvkv_c2"], sBias=F5, rope=(rt, 3 * D, S), wmod=wm,
+                   ln_fold=(st, P["qkvkv_c1"], 0))
+            o.attn(qkv, F5, S * F5, qkv[:, :, D:], qkv[:, :, 3 * D:], F5, S * F5, att,
                    D, S * D, Z, a.dec_heads, S, S)
             o.gemm(att, P["proj_w"], x, S, D, D, Z, sB=D * D, bias=P["proj_b"], sBias=D, **zs,
                    **R32S)
             o.gemm(xb, P["q_wf"], q, S, D, D, Z, sB=D * D, bias=P["q_c2"], sBias=D,
                    rope=(rt, D, S), ln_fold=(st, P["q_c1"], 0), **zs)
-            o.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, att, D, S * D, Z, a.dec_heads,
-                   S, S)
+            # k' / v' of problem z were computed in problem z ^ 1's rows
+            o.attn(q, D, S * D, qkv[:, :, 2 * D:], qkv[:, :, 4 * D:], F5, S * F5, att, D, S * D,
+                   Z, a.dec_heads, S, S, kv_xor=1)
             o.gemm(att, P["cproj_w"], x, S, D, D, Z, sB=D * D, bias=P["cproj_b"], sBias=D, **zs,
                    **R32S)
             o.gemm(xb, P["fc1_wf"], hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm,

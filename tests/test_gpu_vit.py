@@ -533,3 +533,47 @@ def test_gemm_ln_fold_consumer(ops, dev, M, N, K, batch, axor, epi):
         r = V.rope2d(r.transpose(1, 2), posb, 100.0).transpose(1, 2)
         ref = torch.cat([r.reshape(batch, S, rc), ref[..., rc:]], -1)
     assert _rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9])
+@pytest.mark.parametrize("epi", ["gelu", "res"])
+def test_gemm_every_tile_config(ops, dev, monkeypatch, tile, epi):
+    """Every tile configuration (M3S_GEMM_TILE override) on a 768-row problem, straight-
+    line epilogues: 96-row tiles once ran their vector epilogue past the tile (rows of the
+    next tile overwritten) — the tile sweep caught it, this pins it."""
+    from monst3r_slam_amd import _lib
+    monkeypatch.setenv("M3S_GEMM_TILE", str(tile))
+    M, N, K, b = 768, 768, 512, 2
+    g = torch.Generator(device=dev).manual_seed(21 + tile)
+    A = torch.randn(b, M, K, device=dev, generator=g).bfloat16()
+    B = (torch.randn(b, N, K, device=dev, generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(b, N, device=dev, generator=g)
+    ref = torch.bmm(A.float(), B.float().transpose(1, 2)) + bias[:, None]
+    if epi == "gelu":
+        C = torch.empty(b, M, N, device=dev, dtype=torch.bfloat16)
+        ops.gemm(A, B, C, M, N, K, b, sA=M * K, sB=N * K, sC=M * N, bias=bias, sBias=N,
+                 flags=_lib.EPI_GELU, split_k=1)
+        assert _rel(C, F.gelu(ref)) < 1e-2
+    else:
+        R = torch.randn(b, M, N, device=dev, generator=g)
+        C = torch.empty(b, M, N, device=dev)
+        ops.gemm(A, B, C, M, N, K, b, sA=M * K, sB=N * K, sC=M * N, bias=bias, sBias=N, R=R,
+                 sR=M * N, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, split_k=1)
+        assert _rel(C, ref + R) < 1e-3
+
+
+def test_cross_attention_kv_batch_xor(ops, dev):
+    """kv_xor = 1: problem b attends to the k / v rows of problem b ^ 1 (the decoder's fused
+    qkv + cross-k/v projection) — same result as swapping the k / v batches by hand."""
+    g = torch.Generator(device=dev).manual_seed(31)
+    B, S, heads = 4, 768, 12
+    D = heads * 64
+    q = torch.randn(B, S, D, device=dev, generator=g).bfloat16()
+    kv = torch.randn(B, S, 2 * D, device=dev, generator=g).bfloat16()
+    o = torch.empty(B, S, D, device=dev, dtype=torch.bfloat16)
+    ops.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, o, D, S * D, B, heads, S, S,
+             kv_xor=1)
+    kvs = kv[[1, 0, 3, 2]].contiguous()
+    o2 = torch.empty_like(o)
+    ops.attn(q, D, S * D, kvs, kvs[:, :, D:], 2 * D, S * 2 * D, o2, D, S * D, B, heads, S, S)
+    assert torch.equal(o, o2)

@@ -41,9 +41,39 @@ shapes = [("enc qkv", 768, 3072, 1024, 1, 0), ("enc proj", 768, 1024, 1024, 1, 1
           ("enc fc1", 768, 4096, 1024, 1, 0), ("enc fc2", 768, 1024, 4096, 1, 1),
           ("dec qkv", 768, 2304, 768, 4, 0), ("dec proj", 768, 768, 768, 4, 1),
           ("dec fc1", 768, 3072, 768, 4, 0), ("dec fc2", 768, 768, 3072, 4, 1),
-          ("dec kv", 768, 1536, 768, 4, 0), ("big", 4096, 4096, 4096, 1, 0)]
-tiles = [int(t) for t in os.environ.get("TILES", "0,1,10,11,2,12,7").split(",")]
-for name, M, N, K, b, res in shapes:
+          ("dec kv", 768, 1536, 768, 4, 0), ("dec qkvkv", 768, 3840, 768, 4, 0),
+          ("big", 4096, 4096, 4096, 1, 0)]
+tiles = [int(t) for t in os.environ.get("TILES", "0,1,2,7,8").split(",")]
+# DPT implicit 3x3 convs (NHWC bf16, Z = 4): (name, H, W, cin, cout, epilogue)
+convs = [("head.2+dpt", 384, 512, 128, 128, "dpt"), ("head.0", 192, 256, 256, 128, "bias"),
+         ("rcu 96x128", 96, 128, 256, 256, "relu_res"), ("rn0 96x128", 96, 128, 96, 256, "none"),
+         ("rcu 48x64", 48, 64, 256, 256, "relu_res")]
+for name, H, W, cin, cout, epi in convs if os.environ.get("CONVS", "1") != "0" else []:
+    b = 4
+    x = torch.randn(b, H, W, cin, device=dev).bfloat16()
+    w = (torch.randn(cout, 9 * cin, device=dev) / (9 * cin) ** 0.5).bfloat16()
+    bias = torch.randn(cout, device=dev)
+    out = torch.empty(b, H, W, cout, device=dev, dtype=torch.bfloat16)
+    kw = dict(sA=H * W * cin, sB=0, sC=H * W * cout, conv=(H, W, cin, H, W, 1))
+    if epi == "dpt":
+        w4, b4 = torch.randn(1, 4, 128, device=dev) * 0.05, torch.zeros(1, 4, device=dev)
+        pts = torch.empty(b, H * W, 3, device=dev)
+        conf = torch.empty(b, H * W, device=dev)
+        kw.update(bias=bias, flags=_lib.EPI_RELU, dpt=(w4, b4, pts, conf, 1.0), wmod=1)
+    elif epi == "bias":
+        kw.update(bias=bias)
+    elif epi == "relu_res":
+        R = torch.randn(b, H, W, cout, device=dev).bfloat16()
+        kw.update(bias=bias, R=R, sR=H * W * cout, flags=_lib.PRO_RELU | _lib.EPI_RES_BF16)
+    fl = 2.0 * H * W * cout * 9 * cin * b
+    res_s = []
+    for t in tiles:
+        os.environ["M3S_GEMM_TILE"] = str(t)
+        us = t_us(lambda: ops.gemm(x, w, out, H * W, cout, 9 * cin, b, **kw), n=10)
+        res_s.append(f"t{t}:{us:7.1f}us/{fl / us / 1e6:5.0f}TF")
+    os.environ.pop("M3S_GEMM_TILE", None)
+    print(f"conv {name:11s} {H}x{W} {cin}->{cout} x{b}: " + "  ".join(res_s), flush=True)
+for name, M, N, K, b, res in shapes if os.environ.get("GEMMS", "1") != "0" else []:
     A = torch.randn(b, M, K, device=dev).bfloat16()
     B = torch.randn(b, N, K, device=dev).bfloat16()
     bias = torch.randn(b * N, device=dev)
