@@ -148,6 +148,28 @@ int m3s_track_rays(const float* d_Twc_k, const float* d_Twc_f, const float* d_Xf
                    float rel_error, float delta_norm, float* d_T_WCf_out, float* d_T_CkCf_out,
                    int* d_info, void* d_workspace, void* stream);
 
+/* Frontend tracking glue around m3s_track_rays (FrameTracker2.track, tracker2.py:127-257,
+ * use_calib False): replaces the reference's torch ops between matching and the pose solve
+ * and after it.  X, C, Q: the pair outputs [2][n] (x3 for X; row 0 = frame, 1 = keyframe),
+ * idx i64[n] / valid_match u8[n]: matching.match's result, kf_C f32[n], kf_N f32[1]: the
+ * keyframe's accumulated confidence / update count.  workspace: m3s_glue_workspace_bytes(n),
+ * 16-B aligned, shared by the pre / post calls of one frame.
+ *   pre:  Xf = X[0][idx], Qk = sqrt(Q[0][idx] Q[1]), valid_opt (u8) as tracker2.py:130-193
+ *   post: lost = match_frac < min_match_frac | info[1]; unless lost, X_canon / C / N of the
+ *         keyframe take the weighted fusion with T_CkCf.act(X[1]) (frame.py:105-109);
+ *         flags u8[2] = {new_kf, lost} (tracker2.py:246-257), fracs f32[3] = {match_frac,
+ *         match_frac_k, unique_frac}. */
+size_t m3s_glue_workspace_bytes(int64_t n);
+int m3s_track_glue_pre(const float* d_X, const float* d_C, const float* d_Q, const int64_t* d_idx,
+                       const uint8_t* d_valid_match, const float* d_kf_C, const float* d_kf_N,
+                       int64_t n, float Q_conf, float C_conf, float* d_Xf, float* d_Qk,
+                       uint8_t* d_valid_opt, void* d_workspace, void* stream);
+int m3s_track_glue_post(const float* d_X, const float* d_C, const int64_t* d_idx,
+                        const uint8_t* d_valid_match, const int* d_info, const float* d_T_CkCf,
+                        int64_t n, float min_match_frac, float match_frac_thresh, float* d_kf_X,
+                        float* d_kf_C, float* d_kf_N, uint8_t* d_flags, float* d_fracs,
+                        void* d_workspace, void* stream);
+
 /* Calibrated variant.  K f32[3,3] device; n points; img h,w; meas_k f32[n,3];
  * valid_meas_k u8[n]. */
 int m3s_track_calib(const float* d_Twc_k, const float* d_Twc_f, const float* d_Xf,

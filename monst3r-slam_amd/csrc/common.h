@@ -29,6 +29,12 @@ __device__ __forceinline__ float m3s_wave_sum(float v) {
   return v;
 }
 
+__device__ __forceinline__ int m3s_wave_sum_int(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
 __device__ __forceinline__ double m3s_wave_sum_d(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

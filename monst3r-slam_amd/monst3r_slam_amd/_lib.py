@@ -43,6 +43,10 @@ SIGNATURES = {
                             _P]),
     "m3s_track_calib": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _F, _F, _F, _F,
                              _I, _F, _F, _P, _P, _P, _P, _P]),
+    "m3s_glue_workspace_bytes": (_SZ, [_I64]),
+    "m3s_track_glue_pre": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _F, _F, _P, _P, _P, _P, _P]),
+    "m3s_track_glue_post": (_I, [_P, _P, _P, _P, _P, _P, _I64, _F, _F, _P, _P, _P, _P, _P, _P,
+                                 _P]),
     "m3s_vit_gemm": (_I, [_P, _P]),
     "m3s_vit_layernorm": (_I, [_P, _I, _P, _P, _P, _I, _I64, _I64, _F, _I64, _I64, _I64, _I64,
                                _I64, _I, _P]),

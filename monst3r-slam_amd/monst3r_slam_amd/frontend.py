@@ -14,9 +14,11 @@ synchronisation except for the returned booleans (read lazily)."""
 from __future__ import annotations
 
 import dataclasses
+import os
 
 import torch
 
+from . import _lib
 from . import matching as M
 from . import tracker as T
 from .config import config as _config
@@ -46,6 +48,10 @@ class Tracker:
         self.idx_f2k = None
         self.kf = None
         self.split_heads = False   # measured: no gain
+        # the glue around the pose solve as 3 fused kernels (csrc/glue.hip) instead of the
+        # torch restatement below (~25 small launches)
+        self.fused_glue = os.environ.get("M3S_FUSED_GLUE", "1") != "0"
+        self._glue = None
 
     def add_keyframe(self, img, T_WC, X=None, C=None, feat=None):
         if feat is None:
@@ -93,6 +99,8 @@ class Tracker:
         self.idx_f2k.copy_(idx)                            # tracker2.py:127
         idx = idx[0]
         valid_match = valid_match[0]                       # [N,1]
+        if self.fused_glue and out["X"].is_contiguous() and out["C"].is_contiguous():
+            return self._track_fused(out, idx, valid_match, n, T_WCf_init)
         Qff = out["Q"][0].reshape(n, 1)
         Qkf = out["Q"][1].reshape(n, 1)
         Qk = torch.sqrt(Qff[idx] * Qkf)                    # tracker2.py:130
@@ -131,6 +139,44 @@ class Tracker:
                     feat_i=out.get("feat_i"), pair=out)
 
 
+    def _track_fused(self, out, idx, valid_match, n, T_WCf_init):
+        """track_outputs' glue on the fused kernels (m3s_track_glue_pre / _post): same
+        quantities and the same device-side lost / new-keyframe semantics."""
+        cfg_t = self.cfg["tracking"]
+        kf = self.kf
+        dev = idx.device
+        lib = _lib.load()
+        g = self._glue
+        if g is None or g["n"] != n:
+            g = self._glue = dict(
+                n=n, Xf=torch.empty((n, 3), dtype=torch.float32, device=dev),
+                Qk=torch.empty((n, 1), dtype=torch.float32, device=dev),
+                vo=torch.empty((n, 1), dtype=torch.uint8, device=dev),
+                ws=torch.empty((lib.m3s_glue_workspace_bytes(n),), dtype=torch.uint8, device=dev),
+                flags=torch.zeros(2, dtype=torch.uint8, device=dev),
+                fracs=torch.zeros(3, dtype=torch.float32, device=dev))
+        vm = valid_match.view(torch.uint8) if valid_match.dtype == torch.bool else valid_match
+        s = _lib.stream(dev)
+        X, C, Q = out["X"], out["C"], out["Q"].contiguous()
+        P = _lib.ptr
+        _lib.check(lib.m3s_track_glue_pre(P(X), P(C), P(Q), P(idx), P(vm), P(kf.C), P(kf.N), n,
+                                          float(cfg_t["Q_conf"]), float(cfg_t["C_conf"]),
+                                          P(g["Xf"]), P(g["Qk"]), P(g["vo"]), P(g["ws"]), s),
+                   "track_glue_pre")
+        T_WCf0 = kf.T_WC if T_WCf_init is None else T_WCf_init
+        T_WCf, T_CkCf, info = T.opt_pose_ray_dist_sim3(g["Xf"], kf.X_canon, T_WCf0, kf.T_WC,
+                                                       g["Qk"], g["vo"], cfg_t, check=False)
+        _lib.check(lib.m3s_track_glue_post(P(X), P(C), P(idx), P(vm), P(info), P(T_CkCf), n,
+                                           float(cfg_t["min_match_frac"]),
+                                           float(cfg_t["match_frac_thresh"]), P(kf.X_canon),
+                                           P(kf.C), P(kf.N), P(g["flags"]), P(g["fracs"]),
+                                           P(g["ws"]), s), "track_glue_post")
+        flags = g["flags"].view(torch.bool)
+        return dict(new_kf=flags[0], lost=flags[1], T_WCf=T_WCf, T_CkCf=T_CkCf, idx_f2k=idx,
+                    valid_match=valid_match, match_frac=g["fracs"][0], info=info,
+                    feat_i=out.get("feat_i"), pair=out)
+
+
 class FramePipeline:
     """Streaming tracking with the next frame's encoder prefetched: the MonST3R encoder of
     frame t+1 depends only on its image, so it runs on a side stream concurrently with
@@ -160,4 +206,3 @@ class FramePipeline:
         res = self.tr.track(img_cur, T_WCf_init, feat_i=self.feat[k % 2])
         main.wait_stream(self.side)
         return res
-

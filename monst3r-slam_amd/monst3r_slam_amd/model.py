@@ -383,6 +383,8 @@ class PairModel:
         # bf16 path: the blocks' LayerNorms folded into the following projections (ln_fold;
         # LN_STATS / LN_FOLD epilogues) instead of separate LayerNorm launches
         self.lnfold = os.environ.get("M3S_LNFOLD", "1") != "0"
+        # split heads: the local-feature MLP runs on the side chain ahead of the MASt3R heads
+        self.lf_side = os.environ.get("M3S_LF_SIDE", "1") != "0"
         self._tag = None      # buffer-key prefix of the head set being issued (split heads)
         self._wbase = 0       # first head-weight stack of that set
         self._wm = 4
@@ -706,14 +708,15 @@ class PairModel:
 
     def _fusion(self, k, path, skip, b, h, w, next_hw, next_skip, out):
         """FeatureFusionBlock (dpt_block.py:185-218) at resolution (h, w):
-        s = path + RCU1(skip) (path given; skip None for refinenet4); s = RCU2(s);
-        out = up2(out_conv(s)) (+ next_skip)  — out_conv commuted before the upsample."""
+        s = path + RCU1(skip) (skip None for refinenet4); s = RCU2(s);
+        out = up2(out_conv(s)) (+ next_skip)  — out_conv commuted before the upsample.
+        With a skip, `path` already holds path + skip (the previous level's upsample added
+        it), which is exactly RCU1's residual addend."""
         o, H = self.ops, self._hw
         F = self.a.feature_dim
         s1 = self._buf(("fus_s1", h, w), (b, h, w, F), BF16)
         if skip is not None:
-            self._rcu(skip, k, 1, b, h, w, s1, addend_res=path)   # path + conv(..)+skip
-            # RCU1's own residual is `skip`; path is added too → addend = path + skip
+            self._rcu(skip, k, 1, b, h, w, s1, addend_res=path)   # conv(..) + (path + skip)
         else:
             s1 = path
         s2 = self._buf(("fus_s2", h, w), (b, h, w, F), BF16)
@@ -774,18 +777,25 @@ class PairModel:
         pts = self._buf("pts3d", (Z, H, W, 3), F32)
         conf = self._buf("conf", (Z, H, W), F32)
         split = split and models == 2 and G == 1
+        desc = desc16 = dconf = ev_lf = None
         if split:
             main = torch.cuda.current_stream(self.dev)
             side = self.side[0]
             side.wait_stream(main)
             with torch.cuda.stream(side):
+                if self.lf_side:
+                    # the local features (needed by the matching) first on the side chain,
+                    # overlapping the MonST3R heads; then the MASt3R heads (joined later)
+                    self._wm = wm
+                    desc, desc16, dconf, _ = self._local_features(hooks, G, S, E, D, H, W)
+                    ev_lf = torch.cuda.Event()
+                    ev_lf.record(side)
                 sub = {k: v[2:4] for k, v in hooks.items()}
                 self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4])
                 self._ev_heads = torch.cuda.Event()
                 self._ev_heads.record(side)
         # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle
-        desc = desc16 = dconf = ev_lf = None
-        if models == 2:
+        if models == 2 and desc is None:
             self._wm = wm
             desc, desc16, dconf, ev_lf = self._local_features(hooks, G, S, E, D, H, W)
         if split:
@@ -848,13 +858,15 @@ class PairModel:
         # refinenets: path_k = up2(out_conv(RCU2(path_{k+1} + RCU1(R_k)))) with the next
         # level's skip pre-added by the upsample (consumed as RCU1's residual addend)
         p4 = self._buf("path4", (Z, gh, gw, F), BF16)
-        self._fusion(4, R[3], None, Z, g3h, g3w, (gh, gw), None, p4)
+        # (each level's upsample also adds the next level's skip: p_k = path_k + R_{k-1},
+        # the `path + skip` that refinenet_{k-1}'s RCU1 residual takes)
+        self._fusion(4, R[3], None, Z, g3h, g3w, (gh, gw), R[2], p4)
         p3 = self._buf("path3", (Z, 2 * gh, 2 * gw, F), BF16)
-        self._fusion_skip(3, p4, R[2], Z, gh, gw, (2 * gh, 2 * gw), p3)
+        self._fusion(3, p4, R[2], Z, gh, gw, (2 * gh, 2 * gw), R[1], p3)
         p2 = self._buf("path2", (Z, 4 * gh, 4 * gw, F), BF16)
-        self._fusion_skip(2, p3, R[1], Z, 2 * gh, 2 * gw, (4 * gh, 4 * gw), p2)
+        self._fusion(2, p3, R[1], Z, 2 * gh, 2 * gw, (4 * gh, 4 * gw), R[0], p2)
         p1 = self._buf("path1", (Z, 8 * gh, 8 * gw, F), BF16)
-        self._fusion_skip(1, p2, R[0], Z, 4 * gh, 4 * gw, (8 * gh, 8 * gw), p1)
+        self._fusion(1, p2, R[0], Z, 4 * gh, 4 * gw, (8 * gh, 8 * gw), None, p1)
         # head: conv3x3 F→F/2 @ (H/2, W/2), up2, conv3x3 → last_dim + ReLU, 1x1 → 4 + post
         h2, w2 = 8 * gh, 8 * gw
         hd0 = self._buf("head0", (Z, h2, w2, F // 2), BF16)
@@ -868,12 +880,6 @@ class PairModel:
                     dpt=(Hw("head4_w"), Hw("head4_b"), pts, conf, a.conf_min))
         self._tag, self._wbase = None, 0
 
-    def _fusion_skip(self, k, path, skip, b, h, w, next_hw, out):
-        """refinenet_k(path, skip): s = path + RCU1(skip) = conv2(...) + (skip + path)."""
-        F = self.a.feature_dim
-        sp = self._buf(("fus_sp", h, w), (b, h, w, F), BF16)
-        torch.add(skip, path, out=sp)
-        self._fusion(k, sp, skip, b, h, w, next_hw, None, out)
 
     # ---- monst3r_asymmetric_inference ----
     def pair(self, img_i, feat_j=None, img_j=None, feat_i=None, split_heads=False):
