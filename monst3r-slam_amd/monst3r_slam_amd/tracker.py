@@ -37,7 +37,7 @@ def opt_pose_ray_dist_sim3(Xf, Xk, T_WCf, T_WCk, Qk, valid, cfg=None, check=True
     T_WCf, T_WCk = _prep(T_WCf.reshape(8)), _prep(T_WCk.reshape(8))
     out_f = torch.empty(8, dtype=torch.float32, device=dev)
     out_rel = torch.empty(8, dtype=torch.float32, device=dev)
-    info = torch.zeros(4, dtype=torch.int32, device=dev)
+    info = torch.empty(4, dtype=torch.int32, device=dev)  # track_finish writes all 4
     ws = _ws(n, dev)
     st = _lib.load().m3s_track_rays(
         _lib.ptr(T_WCk), _lib.ptr(T_WCf), _lib.ptr(Xf), _lib.ptr(Xk), _lib.ptr(Qk),
@@ -68,7 +68,7 @@ def opt_pose_calib_sim3(Xf, T_WCf, T_WCk, Qk, valid, meas_k, valid_meas_k, K, im
     T_WCf, T_WCk = _prep(T_WCf.reshape(8)), _prep(T_WCk.reshape(8))
     out_f = torch.empty(8, dtype=torch.float32, device=dev)
     out_rel = torch.empty(8, dtype=torch.float32, device=dev)
-    info = torch.zeros(4, dtype=torch.int32, device=dev)
+    info = torch.empty(4, dtype=torch.int32, device=dev)  # track_finish writes all 4
     ws = _ws(n, dev)
     h, w = int(img_size[0]), int(img_size[1])
     st = _lib.load().m3s_track_calib(
