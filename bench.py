@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="skip the keyframe-graph (C4) leg")
     ap.add_argument("--graph-steps", type=int, default=2)
     ap.add_argument("--no-c5", action="store_true", help="skip the fp8 512x512 dyn-mask leg")
+    ap.add_argument("--no-retrieval", action="store_true",
+                    help="skip the keyframe-retrieval (loop-closure candidate) leg")
     ap.add_argument("--main-priority", type=int, default=0, help="tracking-chain stream priority")
     ap.add_argument("--side-priority", type=int, default=0, help="prefetch stream priority")
     ap.add_argument("--no-split-heads", action="store_true",
@@ -291,6 +293,79 @@ def c5_bench(model, dev, steps):
             "tolerance": "tests/test_gpu_vit.py::test_fp8_model_vs_fp32_restatement_512"}
 
 
+def retrieval_bench(dev, steps, n_db=64, cpu=True):
+    """RetrievalDatabase.update (query + add) per new keyframe at the
+    reference's sizes — 768 encoder tokens x 1024, nfeat 300, 64k x 1024 codebook, 5-way query
+    assignment — against a database of n_db keyframes, through the public update() (with its
+    two host syncs: the entry count and the k returned indices).  The dominant kernel
+    (m3s_retr_quantize, 2*300*65536*1024 flop fp32) is timed alone with HIP events on its stream.
+    CPU: the numpy oracle's update on the same database size (one keyframe, host cores)."""
+    import numpy as np
+    from monst3r_slam_amd import _lib
+    from monst3r_slam_amd.retrieval import RetrievalDatabase, synthetic_retrieval_weights
+    w = synthetic_retrieval_weights(seed=0)
+    db = RetrievalDatabase(w, device=dev, image_capacity=n_db + steps + 8)
+    g = torch.Generator(device=dev).manual_seed(21)
+    feats = [torch.randn(1, 768, 1024, device=dev, generator=g).bfloat16()
+             for _ in range(n_db + steps + 2)]
+    for f in feats[:n_db]:
+        db.update(f, True, 3, 5e-3)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for f in feats[n_db:n_db + steps]:
+        db.update(f, True, 3, 5e-3)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    # quantize kernel alone
+    lib, s = _lib.load(), _lib.stream(dev)
+    q = db.prep_features(feats[-1])[0].contiguous()
+    M, k = q.shape[0], 5
+    qn = torch.empty(M, dtype=torch.float32, device=dev)
+    _lib.check(lib.m3s_retr_rownorm(_lib.ptr(q), M, db.dim, 1, _lib.ptr(qn), s), "qn")
+    ws = torch.empty(int(lib.m3s_retr_quantize_workspace_bytes(M, db.ncent, k)), dtype=torch.uint8,
+                     device=dev)
+    codes = torch.empty((M, k), dtype=torch.int32, device=dev)
+    reps = 20
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for r in range(reps + 2):
+        if r == 2:
+            ev0.record()
+        _lib.check(lib.m3s_retr_quantize(_lib.ptr(q), _lib.ptr(qn), M, _lib.ptr(db.centroids),
+                                         _lib.ptr(db.cnorm2), db.ncent, db.dim, k, _lib.ptr(codes),
+                                         None, _lib.ptr(ws), s), "quantize")
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    q_ms = ev0.elapsed_time(ev1) / reps
+    flop = 2.0 * M * db.ncent * db.dim
+    out = {"workload": f"RetrievalDatabase.update(add_after_query=True, k=3) per keyframe, "
+                       f"{n_db}+ keyframes indexed, 768x1024 tokens, nfeat 300, "
+                       f"{db.ncent}x{db.dim} codebook, query multiple assignment 5",
+           "ms_per_keyframe_update": ms, "updates_per_s": 1e3 / ms,
+           "quantize_kernel": {"ms": q_ms, "tflops": flop / q_ms / 1e9, "peak_fp32_vector": 157.3,
+                               "frac": flop / q_ms / 1e9 / 157.3,
+                               "timing": "HIP events on the launch stream (the current stream)"}}
+    if cpu:
+        from oracle import retrieval_ref as R
+        wn = dict(w)
+        ref = R.RetrievalDatabase(wn, w["centroids"])
+        # index n_db keyframes cheaply: reuse the GPU's aggregated database contents
+        for gi in range(n_db):
+            n0, n1 = int(db.img_start[gi]), int(db.img_start[gi + 1])
+            ref.ivf.add(db.db_packed[n0:n1].cpu().numpy().view(np.uint32),
+                        db.db_words[n0:n1].cpu().numpy(), gi)
+        ref.kf_counter = n_db
+        f = feats[-2][0].float().cpu().numpy()
+        t0 = time.perf_counter()
+        ref.update(f, True, 3, 5e-3)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"ms_per_keyframe_update": dt * 1e3, "kind": "port",
+                               "cores": torch.get_num_threads(),
+                               "sample": "numpy oracle update of one keyframe vs the same "
+                                         f"{n_db}-keyframe database (fp64 whitening, fp32 "
+                                         "quantisation GEMM, python inverted file)"}
+    return out
+
+
 def pmc_traffic():
     """HBM bytes of the GEMM launches of one pair inference, from the committed rocprofv3
     PMC passes (tools/pmc_traffic.py over FETCH_SIZE / WRITE_SIZE runs of this bench; PMC
@@ -460,6 +535,9 @@ def main():
             line["cpu_baseline"] = cpu_baseline()
     if not args.no_c5 and rank == 0:
         line["fp8_dynmask_512"] = c5_bench(model, dev, max(5, args.steps // 2))
+    if not args.no_retrieval and rank == 0:
+        line["keyframe_retrieval"] = retrieval_bench(
+            dev, max(5, args.steps // 2), cpu=not args.no_cpu_baseline and world == 1)
     if not args.no_graph:
         kg = keyframe_graph_bench(model, dev, world, args.graph_steps)
         if rank == 0:

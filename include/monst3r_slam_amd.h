@@ -370,6 +370,60 @@ int m3s_apply_dynamic_mask(const uint8_t* d_mask, float* d_C, float* d_Q, void* 
                            int D_is_f16, int64_t batch, int64_t hw, int64_t fdim,
                            float value, int zero_descriptors, void* stream);
 
+/* ---- Keyframe retrieval / loop-closure candidates (RetrievalDatabase, 8(f) row 3) --------
+ * Replaces the per-keyframe work of mast3r_slam/retrieval_database.py:25-166 (prep_features,
+ * quantize_custom, accumulate_scores / aggregate_image, add_to_ivf_custom, ivf.search) and
+ * the Cython asmk/cython/hamming.pyx it calls.  Host bookkeeping (kf_counter, kf_ids, the
+ * inverted file's growth) stays in monst3r_slam_amd/retrieval.py.                          */
+
+/* Y[M][N] = (X[rows[i]][:K] - mu) W + bias (fp32; W [K][N] row-major, mu [K] and bias [N]
+ * optional, rows optional = identity).  X is f32 or bf16 with row stride ldx.  Whitener
+ * (mast3r/retrieval/model.py:55-76, fp64 in the reference) and the projector Linear. */
+int m3s_retr_affine(const void* d_X, int X_is_bf16, int64_t ldx, const int64_t* d_rows,
+                    const float* d_mu, const float* d_W, const float* d_bias, int64_t M,
+                    int64_t N, int64_t K, float* d_Y, void* stream);
+
+/* Per-row L2 norm (squared = 0; the 'l2norm' attention, model.py:133) or squared norm. */
+int m3s_retr_rownorm(const float* d_Y, int64_t M, int64_t N, int squared, float* d_out,
+                     void* stream);
+
+/* Sorted top-k of n <= 4096 keys (f32 or f64): largest first (largest = 1) or smallest
+ * first, ties to the lower index.  torch.topk as used by how_select_local (model.py:101)
+ * and RetrievalDatabase.update (retrieval_database.py:63).  d_vals optional. */
+int m3s_topk_select(const void* d_keys, int keys_f64, int64_t n, int64_t k, int largest,
+                    int64_t* d_idx, void* d_vals, void* stream);
+
+/* quantize_custom (retrieval_database.py:96-105): d = (|q|^2 + |c|^2) - 2 q.c against the
+ * codebook C [ncent][D] f32 (|c|^2 precomputed: m3s_retr_rownorm squared), the k <= 8
+ * smallest per query row, ascending (ties: lower index) -> codes i32 [M][k], dists f32
+ * (optional).  D % 16 == 0.  workspace: m3s_retr_quantize_workspace_bytes(M, ncent, k). */
+size_t m3s_retr_quantize_workspace_bytes(int64_t M, int64_t ncent, int64_t k);
+int m3s_retr_quantize(const float* d_Q, const float* d_qnorm2, int64_t M, const float* d_C,
+                      const float* d_cnorm2, int64_t ncent, int64_t D, int64_t k,
+                      int32_t* d_codes, float* d_dists, void* d_workspace, void* stream);
+
+/* ASMKKernel.aggregate_image + binarize_and_pack_2D (asmk/kernel.py:26-39,
+ * hamming.pyx:77-110): unique words of codes [n][k] (sorted, as np.unique) -> d_words
+ * (capacity n*k) and *d_count (device); per word the index-order sum of des[i] - C[word]
+ * over descriptors holding the word, packed as D/32 u32 with element 0 in bit 31
+ * -> d_packed [n*k][D/32].  d_flags: i32 [ncent] zeroed once by the caller, left zeroed.
+ * n <= 16384, D % 32 == 0. */
+int m3s_asmk_aggregate(const float* d_des, int64_t n, int64_t D, const int32_t* d_codes,
+                       int64_t k, const float* d_C, int64_t ncent, int32_t* d_flags,
+                       int32_t* d_words, int32_t* d_count, uint32_t* d_packed, void* stream);
+
+/* IVF.search with the binary ASMK similarity (inverted_file.py:186-208, kernel.py:56-68,
+ * functional.py:96-100; use_idf = False): the inverted file is flat and image-major (image g
+ * owns entries [img_start[g], img_start[g+1]) in ascending word order, as add() receives
+ * them).  scores f64 [n_images] = sum over entries whose word the query holds of
+ * f32(sim^alpha / sqrt(entries of g)) where sim = 1 - 2 hamming/D >= threshold, divided by
+ * sqrt(#query words).  d_word_map: i32 [ncent] all -1 (caller initialises once; restored). */
+int m3s_ivf_search(const uint32_t* d_qpacked, const int32_t* d_qwords, const int32_t* d_qcount,
+                   int64_t max_qwords, const uint32_t* d_db_packed, const int32_t* d_db_words,
+                   const int32_t* d_img_start, int64_t n_images, int64_t D, float alpha,
+                   float similarity_threshold, int32_t* d_word_map, double* d_scores,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

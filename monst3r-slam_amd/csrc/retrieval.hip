@@ -1,0 +1,575 @@
+// Keyframe retrieval / loop-closure candidate search (gfx950): the MASt3R retrieval head
+// (Whitener + projector + how_select_local) and the binary ASMK inverted-file search that
+// RetrievalDatabase.update runs once per new keyframe
+// (mast3r_slam/retrieval_database.py:25-166; asmk/kernel.py:26-68; asmk/inverted_file.py:156-208;
+//  asmk/cython/hamming.pyx; mast3r/retrieval/model.py:55-104).
+//
+//   m3s_retr_affine       Y = (X[rows] - mu) W + b, fp32 FMA tiles (whitening / projector)
+//   m3s_retr_rownorm      ||Y_r||_2 (the 'l2norm' attention, model.py:133)
+//   m3s_topk_select       sorted top-k of <= 4096 keys in one workgroup (bitonic in LDS)
+//   m3s_retr_quantize     ||q||^2 + ||c||^2 - 2 q.c against the codebook with the k smallest
+//                         kept in registers per row, chunk partials merged by a second pass
+//   m3s_asmk_aggregate    unique visual words, residual sums, sign binarisation packed MSB-first
+//   m3s_ivf_search        per-image ASMK scores over a flat image-major inverted file
+//
+// Numerics: fp32 like the reference's torch/numpy code, except the scores (fp64, as numpy's
+// `scores = np.zeros(n_images)` accumulates them).  Residual sums add descriptors in index order
+// (numpy's axis-0 sum), so the packed codes are bit-exact given identical descriptors.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// fp32 affine: Y[M][N] = (X[row(i)][:] - mu) * W[K][N] + bias.  64x64 tile, BK 16, 256 threads
+// each owning 4x4 outputs; X may be bf16 (encoder features) or fp32.
+template <typename XT>
+__global__ __launch_bounds__(256) void affine_kernel(const XT* __restrict__ X, int64_t ldx,
+                                                     const int64_t* __restrict__ rows,
+                                                     const float* __restrict__ mu,
+                                                     const float* __restrict__ W,
+                                                     const float* __restrict__ bias, int M, int N,
+                                                     int K, float* __restrict__ Y) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Bs[16][64];
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  float acc[4][4] = {};
+  // A tile load: 64 rows x 16 k -> 4 per thread (row = tid/4, k = (tid%4)*4 ..+3)
+  const int ar = tid >> 2, ak = (tid & 3) * 4;
+  const int grow = m0 + ar;
+  int64_t src = -1;
+  if (grow < M) src = rows ? rows[grow] : grow;
+  // B tile load: 16 k x 64 n -> 4 per thread (k = tid/16, n = (tid%16)*4)
+  const int bk = tid >> 4, bn = (tid & 15) * 4;
+  for (int k0 = 0; k0 < K; k0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int k = k0 + ak + j;
+      float v = 0.f;
+      if (src >= 0 && k < K) {
+        v = (float)X[src * ldx + k];
+        if (mu) v = v - mu[k];
+      }
+      As[ak + j][ar] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int k = k0 + bk, n = n0 + bn + j;
+      Bs[bk][bn + j] = (k < K && n < N) ? W[(int64_t)k * N + n] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; kk++) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; j++) b[j] = Bs[kk][tx + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int m = m0 + ty * 4 + i;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int n = n0 + tx + 16 * j;
+      if (n < N) Y[(int64_t)m * N + n] = acc[i][j] + (bias ? bias[n] : 0.f);
+    }
+  }
+}
+
+// One wave per row: sqrt(sum x^2) (sq = 0) or sum x^2 (sq = 1).
+__global__ __launch_bounds__(256) void rownorm_kernel(const float* __restrict__ Y, int64_t M,
+                                                      int N, int sq, float* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= M) return;
+  const float* y = Y + r * N;
+  float s = 0.f;
+  for (int c = lane; c < N; c += 64) s = fmaf(y[c], y[c], s);
+  s = m3s_wave_sum(s);
+  if (lane == 0) out[r] = sq ? s : sqrtf(s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sorted top-k of n <= 4096 keys (descending, ties to the lower index) by a bitonic sort of
+// (key, index) pairs in LDS; one workgroup of 1024 threads.  fp32 keys are widened exactly.
+constexpr int TOPK_MAX_N = 4096;
+
+template <typename KT>
+__global__ __launch_bounds__(1024) void topk_kernel(const KT* __restrict__ keys, int n, int k,
+                                                    int largest, int64_t* __restrict__ idx_out,
+                                                    KT* __restrict__ val_out) {
+  __shared__ double sk[TOPK_MAX_N];
+  __shared__ int si[TOPK_MAX_N];
+  int P = 1;
+  while (P < n) P <<= 1;
+  const double pad = largest ? -INFINITY : INFINITY;
+  for (int i = threadIdx.x; i < P; i += 1024) {
+    sk[i] = i < n ? (double)keys[i] : pad;
+    si[i] = i < n ? i : 0x7fffffff;
+  }
+  __syncthreads();
+  // "a before b": larger key first (or smaller when !largest), ties by lower index
+  auto before = [largest](double ka, int ia, double kb, int ib) {
+    if (ka != kb) return largest ? ka > kb : ka < kb;
+    return ia < ib;
+  };
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < P / 2; t += 1024) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const double ka = sk[lo], kb = sk[hi];
+        const int ia = si[lo], ib = si[hi];
+        const bool swap = up ? before(kb, ib, ka, ia) : before(ka, ia, kb, ib);
+        if (swap) {
+          sk[lo] = kb; sk[hi] = ka;
+          si[lo] = ib; si[hi] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < k; i += 1024) {
+    idx_out[i] = si[i];
+    if (val_out) val_out[i] = (KT)sk[i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Codebook quantisation (retrieval_database.py:96-105): d = (|q|^2 + |c|^2) - 2 q.c, the k
+// smallest per query row, ascending, ties to the lower centroid index.
+// Grid (chunks, ceil(M/64)); a block covers 64 query rows x `chunk` centroids in 128-wide tiles.
+constexpr int QK_MAX = 8;
+
+__device__ __forceinline__ bool qless(float da, int ia, float db, int ib) {
+  return da < db || (da == db && ia < ib);
+}
+
+__device__ __forceinline__ void qinsert(float* bd, int* bi, int k, float d, int i) {
+  float wd = bd[0];
+  int wi = bi[0];
+#pragma unroll
+  for (int s = 1; s < QK_MAX; s++)
+    if (s == k - 1) {
+      wd = bd[s];
+      wi = bi[s];
+    }
+  if (!qless(d, i, wd, wi)) return;
+  bool placed = false;
+#pragma unroll
+  for (int s = QK_MAX - 1; s >= 0; s--) {
+    if (s >= k || placed) continue;
+    if (s > 0 && qless(d, i, bd[s - 1], bi[s - 1])) {
+      bd[s] = bd[s - 1];
+      bi[s] = bi[s - 1];
+    } else {
+      bd[s] = d;
+      bi[s] = i;
+      placed = true;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__ Q,
+                                                       const float* __restrict__ qn,
+                                                       const float* __restrict__ C,
+                                                       const float* __restrict__ cn, int M,
+                                                       int NC, int D, int chunk, int k,
+                                                       float* __restrict__ part_d,
+                                                       int* __restrict__ part_i) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Bs[16][128 + 4];
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;
+  const int m0 = blockIdx.y * 64;
+  const int c_begin = blockIdx.x * chunk;
+  const int c_end = min(NC, c_begin + chunk);
+  float bd[4][QK_MAX];
+  int bi[4][QK_MAX];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int s = 0; s < QK_MAX; s++) {
+      bd[i][s] = INFINITY;
+      bi[i][s] = 0x7fffffff;
+    }
+  const int ar = tid >> 2, ak = (tid & 3) * 4;
+  const int bc = tid >> 1, bk = (tid & 1) * 8;  // B load: 128 centroids x 16 dims, 8 per thread
+  for (int c0 = c_begin; c0 < c_end; c0 += 128) {
+    float acc[4][8] = {};
+    for (int k0 = 0; k0 < D; k0 += 16) {
+      {
+        const int m = m0 + ar;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < M && k0 + ak + 3 < D)
+          v = *reinterpret_cast<const float4*>(Q + (int64_t)m * D + k0 + ak);
+        As[ak + 0][ar] = v.x;
+        As[ak + 1][ar] = v.y;
+        As[ak + 2][ar] = v.z;
+        As[ak + 3][ar] = v.w;
+      }
+      {
+        const int c = c0 + bc;
+        float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+        if (c < c_end && k0 + bk + 7 < D) {
+          const float4* p = reinterpret_cast<const float4*>(C + (int64_t)c * D + k0 + bk);
+          v0 = p[0];
+          v1 = p[1];
+        }
+        Bs[bk + 0][bc] = v0.x; Bs[bk + 1][bc] = v0.y; Bs[bk + 2][bc] = v0.z; Bs[bk + 3][bc] = v0.w;
+        Bs[bk + 4][bc] = v1.x; Bs[bk + 5][bc] = v1.y; Bs[bk + 6][bc] = v1.z; Bs[bk + 7][bc] = v1.w;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < 16; kk++) {
+        float a[4], b[8];
+#pragma unroll
+        for (int i = 0; i < 4; i++) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+        for (int j = 0; j < 8; j++) b[j] = Bs[kk][tx + 16 * j];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int j = 0; j < 8; j++) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int m = m0 + ty * 4 + i;
+      const float q2 = m < M ? qn[m] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int c = c0 + tx + 16 * j;  // increasing per thread: ties keep the earlier index
+        if (c < c_end) {
+          const float d = (q2 + cn[c]) - 2.0f * acc[i][j];
+          qinsert(bd[i], bi[i], k, d, c);
+        }
+      }
+    }
+  }
+  // merge the 16 column-threads of every row (adjacent lanes, disjoint columns): butterfly
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      float od[QK_MAX];
+      int oi[QK_MAX];
+#pragma unroll
+      for (int s = 0; s < QK_MAX; s++) {
+        od[s] = __shfl_xor(bd[i][s], off, 64);
+        oi[s] = __shfl_xor(bi[i][s], off, 64);
+      }
+#pragma unroll
+      for (int s = 0; s < QK_MAX; s++)
+        if (s < k) qinsert(bd[i], bi[i], k, od[s], oi[s]);
+    }
+  }
+  if (tx == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int m = m0 + ty * 4 + i;
+      if (m >= M) continue;
+      const int64_t o = ((int64_t)m * gridDim.x + blockIdx.x) * k;
+#pragma unroll
+      for (int s = 0; s < QK_MAX; s++)
+        if (s < k) {
+          part_d[o + s] = bd[i][s];
+          part_i[o + s] = bi[i][s];
+        }
+    }
+  }
+}
+
+// One 64-thread block per query row: merge the chunk partials into the final k codes.
+__global__ __launch_bounds__(64) void quantize_merge_kernel(const float* __restrict__ part_d,
+                                                            const int* __restrict__ part_i,
+                                                            int nchunk, int k,
+                                                            int32_t* __restrict__ codes,
+                                                            float* __restrict__ dists) {
+  __shared__ float sd[64 * QK_MAX];
+  __shared__ int si[64 * QK_MAX];
+  const int m = blockIdx.x, t = threadIdx.x;
+  float rd[QK_MAX];
+  int ri[QK_MAX];
+  for (int s = 0; s < QK_MAX; s++) {
+    rd[s] = INFINITY;
+    ri[s] = 0x7fffffff;
+  }
+  const int64_t base = (int64_t)m * nchunk * k;
+  for (int c = t; c < nchunk; c += 64)
+    for (int s = 0; s < k; s++) qinsert(rd, ri, k, part_d[base + c * k + s], part_i[base + c * k + s]);
+  for (int s = 0; s < k; s++) {
+    sd[t * QK_MAX + s] = rd[s];
+    si[t * QK_MAX + s] = ri[s];
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int u = 1; u < 64; u++)
+      for (int s = 0; s < k; s++) qinsert(rd, ri, k, sd[u * QK_MAX + s], si[u * QK_MAX + s]);
+    for (int s = 0; s < k; s++) {
+      codes[(int64_t)m * k + s] = ri[s];
+      if (dists) dists[(int64_t)m * k + s] = rd[s];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// ASMK aggregation (kernel.py:26-39): unique words of the codes (sorted, np.unique), per word
+// the sum over descriptors having that word among their k codes of (des - centroid), then
+// binarize_and_pack_2D (hamming.pyx:77-110): bit = sum > 0, element 0 of each 32 in the MSB.
+__global__ __launch_bounds__(256) void mark_words_kernel(const int32_t* __restrict__ codes,
+                                                         int64_t n, int32_t* __restrict__ flags) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) flags[codes[i]] = 1;
+}
+
+// One workgroup: ordered compaction of the flag array -> sorted unique words + count; clears
+// the flags it read so the workspace is ready for the next call.
+__global__ __launch_bounds__(1024) void compact_words_kernel(int32_t* __restrict__ flags, int NC,
+                                                             int32_t* __restrict__ words,
+                                                             int32_t* __restrict__ count) {
+  __shared__ int wsum[16];
+  __shared__ int base;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) base = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < NC; c0 += 1024) {
+    const int c = c0 + t;
+    const int f = c < NC ? flags[c] : 0;
+    const uint64_t b = __ballot(f);
+    const int pre = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(b);
+    __syncthreads();
+    int off = base;
+    for (int u = 0; u < w; u++) off += wsum[u];
+    if (f) {
+      words[off + pre] = c;
+      flags[c] = 0;
+    }
+    __syncthreads();
+    if (t == 0) {
+      int s = 0;
+      for (int u = 0; u < 16; u++) s += wsum[u];
+      base += s;
+    }
+    __syncthreads();
+  }
+  if (t == 0) *count = base;
+}
+
+// One workgroup per unique word (blocks past the count exit): thread t owns elements
+// t, t+256, ... of the residual sum; packed with a wave ballot (lane l = element base + l).
+__global__ __launch_bounds__(256) void aggregate_kernel(const float* __restrict__ des, int n,
+                                                        int D, const int32_t* __restrict__ codes,
+                                                        int k, const float* __restrict__ C,
+                                                        const int32_t* __restrict__ words,
+                                                        const int32_t* __restrict__ count,
+                                                        uint32_t* __restrict__ packed) {
+  const int u = blockIdx.x;
+  if (u >= *count) return;
+  const int word = words[u];
+  const int W32 = D / 32;
+  extern __shared__ int member[];
+  for (int i = threadIdx.x; i < n; i += 256) {
+    int hit = 0;
+    for (int s = 0; s < k; s++) hit |= codes[(int64_t)i * k + s] == word;
+    member[i] = hit;
+  }
+  __syncthreads();
+  const float* c = C + (int64_t)word * D;
+  const int lane = threadIdx.x & 63;
+  for (int e0 = 0; e0 < D; e0 += 256) {
+    const int e = e0 + threadIdx.x;
+    float acc = 0.f;
+    if (e < D) {
+      const float ce = c[e];
+      for (int i = 0; i < n; i++)
+        if (member[i]) acc = acc + (des[(int64_t)i * D + e] - ce);
+    }
+    const uint64_t b = __ballot(e < D && acc > 0.f);
+    // elements e0 + wave*64 + [0,32) -> word (e0 + wave*64)/32, [32,64) -> the next
+    const int wbase = (e0 + (threadIdx.x & ~63)) / 32;
+    if (lane == 0 && wbase < W32)
+      packed[(int64_t)u * W32 + wbase] = __builtin_bitreverse32((uint32_t)(b & 0xffffffffull));
+    if (lane == 32 && wbase + 1 < W32)
+      packed[(int64_t)u * W32 + wbase + 1] = __builtin_bitreverse32((uint32_t)(b >> 32));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// IVF search (inverted_file.py:186-208 + kernel.py:56-68 + functional.py:96-100) over a flat
+// image-major inverted file: image g owns entries [img_start[g], img_start[g+1]).  Per entry
+// whose word the query holds: sim = 1 - 2 hamming/bits (fp32), kept if sim >= thr, sim^alpha,
+// divided by sqrt(norm_factor[g]) (= entries of g without idf) in fp64; per-image sums in a
+// fixed order; the total / sqrt(#query words).
+__global__ __launch_bounds__(256) void word_map_kernel(const int32_t* __restrict__ qwords,
+                                                       const int32_t* __restrict__ qcount,
+                                                       int32_t* __restrict__ map, int set) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < *qcount) map[qwords[i]] = set ? i : -1;
+}
+
+__global__ __launch_bounds__(256) void ivf_score_kernel(
+    const uint32_t* __restrict__ qpacked, const int32_t* __restrict__ qcount,
+    const int32_t* __restrict__ map, const uint32_t* __restrict__ db_packed,
+    const int32_t* __restrict__ db_words, const int32_t* __restrict__ img_start, int W32,
+    float alpha, float thr, double* __restrict__ scores) {
+  __shared__ float contrib[256];
+  const int g = blockIdx.x;
+  const int b = img_start[g], e = img_start[g + 1];
+  const float nbits = (float)(W32 * 32);
+  const double rnorm = sqrt((double)(e - b));  // norm_factor[g] without idf
+  double s = 0.0;
+  for (int j0 = b; j0 < e; j0 += 256) {
+    const int j = j0 + threadIdx.x;
+    float c = 0.f;
+    if (j < e) {
+      const int q = map[db_words[j]];
+      if (q >= 0) {
+        int hd = 0;
+        for (int w = 0; w < W32; w++)
+          hd += __popc(qpacked[(int64_t)q * W32 + w] ^ db_packed[(int64_t)j * W32 + w]);
+        const float h = (float)hd / nbits;
+        const float sim = -2.0f * h + 1.0f;  // hamming -> similarity in [-1, 1] (fp32)
+        if (sim >= thr) {
+          // sim ** alpha (fp32), *= idf (1), /= sqrt(norm_factor) in fp64 stored back to fp32
+          c = (float)((double)powf(sim, alpha) / rnorm);
+        }
+      }
+    }
+    contrib[threadIdx.x] = c;
+    __syncthreads();
+    // entries of an image are in ascending word order, the order the reference's loop over
+    // the query's (sorted) words adds them: sum sequentially in fp64
+    if (threadIdx.x == 0) {
+      const int m = min(256, e - j0);
+      for (int u = 0; u < m; u++) s += (double)contrib[u];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) scores[g] = s / (double)sqrtf((float)*qcount);
+}
+
+}  // namespace
+
+extern "C" int m3s_retr_affine(const void* d_X, int X_is_bf16, int64_t ldx, const int64_t* d_rows,
+                               const float* d_mu, const float* d_W, const float* d_bias, int64_t M,
+                               int64_t N, int64_t K, float* d_Y, void* stream) {
+  if (!d_X || !d_W || !d_Y || M < 0 || N <= 0 || K <= 0 || ldx < K) return M3S_ERR_INVALID_ARG;
+  if (M == 0) return M3S_OK;
+  dim3 grid(m3s_div_up(N, 64), m3s_div_up(M, 64));
+  hipStream_t s = m3s_stream(stream);
+  if (X_is_bf16)
+    hipLaunchKernelGGL((affine_kernel<__bf16>), grid, dim3(256), 0, s,
+                       reinterpret_cast<const __bf16*>(d_X), ldx, d_rows, d_mu, d_W, d_bias,
+                       (int)M, (int)N, (int)K, d_Y);
+  else
+    hipLaunchKernelGGL((affine_kernel<float>), grid, dim3(256), 0, s,
+                       reinterpret_cast<const float*>(d_X), ldx, d_rows, d_mu, d_W, d_bias,
+                       (int)M, (int)N, (int)K, d_Y);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_retr_rownorm(const float* d_Y, int64_t M, int64_t N, int squared, float* d_out,
+                                void* stream) {
+  if (!d_Y || !d_out || M < 0 || N <= 0) return M3S_ERR_INVALID_ARG;
+  if (M == 0) return M3S_OK;
+  hipLaunchKernelGGL(rownorm_kernel, dim3(m3s_div_up(M, 4)), dim3(256), 0, m3s_stream(stream),
+                     d_Y, M, (int)N, squared, d_out);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_topk_select(const void* d_keys, int keys_f64, int64_t n, int64_t k, int largest,
+                               int64_t* d_idx, void* d_vals, void* stream) {
+  if (!d_keys || !d_idx || n <= 0 || n > TOPK_MAX_N || k < 0 || k > n) return M3S_ERR_INVALID_ARG;
+  if (k == 0) return M3S_OK;
+  hipStream_t s = m3s_stream(stream);
+  if (keys_f64)
+    hipLaunchKernelGGL((topk_kernel<double>), dim3(1), dim3(1024), 0, s,
+                       reinterpret_cast<const double*>(d_keys), (int)n, (int)k, largest, d_idx,
+                       reinterpret_cast<double*>(d_vals));
+  else
+    hipLaunchKernelGGL((topk_kernel<float>), dim3(1), dim3(1024), 0, s,
+                       reinterpret_cast<const float*>(d_keys), (int)n, (int)k, largest, d_idx,
+                       reinterpret_cast<float*>(d_vals));
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" size_t m3s_retr_quantize_workspace_bytes(int64_t M, int64_t ncent, int64_t k) {
+  const int64_t nchunk = (ncent + 255) / 256;
+  return (size_t)(M * nchunk * k) * (sizeof(float) + sizeof(int));
+}
+
+extern "C" int m3s_retr_quantize(const float* d_Q, const float* d_qnorm2, int64_t M,
+                                 const float* d_C, const float* d_cnorm2, int64_t ncent, int64_t D,
+                                 int64_t k, int32_t* d_codes, float* d_dists, void* d_workspace,
+                                 void* stream) {
+  if (!d_Q || !d_qnorm2 || !d_C || !d_cnorm2 || !d_codes || !d_workspace) return M3S_ERR_INVALID_ARG;
+  if (M < 0 || ncent <= 0 || D <= 0 || D % 16 || k < 1 || k > QK_MAX || k > ncent)
+    return M3S_ERR_INVALID_ARG;
+  if (M == 0) return M3S_OK;
+  const int chunk = 256;
+  const int nchunk = (int)((ncent + chunk - 1) / chunk);
+  float* pd = reinterpret_cast<float*>(d_workspace);
+  int* pi = reinterpret_cast<int*>(pd + M * nchunk * k);
+  hipStream_t s = m3s_stream(stream);
+  hipLaunchKernelGGL(quantize_kernel, dim3(nchunk, m3s_div_up(M, 64)), dim3(256), 0, s, d_Q,
+                     d_qnorm2, d_C, d_cnorm2, (int)M, (int)ncent, (int)D, chunk, (int)k, pd, pi);
+  hipLaunchKernelGGL(quantize_merge_kernel, dim3((unsigned)M), dim3(64), 0, s, pd, pi, nchunk,
+                     (int)k, d_codes, d_dists);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_asmk_aggregate(const float* d_des, int64_t n, int64_t D, const int32_t* d_codes,
+                                  int64_t k, const float* d_C, int64_t ncent, int32_t* d_flags,
+                                  int32_t* d_words, int32_t* d_count, uint32_t* d_packed,
+                                  void* stream) {
+  if (!d_des || !d_codes || !d_C || !d_flags || !d_words || !d_count || !d_packed)
+    return M3S_ERR_INVALID_ARG;
+  if (n <= 0 || D <= 0 || D % 32 || k < 1 || ncent <= 0 || n > 16384) return M3S_ERR_INVALID_ARG;
+  hipStream_t s = m3s_stream(stream);
+  hipLaunchKernelGGL(mark_words_kernel, dim3(m3s_div_up(n * k, 256)), dim3(256), 0, s, d_codes,
+                     n * k, d_flags);
+  hipLaunchKernelGGL(compact_words_kernel, dim3(1), dim3(1024), 0, s, d_flags, (int)ncent, d_words,
+                     d_count);
+  hipLaunchKernelGGL(aggregate_kernel, dim3((unsigned)(n * k)), dim3(256), n * sizeof(int), s,
+                     d_des, (int)n, (int)D, d_codes, (int)k, d_C, d_words, d_count, d_packed);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_ivf_search(const uint32_t* d_qpacked, const int32_t* d_qwords,
+                              const int32_t* d_qcount, int64_t max_qwords,
+                              const uint32_t* d_db_packed, const int32_t* d_db_words,
+                              const int32_t* d_img_start, int64_t n_images, int64_t D, float alpha,
+                              float similarity_threshold, int32_t* d_word_map, double* d_scores,
+                              void* stream) {
+  if (!d_qpacked || !d_qwords || !d_qcount || !d_db_packed || !d_db_words || !d_img_start ||
+      !d_word_map || !d_scores || D % 32 || max_qwords <= 0)
+    return M3S_ERR_INVALID_ARG;
+  if (n_images <= 0) return M3S_OK;
+  hipStream_t s = m3s_stream(stream);
+  const unsigned gq = m3s_div_up(max_qwords, 256);
+  hipLaunchKernelGGL(word_map_kernel, dim3(gq), dim3(256), 0, s, d_qwords, d_qcount, d_word_map, 1);
+  hipLaunchKernelGGL(ivf_score_kernel, dim3((unsigned)n_images), dim3(256), 0, s, d_qpacked,
+                     d_qcount, d_word_map, d_db_packed, d_db_words, d_img_start, (int)(D / 32),
+                     alpha, similarity_threshold, d_scores);
+  hipLaunchKernelGGL(word_map_kernel, dim3(gq), dim3(256), 0, s, d_qwords, d_qcount, d_word_map, 0);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}

@@ -63,6 +63,13 @@ SIGNATURES = {
     "m3s_ego_flow": (_I, [_P, _P, _I64, _I64, _P, _P]),
     "m3s_flow_error_mask": (_I, [_P, _P, _I64, _F, _P, _P, _P]),
     "m3s_apply_dynamic_mask": (_I, [_P, _P, _P, _P, _I, _I64, _I64, _I64, _F, _I, _P]),
+    "m3s_retr_affine": (_I, [_P, _I, _I64, _P, _P, _P, _P, _I64, _I64, _I64, _P, _P]),
+    "m3s_retr_rownorm": (_I, [_P, _I64, _I64, _I, _P, _P]),
+    "m3s_topk_select": (_I, [_P, _I, _I64, _I64, _I, _P, _P, _P]),
+    "m3s_retr_quantize_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
+    "m3s_retr_quantize": (_I, [_P, _P, _I64, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P]),
+    "m3s_asmk_aggregate": (_I, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
+    "m3s_ivf_search": (_I, [_P, _P, _P, _I64, _P, _P, _P, _I64, _I64, _F, _F, _P, _P, _P]),
 }
 
 
