@@ -396,7 +396,7 @@ int m3s_topk_select(const void* d_keys, int keys_f64, int64_t n, int64_t k, int 
 /* quantize_custom (retrieval_database.py:96-105): d = (|q|^2 + |c|^2) - 2 q.c against the
  * codebook C [ncent][D] f32 (|c|^2 precomputed: m3s_retr_rownorm squared), the k <= 8
  * smallest per query row, ascending (ties: lower index) -> codes i32 [M][k], dists f32
- * (optional).  D % 16 == 0.  workspace: m3s_retr_quantize_workspace_bytes(M, ncent, k). */
+ * (optional).  D % 32 == 0.  workspace: m3s_retr_quantize_workspace_bytes(M, ncent, k). */
 size_t m3s_retr_quantize_workspace_bytes(int64_t M, int64_t ncent, int64_t k);
 int m3s_retr_quantize(const float* d_Q, const float* d_qnorm2, int64_t M, const float* d_C,
                       const float* d_cnorm2, int64_t ncent, int64_t D, int64_t k,

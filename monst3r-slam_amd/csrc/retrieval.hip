@@ -7,8 +7,8 @@
 //   m3s_retr_affine       Y = (X[rows] - mu) W + b, fp32 FMA tiles (whitening / projector)
 //   m3s_retr_rownorm      ||Y_r||_2 (the 'l2norm' attention, model.py:133)
 //   m3s_topk_select       sorted top-k of <= 4096 keys in one workgroup (bitonic in LDS)
-//   m3s_retr_quantize     ||q||^2 + ||c||^2 - 2 q.c against the codebook with the k smallest
-//                         kept in registers per row, chunk partials merged by a second pass
+//   m3s_retr_quantize     ||q||^2 + ||c||^2 - 2 q.c against the codebook on the f32 MFMA, the
+//                         k smallest per row and 256-centroid chunk, merged by a second pass
 //   m3s_asmk_aggregate    unique visual words, residual sums, sign binarisation packed MSB-first
 //   m3s_ivf_search        per-image ASMK scores over a flat image-major inverted file
 //
@@ -180,114 +180,143 @@ __device__ __forceinline__ void qinsert(float* bd, int* bi, int k, float d, int 
   }
 }
 
-__global__ __launch_bounds__(256) void quantize_kernel(const float* __restrict__ Q,
-                                                       const float* __restrict__ qn,
-                                                       const float* __restrict__ C,
-                                                       const float* __restrict__ cn, int M,
-                                                       int NC, int D, int chunk, int k,
-                                                       float* __restrict__ part_d,
-                                                       int* __restrict__ part_i) {
-  __shared__ float As[16][64 + 4];
-  __shared__ float Bs[16][128 + 4];
-  const int tid = threadIdx.x;
-  const int tx = tid & 15, ty = tid >> 4;
-  const int m0 = blockIdx.y * 64;
-  const int c_begin = blockIdx.x * chunk;
-  const int c_end = min(NC, c_begin + chunk);
-  float bd[4][QK_MAX];
-  int bi[4][QK_MAX];
+// f32-input MFMA (v_mfma_f32_32x32x2_f32: exact fp32 products, k-ordered fp32 accumulation).
+// Block: 64 query rows x 256 centroids (one chunk), 4 waves in 2 (rows) x 2 (cols), each wave
+// 32 rows x 128 cols = 4 accumulators of 32x32.  K staged through LDS 32 at a time, operands
+// kept row-major with a 1-float pad (fragment reads conflict-free).  The distance tile then
+// goes through LDS: 4 threads per row scan 64 columns each keeping the k smallest, merged by a
+// 2-step butterfly.  1-D grid, XCD-aware: the row blocks of one chunk run on one XCD so the
+// chunk's 1 MB of centroids is fetched from HBM once and re-read from that XCD's L2.
+constexpr int QBM = 64, QBN = 256, QBK = 32, QPAD = QBK + 1;
+constexpr int QDST = QBN + 1;
+constexpr int Q_LDS_FLOATS = (QBM * QDST > (QBM + QBN) * QPAD) ? QBM * QDST : (QBM + QBN) * QPAD;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(256, 2) void quantize_kernel(const float* __restrict__ Q,
+                                                          const float* __restrict__ qn,
+                                                          const float* __restrict__ C,
+                                                          const float* __restrict__ cn, int M,
+                                                          int NC, int D, int nchunk, int nrb,
+                                                          int k, float* __restrict__ part_d,
+                                                          int* __restrict__ part_i) {
+  __shared__ float lds[Q_LDS_FLOATS];
+  float* As = lds;                 // [QBM][QPAD]
+  float* Bs = lds + QBM * QPAD;    // [QBN][QPAD]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // blockIdx -> (chunk, row block); same chunk on the same XCD when nchunk % 8 == 0
+  int chunk, rb;
+  {
+    const int L = blockIdx.x;
+    if ((nchunk & 7) == 0) {
+      const int xcd = L & 7, j = L >> 3;
+      chunk = (j / nrb) * 8 + xcd;
+      rb = j % nrb;
+    } else {
+      chunk = L / nrb;
+      rb = L % nrb;
+    }
+  }
+  const int m0 = rb * QBM, c0 = chunk * QBN;
+  const int wm = wave >> 1, wn = wave & 1;
+  f32x16 acc[4];
 #pragma unroll
-  for (int i = 0; i < 4; i++)
+  for (int t = 0; t < 4; t++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[t][r] = 0.f;
+  // loaders: A 64 rows x 32 k = 512 float4 (2 per thread); B 256 x 32 = 2048 float4 (8 each).
+  // The next K slice is fetched into registers while the MFMAs consume the current one.
+  float4 ra[2], rb4[8];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int f = tid + u * 256;
+      const int m = m0 + (f >> 3);
+      ra[u] = m < M ? *reinterpret_cast<const float4*>(Q + (int64_t)m * D + k0 + (f & 7) * 4)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int f = tid + u * 256;
+      const int c = c0 + (f >> 3);
+      rb4[u] = c < NC ? *reinterpret_cast<const float4*>(C + (int64_t)c * D + k0 + (f & 7) * 4)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  fetch(0);
+  const float* ap = As + (wm * 32 + (lane & 31)) * QPAD + (lane >> 5);
+  const float* bp = Bs + (wn * 128 + (lane & 31)) * QPAD + (lane >> 5);
+  for (int k0 = 0; k0 < D; k0 += QBK) {
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int f = tid + u * 256;
+      float* d = As + (f >> 3) * QPAD + (f & 7) * 4;
+      d[0] = ra[u].x; d[1] = ra[u].y; d[2] = ra[u].z; d[3] = ra[u].w;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int f = tid + u * 256;
+      float* d = Bs + (f >> 3) * QPAD + (f & 7) * 4;
+      d[0] = rb4[u].x; d[1] = rb4[u].y; d[2] = rb4[u].z; d[3] = rb4[u].w;
+    }
+    __syncthreads();
+    if (k0 + QBK < D) fetch(k0 + QBK);
+#pragma unroll
+    for (int kk = 0; kk < QBK; kk += 2) {
+      const float a = ap[kk];
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bp[t * 32 * QPAD + kk], acc[t], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // distances into LDS: d = (|q|^2 + |c|^2) - 2 q.c
+  float* dst = lds;  // [QBM][QDST]
+#pragma unroll
+  for (int t = 0; t < 4; t++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int row = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int col = wn * 128 + t * 32 + (lane & 31);
+      dst[row * QDST + col] = acc[t][r];
+    }
+  __syncthreads();
+  const int row = tid >> 2, part = tid & 3;
+  const int m = m0 + row;
+  const float q2 = m < M ? qn[m] : 0.f;
+  float bd[QK_MAX];
+  int bi[QK_MAX];
+#pragma unroll
+  for (int s = 0; s < QK_MAX; s++) {
+    bd[s] = INFINITY;
+    bi[s] = 0x7fffffff;
+  }
+  for (int j = 0; j < QBN / 4; j++) {
+    const int cl = part + 4 * j;  // increasing per thread: ties keep the earlier index
+    const int c = c0 + cl;
+    if (c < NC) qinsert(bd, bi, k, (q2 + cn[c]) - 2.0f * dst[row * QDST + cl], c);
+  }
+#pragma unroll
+  for (int off = 1; off < 4; off <<= 1) {
+    float od[QK_MAX];
+    int oi[QK_MAX];
 #pragma unroll
     for (int s = 0; s < QK_MAX; s++) {
-      bd[i][s] = INFINITY;
-      bi[i][s] = 0x7fffffff;
-    }
-  const int ar = tid >> 2, ak = (tid & 3) * 4;
-  const int bc = tid >> 1, bk = (tid & 1) * 8;  // B load: 128 centroids x 16 dims, 8 per thread
-  for (int c0 = c_begin; c0 < c_end; c0 += 128) {
-    float acc[4][8] = {};
-    for (int k0 = 0; k0 < D; k0 += 16) {
-      {
-        const int m = m0 + ar;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (m < M && k0 + ak + 3 < D)
-          v = *reinterpret_cast<const float4*>(Q + (int64_t)m * D + k0 + ak);
-        As[ak + 0][ar] = v.x;
-        As[ak + 1][ar] = v.y;
-        As[ak + 2][ar] = v.z;
-        As[ak + 3][ar] = v.w;
-      }
-      {
-        const int c = c0 + bc;
-        float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
-        if (c < c_end && k0 + bk + 7 < D) {
-          const float4* p = reinterpret_cast<const float4*>(C + (int64_t)c * D + k0 + bk);
-          v0 = p[0];
-          v1 = p[1];
-        }
-        Bs[bk + 0][bc] = v0.x; Bs[bk + 1][bc] = v0.y; Bs[bk + 2][bc] = v0.z; Bs[bk + 3][bc] = v0.w;
-        Bs[bk + 4][bc] = v1.x; Bs[bk + 5][bc] = v1.y; Bs[bk + 6][bc] = v1.z; Bs[bk + 7][bc] = v1.w;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int kk = 0; kk < 16; kk++) {
-        float a[4], b[8];
-#pragma unroll
-        for (int i = 0; i < 4; i++) a[i] = As[kk][ty * 4 + i];
-#pragma unroll
-        for (int j = 0; j < 8; j++) b[j] = Bs[kk][tx + 16 * j];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-          for (int j = 0; j < 8; j++) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
-      }
-      __syncthreads();
+      od[s] = __shfl_xor(bd[s], off, 64);
+      oi[s] = __shfl_xor(bi[s], off, 64);
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int m = m0 + ty * 4 + i;
-      const float q2 = m < M ? qn[m] : 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int c = c0 + tx + 16 * j;  // increasing per thread: ties keep the earlier index
-        if (c < c_end) {
-          const float d = (q2 + cn[c]) - 2.0f * acc[i][j];
-          qinsert(bd[i], bi[i], k, d, c);
-        }
-      }
-    }
+    for (int s = 0; s < QK_MAX; s++)
+      if (s < k) qinsert(bd, bi, k, od[s], oi[s]);
   }
-  // merge the 16 column-threads of every row (adjacent lanes, disjoint columns): butterfly
+  if (part == 0 && m < M) {
+    const int64_t o = ((int64_t)m * nchunk + chunk) * k;
 #pragma unroll
-  for (int off = 1; off < 16; off <<= 1) {
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      float od[QK_MAX];
-      int oi[QK_MAX];
-#pragma unroll
-      for (int s = 0; s < QK_MAX; s++) {
-        od[s] = __shfl_xor(bd[i][s], off, 64);
-        oi[s] = __shfl_xor(bi[i][s], off, 64);
+    for (int s = 0; s < QK_MAX; s++)
+      if (s < k) {
+        part_d[o + s] = bd[s];
+        part_i[o + s] = bi[s];
       }
-#pragma unroll
-      for (int s = 0; s < QK_MAX; s++)
-        if (s < k) qinsert(bd[i], bi[i], k, od[s], oi[s]);
-    }
-  }
-  if (tx == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int m = m0 + ty * 4 + i;
-      if (m >= M) continue;
-      const int64_t o = ((int64_t)m * gridDim.x + blockIdx.x) * k;
-#pragma unroll
-      for (int s = 0; s < QK_MAX; s++)
-        if (s < k) {
-          part_d[o + s] = bd[i][s];
-          part_i[o + s] = bi[i][s];
-        }
-    }
   }
 }
 
@@ -510,7 +539,7 @@ extern "C" int m3s_topk_select(const void* d_keys, int keys_f64, int64_t n, int6
 }
 
 extern "C" size_t m3s_retr_quantize_workspace_bytes(int64_t M, int64_t ncent, int64_t k) {
-  const int64_t nchunk = (ncent + 255) / 256;
+  const int64_t nchunk = (ncent + QBN - 1) / QBN;
   return (size_t)(M * nchunk * k) * (sizeof(float) + sizeof(int));
 }
 
@@ -519,16 +548,17 @@ extern "C" int m3s_retr_quantize(const float* d_Q, const float* d_qnorm2, int64_
                                  int64_t k, int32_t* d_codes, float* d_dists, void* d_workspace,
                                  void* stream) {
   if (!d_Q || !d_qnorm2 || !d_C || !d_cnorm2 || !d_codes || !d_workspace) return M3S_ERR_INVALID_ARG;
-  if (M < 0 || ncent <= 0 || D <= 0 || D % 16 || k < 1 || k > QK_MAX || k > ncent)
+  if (M < 0 || ncent <= 0 || D <= 0 || D % QBK || k < 1 || k > QK_MAX || k > ncent)
     return M3S_ERR_INVALID_ARG;
   if (M == 0) return M3S_OK;
-  const int chunk = 256;
-  const int nchunk = (int)((ncent + chunk - 1) / chunk);
+  const int nchunk = (int)((ncent + QBN - 1) / QBN);
+  const int nrb = (int)((M + QBM - 1) / QBM);
   float* pd = reinterpret_cast<float*>(d_workspace);
   int* pi = reinterpret_cast<int*>(pd + M * nchunk * k);
   hipStream_t s = m3s_stream(stream);
-  hipLaunchKernelGGL(quantize_kernel, dim3(nchunk, m3s_div_up(M, 64)), dim3(256), 0, s, d_Q,
-                     d_qnorm2, d_C, d_cnorm2, (int)M, (int)ncent, (int)D, chunk, (int)k, pd, pi);
+  hipLaunchKernelGGL(quantize_kernel, dim3((unsigned)(nchunk * nrb)), dim3(256), 0, s, d_Q,
+                     d_qnorm2, d_C, d_cnorm2, (int)M, (int)ncent, (int)D, nchunk, nrb, (int)k,
+                     pd, pi);
   hipLaunchKernelGGL(quantize_merge_kernel, dim3((unsigned)M), dim3(64), 0, s, pd, pi, nchunk,
                      (int)k, d_codes, d_dists);
   M3S_LAUNCH_CHECK();
