@@ -179,3 +179,38 @@ def tracking_problem(h=384, w=512, seed=0, noise=1e-3, valid_frac=0.95):
     valid_meas = Xk[:, 2] > 1e-6
     return dict(Xf=Xf, Xk=Xk, Qk=Qk, valid=valid, T_WCk=T_WCk, T_WCf=T_WCf, T_gt=T_gt, K=K,
                 meas_k=meas_k, valid_meas=valid_meas, h=h, w=w)
+
+
+def tracking_sequence(n=8, h=96, w=128, seed=0, noise=1e-3):
+    """A sequence with ground truth for the headless harness: one keyframe surface X_key
+    (world = keyframe camera) and n frames with GT Sim3 poses T_t (frame -> world).  Frame t's
+    pair outputs are what a perfect network would regress: Xji = T_t^-1 X_key on the keyframe
+    pixels, Xii = T_t^-1 of the surface seen with a sub-pixel image shift, descriptors from the
+    world points.  Returns (X_key [N,3], frames [dict X, C, D16, Q numpy], T_gt [n, 8])."""
+    rng = np.random.default_rng(seed)
+    K = intrinsics(h, w)
+    X_key = backproject(depth_surface(h, w, seed), K)
+    yy, xx = np.meshgrid(np.arange(h, dtype=np.float32), np.arange(w, dtype=np.float32),
+                         indexing="ij")
+    frames, T_gt = [], []
+    for t in range(n):
+        q = quat_from_axis_angle([0.3, 1.0, -0.2], 0.004 * t)
+        T = np.concatenate([[0.004 * t, -0.002 * t, 0.003 * t], q, [1.0 + 0.002 * t]])
+        T = T.astype(np.float32)
+        sx, sy = 0.5 + 0.2 * np.sin(t), -0.3 + 0.2 * np.cos(t)
+        xs, ys = np.clip(xx + sx, 0, w - 1), np.clip(yy + sy, 0, h - 1)
+        x0, y0 = np.floor(xs).astype(np.int64), np.floor(ys).astype(np.int64)
+        x1, y1 = np.minimum(x0 + 1, w - 1), np.minimum(y0 + 1, h - 1)
+        fx, fy = (xs - x0)[..., None], (ys - y0)[..., None]
+        Xw = ((1 - fx) * (1 - fy) * X_key[y0, x0] + fx * (1 - fy) * X_key[y0, x1]
+              + (1 - fx) * fy * X_key[y1, x0] + fx * fy * X_key[y1, x1]).astype(np.float32)
+        Tinv = sim3_inv(T)
+        Xii = sim3_act(Tinv, Xw.reshape(-1, 3)).reshape(h, w, 3)
+        Xii = Xii * (1.0 + noise * rng.normal(size=(h, w, 1)))
+        Xji = sim3_act(Tinv, X_key.reshape(-1, 3)).reshape(h, w, 3)
+        D = np.stack([texture_field(Xw), texture_field(X_key)]).astype(np.float16)
+        C = (1.0 + np.exp(rng.normal(1.0, 0.5, size=(2, h, w)))).astype(np.float32)
+        Q = (1.0 + np.exp(rng.normal(1.0, 0.5, size=(2, h, w)))).astype(np.float32)
+        frames.append(dict(X=np.stack([Xii, Xji]).astype(np.float32), C=C, D16=D, Q=Q))
+        T_gt.append(T)
+    return X_key.reshape(-1, 3).astype(np.float32), frames, np.stack(T_gt)
