@@ -378,7 +378,8 @@ int m3s_apply_dynamic_mask(const uint8_t* d_mask, float* d_C, float* d_Q, void* 
 
 /* Y[M][N] = (X[rows[i]][:K] - mu) W + bias (fp32; W [K][N] row-major, mu [K] and bias [N]
  * optional, rows optional = identity).  X is f32 or bf16 with row stride ldx.  Whitener
- * (mast3r/retrieval/model.py:55-76, fp64 in the reference) and the projector Linear. */
+ * (mast3r/retrieval/model.py:55-76, fp64 in the reference) and the projector Linear.
+ * K, N and ldx multiples of 4 (vector loads); f32 MFMA (exact fp32 products). */
 int m3s_retr_affine(const void* d_X, int X_is_bf16, int64_t ldx, const int64_t* d_rows,
                     const float* d_mu, const float* d_W, const float* d_bias, int64_t M,
                     int64_t N, int64_t K, float* d_Y, void* stream);

@@ -20,8 +20,12 @@
 namespace {
 
 // ---------------------------------------------------------------------------------------------
-// fp32 affine: Y[M][N] = (X[row(i)][:] - mu) * W[K][N] + bias.  64x64 tile, BK 16, 256 threads
-// each owning 4x4 outputs; X may be bf16 (encoder features) or fp32.
+// fp32 affine: Y[M][N] = (X[row(i)][:] - mu) * W[K][N] + bias on the f32 MFMA (32x32x2).
+// 64x64 tile, 4 waves of 32x32, K slices of 32 staged through LDS with the next slice
+// prefetched into registers during the MFMAs (the sizes here, M <= 768, give < 1 block per
+// CU, so latency hiding inside the block is what matters).  X may be bf16 or fp32.
+constexpr int ABK = 32, APAD = ABK + 1, ABN = 64, ABNP = ABN + 4;
+
 template <typename XT>
 __global__ __launch_bounds__(256) void affine_kernel(const XT* __restrict__ X, int64_t ldx,
                                                      const int64_t* __restrict__ rows,
@@ -29,58 +33,85 @@ __global__ __launch_bounds__(256) void affine_kernel(const XT* __restrict__ X, i
                                                      const float* __restrict__ W,
                                                      const float* __restrict__ bias, int M, int N,
                                                      int K, float* __restrict__ Y) {
-  __shared__ float As[16][64 + 4];
-  __shared__ float Bs[16][64];
-  const int tid = threadIdx.x;
-  const int tx = tid & 15, ty = tid >> 4;
-  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  float acc[4][4] = {};
-  // A tile load: 64 rows x 16 k -> 4 per thread (row = tid/4, k = (tid%4)*4 ..+3)
-  const int ar = tid >> 2, ak = (tid & 3) * 4;
-  const int grow = m0 + ar;
-  int64_t src = -1;
-  if (grow < M) src = rows ? rows[grow] : grow;
-  // B tile load: 16 k x 64 n -> 4 per thread (k = tid/16, n = (tid%16)*4)
-  const int bk = tid >> 4, bn = (tid & 15) * 4;
-  for (int k0 = 0; k0 < K; k0 += 16) {
+  __shared__ float As[64 * APAD];
+  __shared__ float Bs[ABK * ABNP];
+  typedef float f32x16_t __attribute__((ext_vector_type(16)));
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * ABN;
+  f32x16_t acc;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int k = k0 + ak + j;
-      float v = 0.f;
-      if (src >= 0 && k < K) {
-        v = (float)X[src * ldx + k];
-        if (mu) v = v - mu[k];
+  for (int r = 0; r < 16; r++) acc[r] = 0.f;
+  // A: 64 rows x 32 k = 512 float4 (2 per thread, f = tid + 256u: row f>>3, k (f&7)*4)
+  // B: 32 k x 64 n = 512 float4 (2 per thread, f: k f>>4, n (f&15)*4)
+  int64_t src[2];
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    const int r = m0 + ((tid + u * 256) >> 3);
+    src[u] = r < M ? (rows ? rows[r] : r) : -1;
+  }
+  float4 ra[2], rb[2];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int f = tid + u * 256;
+      const int k = k0 + (f & 7) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (src[u] >= 0 && k < K) {
+        if constexpr (sizeof(XT) == 2) {
+          const uint2 q = *reinterpret_cast<const uint2*>(X + src[u] * ldx + k);
+          v = make_float4(__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                          __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u));
+        } else {
+          v = *reinterpret_cast<const float4*>(X + src[u] * ldx + k);
+        }
+        if (mu) {
+          const float4 mm = *reinterpret_cast<const float4*>(mu + k);
+          v.x = v.x - mm.x; v.y = v.y - mm.y; v.z = v.z - mm.z; v.w = v.w - mm.w;
+        }
       }
-      As[ak + j][ar] = v;
+      ra[u] = v;
+      const int kb = k0 + (f >> 4), n = n0 + (f & 15) * 4;
+      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (kb < K) {
+        if (n + 3 < N) {
+          w = *reinterpret_cast<const float4*>(W + (int64_t)kb * N + n);
+        } else {
+          const float* wp = W + (int64_t)kb * N;
+          w.x = n < N ? wp[n] : 0.f;
+          w.y = n + 1 < N ? wp[n + 1] : 0.f;
+          w.z = n + 2 < N ? wp[n + 2] : 0.f;
+        }
+      }
+      rb[u] = w;
     }
+  };
+  fetch(0);
+  const float* ap = As + (wm * 32 + (lane & 31)) * APAD + (lane >> 5);
+  const float* bp = Bs + (lane >> 5) * ABNP + wn * 32 + (lane & 31);
+  for (int k0 = 0; k0 < K; k0 += ABK) {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int k = k0 + bk, n = n0 + bn + j;
-      Bs[bk][bn + j] = (k < K && n < N) ? W[(int64_t)k * N + n] : 0.f;
+    for (int u = 0; u < 2; u++) {
+      const int f = tid + u * 256;
+      float* d = As + (f >> 3) * APAD + (f & 7) * 4;
+      d[0] = ra[u].x; d[1] = ra[u].y; d[2] = ra[u].z; d[3] = ra[u].w;
+      float* e = Bs + (f >> 4) * ABNP + (f & 15) * 4;
+      e[0] = rb[u].x; e[1] = rb[u].y; e[2] = rb[u].z; e[3] = rb[u].w;
     }
     __syncthreads();
+    if (k0 + ABK < K) fetch(k0 + ABK);
 #pragma unroll
-    for (int kk = 0; kk < 16; kk++) {
-      float a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) a[i] = As[kk][ty * 4 + i];
-#pragma unroll
-      for (int j = 0; j < 4; j++) b[j] = Bs[kk][tx + 16 * j];
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
-    }
+    for (int kk = 0; kk < ABK; kk += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[kk], bp[kk * ABNP], acc, 0, 0, 0);
     __syncthreads();
   }
+  const int col = n0 + wn * 32 + (lane & 31);
+  if (col < N) {
+    const float bb = bias ? bias[col] : 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int m = m0 + ty * 4 + i;
-    if (m >= M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int n = n0 + tx + 16 * j;
-      if (n < N) Y[(int64_t)m * N + n] = acc[i][j] + (bias ? bias[n] : 0.f);
+    for (int r = 0; r < 16; r++) {
+      const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < M) Y[(int64_t)row * N + col] = acc[r] + bb;
     }
   }
 }
@@ -320,17 +351,17 @@ __global__ __launch_bounds__(256, 2) void quantize_kernel(const float* __restric
   }
 }
 
-// One 64-thread block per query row: merge the chunk partials into the final k codes.
+// One 64-thread block (one wave) per query row: each lane merges a strided subset of the chunk
+// partials, then a 6-step butterfly over the wave (lanes hold disjoint candidate sets).
 __global__ __launch_bounds__(64) void quantize_merge_kernel(const float* __restrict__ part_d,
                                                             const int* __restrict__ part_i,
                                                             int nchunk, int k,
                                                             int32_t* __restrict__ codes,
                                                             float* __restrict__ dists) {
-  __shared__ float sd[64 * QK_MAX];
-  __shared__ int si[64 * QK_MAX];
   const int m = blockIdx.x, t = threadIdx.x;
   float rd[QK_MAX];
   int ri[QK_MAX];
+#pragma unroll
   for (int s = 0; s < QK_MAX; s++) {
     rd[s] = INFINITY;
     ri[s] = 0x7fffffff;
@@ -338,18 +369,26 @@ __global__ __launch_bounds__(64) void quantize_merge_kernel(const float* __restr
   const int64_t base = (int64_t)m * nchunk * k;
   for (int c = t; c < nchunk; c += 64)
     for (int s = 0; s < k; s++) qinsert(rd, ri, k, part_d[base + c * k + s], part_i[base + c * k + s]);
-  for (int s = 0; s < k; s++) {
-    sd[t * QK_MAX + s] = rd[s];
-    si[t * QK_MAX + s] = ri[s];
-  }
-  __syncthreads();
-  if (t == 0) {
-    for (int u = 1; u < 64; u++)
-      for (int s = 0; s < k; s++) qinsert(rd, ri, k, sd[u * QK_MAX + s], si[u * QK_MAX + s]);
-    for (int s = 0; s < k; s++) {
-      codes[(int64_t)m * k + s] = ri[s];
-      if (dists) dists[(int64_t)m * k + s] = rd[s];
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    float od[QK_MAX];
+    int oi[QK_MAX];
+#pragma unroll
+    for (int s = 0; s < QK_MAX; s++) {
+      od[s] = __shfl_xor(rd[s], off, 64);
+      oi[s] = __shfl_xor(ri[s], off, 64);
     }
+#pragma unroll
+    for (int s = 0; s < QK_MAX; s++)
+      if (s < k) qinsert(rd, ri, k, od[s], oi[s]);
+  }
+  if (t == 0) {
+#pragma unroll
+    for (int s = 0; s < QK_MAX; s++)
+      if (s < k) {
+        codes[(int64_t)m * k + s] = ri[s];
+        if (dists) dists[(int64_t)m * k + s] = rd[s];
+      }
   }
 }
 
@@ -363,38 +402,59 @@ __global__ __launch_bounds__(256) void mark_words_kernel(const int32_t* __restri
   if (i < n) flags[codes[i]] = 1;
 }
 
-// One workgroup: ordered compaction of the flag array -> sorted unique words + count; clears
-// the flags it read so the workspace is ready for the next call.
+// One workgroup of 16 waves: ordered compaction of the flag array -> sorted unique words +
+// count; wave w owns a contiguous range, lane l four consecutive flags per step (int4).
+// Pass 1 counts per wave, pass 2 writes at wave offset + lane prefix.  Clears the flags.
 __global__ __launch_bounds__(1024) void compact_words_kernel(int32_t* __restrict__ flags, int NC,
                                                              int32_t* __restrict__ words,
                                                              int32_t* __restrict__ count) {
-  __shared__ int wsum[16];
-  __shared__ int base;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t == 0) base = 0;
-  __syncthreads();
-  for (int c0 = 0; c0 < NC; c0 += 1024) {
-    const int c = c0 + t;
-    const int f = c < NC ? flags[c] : 0;
-    const uint64_t b = __ballot(f);
-    const int pre = __popcll(b & ((1ull << lane) - 1ull));
-    if (lane == 0) wsum[w] = __popcll(b);
-    __syncthreads();
-    int off = base;
-    for (int u = 0; u < w; u++) off += wsum[u];
-    if (f) {
-      words[off + pre] = c;
-      flags[c] = 0;
+  __shared__ int wtot[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int per = ((NC + 16 * 256 - 1) / (16 * 256)) * 256;  // multiple of 256 flags per wave
+  const int b0 = w * per, b1 = min(NC, b0 + per);
+  auto load4 = [&](int i) {
+    int4 v = make_int4(0, 0, 0, 0);
+    if (i + 3 < b1) {
+      v = *reinterpret_cast<const int4*>(flags + i);
+    } else {
+      v.x = i < b1 ? flags[i] : 0;
+      v.y = i + 1 < b1 ? flags[i + 1] : 0;
+      v.z = i + 2 < b1 ? flags[i + 2] : 0;
     }
-    __syncthreads();
-    if (t == 0) {
-      int s = 0;
-      for (int u = 0; u < 16; u++) s += wsum[u];
-      base += s;
-    }
-    __syncthreads();
+    return v;
+  };
+  int cnt = 0;
+  for (int i0 = b0; i0 < b1; i0 += 256) {
+    const int4 v = load4(i0 + lane * 4);
+    cnt += (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
   }
-  if (t == 0) *count = base;
+  cnt = m3s_wave_sum_int(cnt);
+  if (lane == 0) wtot[w] = cnt;
+  __syncthreads();
+  int off = 0;
+  for (int u = 0; u < w; u++) off += wtot[u];
+  for (int i0 = b0; i0 < b1; i0 += 256) {
+    const int i = i0 + lane * 4;
+    const int4 v = load4(i);
+    const int c = (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
+    int incl = c;  // inclusive prefix over lanes
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int t = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += t;
+    }
+    int p = off + incl - c;
+    if (v.x) { words[p++] = i; flags[i] = 0; }
+    if (v.y) { words[p++] = i + 1; flags[i + 1] = 0; }
+    if (v.z) { words[p++] = i + 2; flags[i + 2] = 0; }
+    if (v.w) { words[p++] = i + 3; flags[i + 3] = 0; }
+    off += __shfl(incl, 63, 64);
+  }
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int u = 0; u < 16; u++) s += wtot[u];
+    *count = s;
+  }
 }
 
 // One workgroup per unique word (blocks past the count exit): thread t owns elements
@@ -409,13 +469,29 @@ __global__ __launch_bounds__(256) void aggregate_kernel(const float* __restrict_
   if (u >= *count) return;
   const int word = words[u];
   const int W32 = D / 32;
+  // ordered list of the member descriptors (ballot compaction keeps index order)
   extern __shared__ int member[];
-  for (int i = threadIdx.x; i < n; i += 256) {
-    int hit = 0;
-    for (int s = 0; s < k; s++) hit |= codes[(int64_t)i * k + s] == word;
-    member[i] = hit;
-  }
+  __shared__ int wcnt[4];
+  __shared__ int nmem;
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  if (threadIdx.x == 0) nmem = 0;
   __syncthreads();
+  for (int i0 = 0; i0 < n; i0 += 256) {
+    const int i = i0 + threadIdx.x;
+    int hit = 0;
+    if (i < n)
+      for (int s = 0; s < k; s++) hit |= codes[(int64_t)i * k + s] == word;
+    const uint64_t b = __ballot(hit);
+    if (ln == 0) wcnt[wv] = __popcll(b);
+    __syncthreads();
+    int off = nmem;
+    for (int w = 0; w < wv; w++) off += wcnt[w];
+    if (hit) member[off + __popcll(b & ((1ull << ln) - 1ull))] = i;
+    __syncthreads();
+    if (threadIdx.x == 0) nmem += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    __syncthreads();
+  }
+  const int nm = nmem;
   const float* c = C + (int64_t)word * D;
   const int lane = threadIdx.x & 63;
   for (int e0 = 0; e0 < D; e0 += 256) {
@@ -423,8 +499,7 @@ __global__ __launch_bounds__(256) void aggregate_kernel(const float* __restrict_
     float acc = 0.f;
     if (e < D) {
       const float ce = c[e];
-      for (int i = 0; i < n; i++)
-        if (member[i]) acc = acc + (des[(int64_t)i * D + e] - ce);
+      for (int j = 0; j < nm; j++) acc = acc + (des[(int64_t)member[j] * D + e] - ce);
     }
     const uint64_t b = __ballot(e < D && acc > 0.f);
     // elements e0 + wave*64 + [0,32) -> word (e0 + wave*64)/32, [32,64) -> the next
@@ -495,9 +570,10 @@ __global__ __launch_bounds__(256) void ivf_score_kernel(
 extern "C" int m3s_retr_affine(const void* d_X, int X_is_bf16, int64_t ldx, const int64_t* d_rows,
                                const float* d_mu, const float* d_W, const float* d_bias, int64_t M,
                                int64_t N, int64_t K, float* d_Y, void* stream) {
-  if (!d_X || !d_W || !d_Y || M < 0 || N <= 0 || K <= 0 || ldx < K) return M3S_ERR_INVALID_ARG;
+  if (!d_X || !d_W || !d_Y || M < 0 || N <= 0 || K <= 0 || ldx < K || K % 4 || ldx % 4 || N % 4)
+    return M3S_ERR_INVALID_ARG;
   if (M == 0) return M3S_OK;
-  dim3 grid(m3s_div_up(N, 64), m3s_div_up(M, 64));
+  dim3 grid(m3s_div_up(N, ABN), m3s_div_up(M, 64));
   hipStream_t s = m3s_stream(stream);
   if (X_is_bf16)
     hipLaunchKernelGGL((affine_kernel<__bf16>), grid, dim3(256), 0, s,
