@@ -144,21 +144,24 @@ __global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__
 }
 
 // ---- bilinear x2, align_corners=True (torch upsample_bilinear2d formula) -------------
+// IT: index type — 32-bit whenever the element count allows (the 64-bit div/mod of the
+// index decomposition otherwise costs more than the memory traffic).
+template <typename IT>
 __global__ __launch_bounds__(256) void upsample2x_kernel(const bf16_t* __restrict__ in,
                                                          bf16_t* __restrict__ out,
                                                          const bf16_t* __restrict__ addend,
                                                          int h, int w, int c, int oh, int ow,
-                                                         int64_t total) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                         IT total) {
+  const IT idx = (IT)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
-  const int c8 = c / 8;
+  const IT c8 = (IT)(c / 8);
   const int cc = (int)(idx % c8) * 8;
-  int64_t t = idx / c8;
+  IT t = idx / c8;
   const int H2 = 2 * h, W2 = 2 * w;  // interpolation grid; the output keeps [0,oh)x[0,ow)
-  const int ox = (int)(t % ow);
-  t /= ow;
-  const int oy = (int)(t % oh);
-  const int64_t b = t / oh;
+  const int ox = (int)(t % (IT)ow);
+  t /= (IT)ow;
+  const int oy = (int)(t % (IT)oh);
+  const int64_t b = (int64_t)(t / (IT)oh);
   const float sh = H2 > 1 ? (float)(h - 1) / (float)(H2 - 1) : 0.f;
   const float sw = W2 > 1 ? (float)(w - 1) / (float)(W2 - 1) : 0.f;
   const float fy = sh * (float)oy, fx = sw * (float)ox;
@@ -341,10 +344,16 @@ extern "C" int m3s_vit_upsample2x(const void* d_in, void* d_out, const void* d_a
   if (!d_in || !d_out || batch <= 0 || h <= 0 || w <= 0 || c % 8) return M3S_ERR_INVALID_ARG;
   if (oh <= 0 || ow <= 0 || oh > 2 * h || ow > 2 * w) return M3S_ERR_INVALID_ARG;
   const int64_t total = batch * oh * ow * (c / 8);
-  hipLaunchKernelGGL(upsample2x_kernel, dim3(m3s_div_up(total, 256)), dim3(256), 0,
-                     m3s_stream(stream), reinterpret_cast<const bf16_t*>(d_in),
-                     reinterpret_cast<bf16_t*>(d_out), reinterpret_cast<const bf16_t*>(d_add),
-                     (int)h, (int)w, (int)c, (int)oh, (int)ow, total);
+  if (total < (int64_t(1) << 31) - 256)
+    hipLaunchKernelGGL(upsample2x_kernel<uint32_t>, dim3(m3s_div_up(total, 256)), dim3(256), 0,
+                       m3s_stream(stream), reinterpret_cast<const bf16_t*>(d_in),
+                       reinterpret_cast<bf16_t*>(d_out), reinterpret_cast<const bf16_t*>(d_add),
+                       (int)h, (int)w, (int)c, (int)oh, (int)ow, (uint32_t)total);
+  else
+    hipLaunchKernelGGL(upsample2x_kernel<int64_t>, dim3(m3s_div_up(total, 256)), dim3(256), 0,
+                       m3s_stream(stream), reinterpret_cast<const bf16_t*>(d_in),
+                       reinterpret_cast<bf16_t*>(d_out), reinterpret_cast<const bf16_t*>(d_add),
+                       (int)h, (int)w, (int)c, (int)oh, (int)ow, total);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }
