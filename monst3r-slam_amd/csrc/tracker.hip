@@ -20,6 +20,7 @@ constexpr int kThreads = 256;
 constexpr int kBlocks = 512;
 constexpr int kPersistentBlocks = 256;  // one per CU: co-resident next to other kernels
 constexpr int kAcc = 36;  // 28 H upper, 7 g, 1 cost
+static_assert(kAcc % 4 == 0, "partial rows are read as float4");
 
 enum : int { TRACK_RAYS = 0, TRACK_CALIB = 1 };
 
@@ -238,17 +239,33 @@ __global__ __launch_bounds__(kThreads) void track_iter_kernel(
 __device__ void reduce_partials(const float* partial, int nblocks, double* sacc) {
   const int tid = threadIdx.x;
   __shared__ double tmp[kThreads / M3S_WAVE][kAcc];
+  // all 36 values of a partial row are loaded before any reduction (one round of L2
+  // latency instead of 36); per-l summation order unchanged: rows b = tid, tid + 256, ...,
+  // then the wave butterfly, then the waves in order
+  double v[kAcc];
+#pragma unroll
+  for (int l = 0; l < kAcc; l++) v[l] = 0.0;
+  for (int b = tid; b < nblocks; b += kThreads) {
+    float r[kAcc];
+    const float4* row = reinterpret_cast<const float4*>(partial + (size_t)b * kAcc);
+#pragma unroll
+    for (int q = 0; q < kAcc / 4; q++) {
+      const float4 f = row[q];
+      r[4 * q] = f.x; r[4 * q + 1] = f.y; r[4 * q + 2] = f.z; r[4 * q + 3] = f.w;
+    }
+#pragma unroll
+    for (int l = 0; l < kAcc; l++) v[l] += (double)r[l];
+  }
+#pragma unroll
   for (int l = 0; l < kAcc; l++) {
-    double v = 0.0;
-    for (int b = tid; b < nblocks; b += kThreads) v += (double)partial[b * kAcc + l];
-    v = m3s_wave_sum_d(v);
-    if ((tid & 63) == 0) tmp[tid >> 6][l] = v;
+    const double t = m3s_wave_sum_d(v[l]);
+    if ((tid & 63) == 0) tmp[tid >> 6][l] = t;
   }
   __syncthreads();
   if (tid < kAcc) {
-    double v = 0.0;
-    for (int w = 0; w < kThreads / M3S_WAVE; w++) v += tmp[w][tid];
-    sacc[tid] = v;
+    double t = 0.0;
+    for (int w = 0; w < kThreads / M3S_WAVE; w++) t += tmp[w][tid];
+    sacc[tid] = t;
   }
   __syncthreads();
 }
