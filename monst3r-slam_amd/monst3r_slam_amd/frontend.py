@@ -47,7 +47,9 @@ class Tracker:
         self.cfg = cfg or _config
         self.idx_f2k = None
         self.kf = None
-        self.split_heads = False   # measured: no gain
+        # MASt3R heads on a side stream (local features first): +3 % frames/s in the
+        # prefetched pipeline (profiles/r01_ab_lfside_glue.txt); bench.py turns it on
+        self.split_heads = False
         # the glue around the pose solve as 3 fused kernels (csrc/glue.hip) instead of the
         # torch restatement below (~25 small launches)
         self.fused_glue = os.environ.get("M3S_FUSED_GLUE", "1") != "0"
