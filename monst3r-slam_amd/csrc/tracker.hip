@@ -10,7 +10,11 @@
 // Default: all iterations in one persistent launch (track_persistent_kernel, grid
 // barrier per iteration, every workgroup takes the same step); M3S_TRACK_PERSISTENT=0
 // enqueues one launch per iteration instead (the remaining ones return at entry once
-// the done flag is set).
+// the done flag is set).  If the persistent launch loses co-residency (a barrier wait
+// times out because not all of its workgroups got a CU next to the concurrently running
+// kernels) it stops with a consistent state (pose after the last completed iteration) and
+// the finish launch runs the remaining iterations in one 1024-thread workgroup; info[3]
+// reports it.  A timeout is never a Cholesky failure.
 #include "common.h"
 #include "sim3.h"
 
@@ -29,6 +33,8 @@ struct TrackState {
   double old_cost;
   int done, fail, iters, conv;
   unsigned ticket;   // workgroups of the current iteration that have published partials
+  int abort;         // persistent launch: a barrier wait timed out (co-residency lost)
+  int recovered;     // iterations the finish launch ran after an aborted persistent launch
 };
 
 struct TrackParams {
@@ -89,6 +95,8 @@ __global__ void track_init_kernel(const float* __restrict__ Twc_k, const float* 
   st->iters = 0;
   st->conv = 0;
   st->ticket = 0;
+  st->abort = 0;
+  st->recovered = 0;
 }
 
 __device__ void track_solve(TrackState* st, const float* partial, int nblocks, float rel_error,
@@ -103,9 +111,8 @@ __device__ __forceinline__ void track_points(const float* T, const TrackParams& 
                                              const uint8_t* __restrict__ valid,
                                              const float* __restrict__ meas_k,
                                              const uint8_t* __restrict__ valid_meas, int64_t n,
-                                             float* acc) {
-  for (int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x; k < n;
-       k += (int64_t)gridDim.x * kThreads) {
+                                             float* acc, int64_t first, int64_t stride) {
+  for (int64_t k = first; k < n; k += stride) {
     const float X[3] = {Xf[3 * k], Xf[3 * k + 1], Xf[3 * k + 2]};
     float P[3];
     m3s_act_sim3<float>(T, T + 3, T[7], X, P);
@@ -173,8 +180,9 @@ __device__ __forceinline__ void track_points(const float* T, const TrackParams& 
 }
 
 // wave butterfly + LDS: the workgroup's 36 sums → out[0..35] (threads < kAcc write)
+template <int NT>
 __device__ __forceinline__ void block_partial(const float* acc, float* out) {
-  __shared__ float red[kThreads / M3S_WAVE][kAcc];
+  __shared__ float red[NT / M3S_WAVE][kAcc];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
   for (int l = 0; l < kAcc; l++) {
@@ -185,7 +193,7 @@ __device__ __forceinline__ void block_partial(const float* acc, float* out) {
   if (threadIdx.x < kAcc) {
     float v = red[0][threadIdx.x];
 #pragma unroll
-    for (int w = 1; w < kThreads / M3S_WAVE; w++) v += red[w][threadIdx.x];
+    for (int w = 1; w < NT / M3S_WAVE; w++) v += red[w][threadIdx.x];
     out[threadIdx.x] = v;
   }
 }
@@ -211,8 +219,9 @@ __global__ __launch_bounds__(kThreads) void track_iter_kernel(
 #pragma unroll
   for (int l = 0; l < kAcc; l++) acc[l] = 0.f;
 
-  track_points<MODE>(T, prm, Xf, Xk, Qk, valid, meas_k, valid_meas, n, acc);
-  block_partial(acc, partial + blockIdx.x * kAcc);
+  track_points<MODE>(T, prm, Xf, Xk, Qk, valid, meas_k, valid_meas, n, acc,
+                     (int64_t)blockIdx.x * kThreads + threadIdx.x, (int64_t)gridDim.x * kThreads);
+  block_partial<kThreads>(acc, partial + blockIdx.x * kAcc);
   // publish this workgroup's partial row; the last to arrive reduces and solves
   __shared__ unsigned s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -354,15 +363,20 @@ __device__ void track_solve(TrackState* st, const float* partial, int nblocks, f
 // workgroup reduces the same partials in the same order and takes the same step — the
 // pose never needs a broadcast and the next iteration starts straight away.  Partials
 // are double-buffered by iteration parity (a workgroup can be at most one barrier ahead).
-// Exit: convergence, Cholesky failure, max_iters, or a barrier wait beyond ~0.2 s
-// (st->fail = 3: co-residency broken), reached by every wave.
+// Exit: convergence, Cholesky failure, max_iters, or a barrier wait beyond `spin_limit`
+// polls (~0.27 s at the default 2^22; co-residency broken) — that workgroup raises
+// st->abort, every other workgroup sees it in its own wait (or at entry, if it only got a
+// CU after the others left) and leaves too.  No workgroup can pass the barrier that timed
+// out, so workgroup 0 still holds the pose after the last completed iteration and writes
+// it back with done = 0; track_finish_kernel then runs the remaining iterations.
+// `abort_at` >= 0 forces that exit at iteration abort_at (tests of the recovery path).
 template <int MODE>
 __global__ __launch_bounds__(kThreads) void track_persistent_kernel(
     TrackState* __restrict__ st, TrackParams prm, const float* __restrict__ K,
     const float* __restrict__ Xf, const float* __restrict__ Xk, const float* __restrict__ Qk,
     const uint8_t* __restrict__ valid, const float* __restrict__ meas_k,
     const uint8_t* __restrict__ valid_meas, int64_t n, float* __restrict__ partial,
-    int max_iters, float rel_error, float delta_norm) {
+    int max_iters, float rel_error, float delta_norm, long spin_limit, int abort_at) {
   if (MODE == TRACK_CALIB) {
     prm.fx = K[0];
     prm.fy = K[4];
@@ -379,28 +393,39 @@ __global__ __launch_bounds__(kThreads) void track_persistent_kernel(
   for (int i = 0; i < 8; i++) T[i] = st->T[i];
   double old_cost = st->old_cost;
   int it = 0, status = 0;
+  if (threadIdx.x == 0)
+    s_status = __hip_atomic_load(&st->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 3 : 0;
+  __syncthreads();
+  if (s_status == 3) return;  // started after the others gave up: nothing to contribute
   for (; it < max_iters; it++) {
     float acc[kAcc];
 #pragma unroll
     for (int l = 0; l < kAcc; l++) acc[l] = 0.f;
-    track_points<MODE>(T, prm, Xf, Xk, Qk, valid, meas_k, valid_meas, n, acc);
+    track_points<MODE>(T, prm, Xf, Xk, Qk, valid, meas_k, valid_meas, n, acc,
+                       (int64_t)blockIdx.x * kThreads + threadIdx.x, (int64_t)nb * kThreads);
     float* slot = partial + (size_t)(it & 1) * nb * kAcc;
-    block_partial(acc, slot + blockIdx.x * kAcc);
+    block_partial<kThreads>(acc, slot + blockIdx.x * kAcc);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned target = (unsigned)(it + 1) * (unsigned)nb;
-      int timeout = 0;
-      for (long spins = 0;
-           __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; spins++) {
-        __builtin_amdgcn_s_sleep(2);
-        if (spins > (1l << 22)) {
-          timeout = 1;
-          break;
+      int timeout = it == abort_at;
+      if (!timeout) {
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = (unsigned)(it + 1) * (unsigned)nb;
+        for (long spins = 0;
+             __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;
+             spins++) {
+          __builtin_amdgcn_s_sleep(2);
+          if (spins > spin_limit ||
+              __hip_atomic_load(&st->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            timeout = 1;
+            break;
+          }
         }
       }
+      if (timeout)
+        __hip_atomic_store(&st->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_status = timeout ? 3 : 0;
     }
     __syncthreads();
@@ -430,15 +455,82 @@ __global__ __launch_bounds__(kThreads) void track_persistent_kernel(
     for (int i = 0; i < 8; i++) st->T[i] = T[i];
     st->old_cost = old_cost;
     st->iters = it;
-    st->fail = status == 3 ? 3 : (status == 2 ? 1 : 0);
+    st->fail = status == 2 ? 1 : 0;
     st->conv = status == 1 ? 1 : 0;
-    st->done = 1;
+    st->done = status == 3 ? 0 : 1;  // aborted: track_finish_kernel continues from here
   }
 }
 
-__global__ void track_finish_kernel(const float* __restrict__ Twc_k, const TrackState* st,
-                                    float* __restrict__ T_WCf, float* __restrict__ T_CkCf,
-                                    int* __restrict__ info) {
+constexpr int kFinishThreads = 1024;
+
+// Outputs T_WCf / T_CkCf / info.  If the iterations did not finish (persistent launch
+// aborted, st->done == 0 with iterations left) this single workgroup runs the rest: same
+// residuals and step, the points' sums in one 1024-thread partial (fp32 rounding differs
+// from the multi-workgroup order, as between the two launch modes).
+template <int MODE>
+__global__ __launch_bounds__(kFinishThreads) void track_finish_kernel(
+    const float* __restrict__ Twc_k, TrackState* st, TrackParams prm, const float* __restrict__ K,
+    const float* __restrict__ Xf, const float* __restrict__ Xk, const float* __restrict__ Qk,
+    const uint8_t* __restrict__ valid, const float* __restrict__ meas_k,
+    const uint8_t* __restrict__ valid_meas, int64_t n, int max_iters, float rel_error,
+    float delta_norm, float* __restrict__ T_WCf, float* __restrict__ T_CkCf,
+    int* __restrict__ info) {
+  __shared__ float srow[kAcc];
+  __shared__ double sacc[kAcc];
+  __shared__ float sT[8];
+  __shared__ int s_go;
+  if (threadIdx.x == 0) {
+    s_go = !st->done && st->iters < max_iters;
+    for (int i = 0; i < 8; i++) sT[i] = st->T[i];
+  }
+  __syncthreads();
+  if (s_go) {
+    if (MODE == TRACK_CALIB) {
+      prm.fx = K[0];
+      prm.fy = K[4];
+      prm.cx = K[2];
+      prm.cy = K[5];
+    }
+    int it = st->iters, status = 0, ran = 0;
+    double old_cost = st->old_cost;
+    for (; it < max_iters; it++) {
+      float T[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) T[i] = sT[i];
+      float acc[kAcc];
+#pragma unroll
+      for (int l = 0; l < kAcc; l++) acc[l] = 0.f;
+      track_points<MODE>(T, prm, Xf, Xk, Qk, valid, meas_k, valid_meas, n, acc, threadIdx.x,
+                         kFinishThreads);
+      block_partial<kFinishThreads>(acc, srow);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        for (int l = 0; l < kAcc; l++) sacc[l] = (double)srow[l];
+        status = gn_step(sacc, T, &old_cost, rel_error, delta_norm);
+        if (status != 2)
+          for (int i = 0; i < 8; i++) sT[i] = T[i];
+        s_go = status;
+      }
+      __syncthreads();
+      status = s_go;
+      ran++;
+      if (status == 2) break;
+      if (status == 1) {
+        it++;
+        break;
+      }
+    }
+    if (threadIdx.x == 0) {
+      for (int i = 0; i < 8; i++) st->T[i] = sT[i];
+      st->old_cost = old_cost;
+      st->iters = it;
+      st->fail = status == 2 ? 1 : 0;
+      st->conv = status == 1 ? 1 : 0;
+      st->recovered = ran;
+      st->done = 1;
+    }
+    __syncthreads();
+  }
   if (threadIdx.x != 0) return;
   // T_WCf = T_WCk * T_CkCf: q = qk*q, s = sk*s, t = tk + sk * Rk t
   const float* Tk = Twc_k;
@@ -452,7 +544,7 @@ __global__ void track_finish_kernel(const float* __restrict__ Twc_k, const Track
   info[0] = st->iters;
   info[1] = st->fail;
   info[2] = st->conv;
-  info[3] = 0;
+  info[3] = st->recovered;
 }
 
 struct Layout {
@@ -487,10 +579,17 @@ int run_track(const float* Twc_k, const float* Twc_f, const float* Xf, const flo
   if (!e || atoi(e) != 0) {
     int nb = (int)((n + kThreads - 1) / kThreads);
     if (nb > kPersistentBlocks) nb = kPersistentBlocks;
+    // debug knobs for the co-residency recovery path (tests): barrier poll limit, forced
+    // abort at a given iteration
+    const char* sl = getenv("M3S_TRACK_SPIN_LIMIT");
+    const long spin_limit = sl ? atol(sl) : (1l << 22);
+    const char* ab = getenv("M3S_TRACK_ABORT_AT");
+    const int abort_at = ab ? atoi(ab) : -1;
     if (max_iters > 0)
       hipLaunchKernelGGL(track_persistent_kernel<MODE>, dim3(nb), dim3(kThreads), 0, s, st, prm,
                          K, Xf, Xk, Qk, valid, meas_k, valid_meas, n, partial, max_iters,
-                         rel_error, delta_norm);
+                         rel_error, delta_norm, spin_limit, abort_at);
+    M3S_LAUNCH_CHECK();
   } else {
     int nb = (int)((n + kThreads - 1) / kThreads);
     if (nb > kBlocks) nb = kBlocks;
@@ -501,8 +600,9 @@ int run_track(const float* Twc_k, const float* Twc_f, const float* Xf, const flo
       M3S_LAUNCH_CHECK();
     }
   }
-  hipLaunchKernelGGL(track_finish_kernel, dim3(1), dim3(64), 0, s, Twc_k, st, T_WCf, T_CkCf,
-                     info);
+  hipLaunchKernelGGL(track_finish_kernel<MODE>, dim3(1), dim3(kFinishThreads), 0, s, Twc_k, st,
+                     prm, K, Xf, Xk, Qk, valid, meas_k, valid_meas, n, max_iters, rel_error,
+                     delta_norm, T_WCf, T_CkCf, info);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }

@@ -2,7 +2,7 @@
 opt_pose_calib_sim3 (tracker2.py:316-409) on the fused HIP tracker kernels
 (m3s_track_rays / m3s_track_calib).  Poses are lietorch Sim3 data tensors [8]
 (t xyz, q xyzw, s).  Returns (T_WCf, T_CkCf, info) with info = [iters, chol_failed,
-converged, 0]; a failed Cholesky raises CholeskyError like torch.linalg.cholesky does
+converged, recovered]; a failed Cholesky raises CholeskyError like torch.linalg.cholesky does
 (tracker2.py:234-236 catches it and reports the frame lost)."""
 from __future__ import annotations
 

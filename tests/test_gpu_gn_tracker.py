@@ -93,8 +93,24 @@ def test_gn_global_ids_parity(oracle, dev):
     np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=POSE_TOL, rtol=0)
 
 
+# launch modes of the GN: persistent (default), one launch per iteration, and the
+# persistent launch forced to abort at its 2nd barrier (co-residency lost) with the
+# remaining iterations run by the recovery path of the finish launch
+LAUNCH_MODES = {"persistent": {}, "per_iteration": {"M3S_TRACK_PERSISTENT": "0"},
+                "recovered": {"M3S_TRACK_ABORT_AT": "1"}}
+
+
+def _launch_mode(monkeypatch, mode):
+    for k in ("M3S_TRACK_PERSISTENT", "M3S_TRACK_ABORT_AT", "M3S_TRACK_SPIN_LIMIT"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in LAUNCH_MODES[mode].items():
+        monkeypatch.setenv(k, v)
+
+
+@pytest.mark.parametrize("mode", list(LAUNCH_MODES))
 @pytest.mark.parametrize("h,w", [(384, 512), (96, 128)])
-def test_tracker_rays_parity(dev, h, w):
+def test_tracker_rays_parity(dev, h, w, mode, monkeypatch):
+    _launch_mode(monkeypatch, mode)
     from oracle import tracker_ref as tr
     from monst3r_slam_amd import tracker as T
     p = syn.tracking_problem(h, w, seed=1)
@@ -107,9 +123,16 @@ def test_tracker_rays_parity(dev, h, w):
     np.testing.assert_allclose(Trel.cpu().numpy(), Trel_ref, atol=TRACK_TOL, rtol=0)
     np.testing.assert_allclose(Tf.cpu().numpy(), Tf_ref, atol=TRACK_TOL, rtol=0)
     assert abs(int(info[0]) - it_ref) <= 1
+    assert int(info[1]) == 0
+    if mode == "recovered":
+        assert int(info[3]) >= 1, "the forced abort must be recovered by the finish launch"
+    else:
+        assert int(info[3]) == 0
 
 
-def test_tracker_calib_parity(dev):
+@pytest.mark.parametrize("mode", list(LAUNCH_MODES))
+def test_tracker_calib_parity(dev, mode, monkeypatch):
+    _launch_mode(monkeypatch, mode)
     from oracle import tracker_ref as tr
     from monst3r_slam_amd import tracker as T
     p = syn.tracking_problem(96, 128, seed=2)
@@ -123,6 +146,25 @@ def test_tracker_calib_parity(dev):
         (p["h"], p["w"]), cfg)
     np.testing.assert_allclose(Trel.cpu().numpy(), Trel_ref, atol=TRACK_TOL, rtol=0)
     assert abs(int(info[0]) - it_ref) <= 1
+    assert (int(info[3]) >= 1) == (mode == "recovered")
+
+
+def test_tracker_barrier_timeout_recovers(dev, monkeypatch):
+    """A barrier poll limit of 0 makes every persistent-launch wait that is not already
+    complete time out: whatever the interleaving, the result equals the oracle's and the
+    frame is not reported as a Cholesky failure."""
+    monkeypatch.setenv("M3S_TRACK_SPIN_LIMIT", "0")
+    from oracle import tracker_ref as tr
+    from monst3r_slam_amd import tracker as T
+    p = syn.tracking_problem(384, 512, seed=4)
+    cfg = default_config()["tracking"]
+    Tf_ref, Trel_ref, it_ref = tr.opt_pose_ray_dist_sim3(p["Xf"], p["Xk"], p["T_WCf"],
+                                                         p["T_WCk"], p["Qk"], p["valid"], cfg)
+    Tf, Trel, info = T.opt_pose_ray_dist_sim3(_t(p["Xf"], dev), _t(p["Xk"], dev),
+                                              _t(p["T_WCf"], dev), _t(p["T_WCk"], dev),
+                                              _t(p["Qk"], dev), _t(p["valid"], dev), cfg)
+    np.testing.assert_allclose(Trel.cpu().numpy(), Trel_ref, atol=TRACK_TOL, rtol=0)
+    assert int(info[1]) == 0 and abs(int(info[0]) - it_ref) <= 1
 
 
 def test_tracker_cholesky_failure_reported(dev):
