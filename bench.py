@@ -2,13 +2,22 @@
 one MI355X — BASELINE.json metric; workload configs[1]+[2] (bf16 ViT pair inference inside
 the full tracking step).
 
-One "step" = one tracked frame of the per-frame hot path, synthetic 384x512 input,
-seeded random weights (no checkpoints offline), everything resident in HBM:
-  pair inference  MonST3R encoder (new frame) + MonST3R decoder + 2 DPT heads +
-                  MASt3R decoder + 2 catmlp+DPT heads (keyframe features cached)
-  matching        prep + iter_proj + occlusion + refine_matches + linear index
+One "step" = one tracked frame of the configs[2] sequence: the main loop's TRACKING branch
+(main_monster_slam.py:247-332) over the synthetic 384x512 room sequence of
+monst3r_slam_amd.sequence (200-frame period, every frame a new image, staged in HBM before
+the timed region), seeded random weights (no checkpoints offline):
+  pair inference  MonST3R encoder (next frame, prefetched) + MonST3R decoder + 2 DPT heads +
+                  MASt3R decoder + 2 catmlp+DPT heads vs the current keyframe's cached features
+  stand-in        the scene's pair outputs replace the random-weight X/C/D/Q in stream order
+  matching        prep + iter_proj (seeded by the previous frame's matches) + occlusion +
+                  refine_matches + linear index
   tracking        glue (Qk, valid, pointmap fusion, keyframe test) + fused Sim3 GN (≤50 it)
-The step is captured once in a HIP graph and replayed (no host work per frame).
+                  from the previous frame's pose; new keyframe → the frame replaces the
+                  keyframe (features, pointmap, pose) and idx_f2k resets
+Two steps (feature parities) are captured as HIP graphs and replayed alternately: no host
+work per frame.  The timed steps are frames 1..K of the sequence (K = 200 by default: the
+whole configs[2] sequence); a shorter K is also followed by an untimed-in-the-headline full
+200-frame pass ("c3_sequence_200").
 Multi-GPU: tracking is sequential per sequence → one independent replica per rank
 ("replicas only"); value = frames of all ranks / max rank time.
 
@@ -46,7 +55,7 @@ METRIC = "tracking frames/sec @512x384 + pairwise pointmap-inference ms, 1/8 MI3
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (debug)")
@@ -66,37 +75,92 @@ def parse():
     return ap.parse_args()
 
 
-def setup(dev, seed):
-    """Model (seeded random weights), the synthetic frame / keyframe images, and the
-    tracking inputs.  The ViT runs on the images; its random-weight pointmaps carry no
-    geometry (no valid matches: every frame would be 'lost' after one GN iteration), so
-    matching, the Sim3 GN and the keyframe fusion run on the analytic 384x512 pointmaps /
-    descriptors of the synthetic scene (synthetic.pair) against a keyframe displaced by a
-    known Sim3 — the tracker does its real iterations every frame."""
-    import numpy as np
+SEQ_FRAMES = 200   # configs[2]: the synthetic sequence's length (and trajectory period)
+
+
+def setup(dev, seed, n_frames):
+    """Model (seeded random weights), tracker and the staged configs[2] sequence (frame 0 is
+    the INIT keyframe, frames 1..n_frames-1 are tracked).  The ViT runs on every frame's
+    image; its random-weight pointmaps carry no geometry, so the sequence's stand-in
+    replaces X/C/D/Q after it (monst3r_slam_amd.sequence) and matching, the Sim3 GN, the
+    keyframe fusion and the keyframe replacement run on the scene's geometry."""
     from monst3r_slam_amd import model as Mdl
-    from monst3r_slam_amd import synthetic as syn
+    from monst3r_slam_amd import sequence as S
     from monst3r_slam_amd.frontend import Tracker
     model, _ = Mdl.build(dev)
-    g = torch.Generator(device=dev).manual_seed(100 + seed)
-    img_k = torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1
-    img_f = torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1
-    rng = np.random.default_rng(seed)
-    X11, X21, D11, D21 = syn.pair(H, W, seed=seed, shift_px=(1.5, -0.75))
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-    glue = dict(X=t(np.stack([X11, X21])),
-                C=t((1.0 + np.exp(rng.normal(1.0, 0.5, size=(2, H, W)))).astype(np.float32)),
-                D16=t(np.stack([D11, D21]).astype(np.float16)),
-                Q=t((1.0 + np.exp(rng.normal(1.0, 0.5, size=(2, H, W)))).astype(np.float32)))
-    T_true = np.array([0.02, -0.01, 0.03, *syn.quat_from_axis_angle([0.3, 1.0, 0.2], 0.02), 1.0],
-                      np.float32)
-    Xk = t(syn.sim3_act(T_true, X21).reshape(-1, 3))
-    Ck = torch.full((H * W, 1), 2.0, device=dev)
+    seq = S.SyntheticSequence(n_frames, H, W, device=dev, seed=seed, period=SEQ_FRAMES)
     tr = Tracker(model)
-    T0 = torch.tensor([0, 0, 0, 0, 0, 0, 1, 1], dtype=torch.float32, device=dev)
-    feat_k = model.encode(img_k)[0].clone()
-    tr.add_keyframe(img_k, T0, X=Xk, C=Ck, feat=feat_k)
-    return model, tr, img_f, glue
+    return model, tr, seq
+
+
+def replay_ms(fn, dev, reps=20, replays=5):
+    """Average duration of one fn() (its launches back to back): fn is captured `reps`
+    times into one HIP graph, replayed, and timed with HIP events on the replay stream."""
+    g = capture(lambda: [fn() for _ in range(reps)], dev)
+    ms = time_replays(g, dev, replays) / reps
+    del g
+    return ms
+
+
+def kernel_rooflines(tr, out, dev):
+    """HBM rooflines of the matching and tracking kernels on the last frame's data
+    (algorithmic bytes per launch, SURVEY §8d / DESIGN §4, ÷ the launch's average duration,
+    replayed back to back): iter_proj 65 B/pixel (ray image 36 + target 12 + init 8 + out
+    8 + converged 1), refine_matches 128 B/pixel (D11 48 + D21 48 + p1 16 + out 16), the
+    persistent tracker GN 29 B/pixel/iteration (Xf 12 + Xk 12 + Qk 4 + valid 1)."""
+    from monst3r_slam_amd import _lib
+    from monst3r_slam_amd import matching as M
+    from monst3r_slam_amd import tracker as T
+    from monst3r_slam_amd.config import config as cfg
+    lib, P = _lib.load(), _lib.ptr
+    n = H * W
+    cm = cfg["matching"]
+    Xii, Xji = out["X"][0:1], out["X"][1:2]
+    rwg, pts, p_init = M.prep_for_iter_proj(Xii, Xji, tr.idx_f2k)
+    p = torch.empty((1, n, 2), dtype=torch.float32, device=dev)
+    conv = torch.empty((1, n), dtype=torch.uint8, device=dev)
+    p1 = torch.empty((1, n, 2), dtype=torch.int64, device=dev)
+    valid = torch.empty((1, n), dtype=torch.uint8, device=dev)
+    p1n = torch.empty_like(p1)
+    d11 = out["D16"][0:1].contiguous()
+    d21 = out["D16"][1:2].reshape(1, n, 24).contiguous()
+
+    def iproj():
+        lib.m3s_iter_proj(P(rwg), P(pts), P(p_init), P(p), P(conv), 1, H, W, n,
+                          int(cm["max_iter"]), float(cm["lambda_init"]),
+                          float(cm["convergence_thresh"]), _lib.stream(dev))
+
+    def refine():
+        lib.m3s_refine_matches(P(d11), P(d21), P(p1), P(p1n), 1, H, W, n, 24,
+                               int(cm["radius"]), int(cm["dilation_max"]), _lib.stream(dev))
+
+    iproj()
+    lib.m3s_match_occlusion(P(Xii.contiguous()), P(Xji.contiguous()), P(p), P(conv), P(p1),
+                            P(valid), 1, H, W, float(cm["dist_thresh"]), _lib.stream(dev))
+    ct = cfg["tracking"]
+    g = tr._glue
+    kf = tr.kf
+    info = T.opt_pose_ray_dist_sim3(g["Xf"], kf.X_canon, kf.T_WC, kf.T_WC, g["Qk"], g["vo"], ct,
+                                    check=False)[2]
+    torch.cuda.synchronize(dev)
+    iters = int(info[0])
+
+    def gn():
+        T.opt_pose_ray_dist_sim3(g["Xf"], kf.X_canon, kf.T_WC, kf.T_WC, g["Qk"], g["vo"], ct,
+                                 check=False)
+
+    res = {}
+    for name, fn, nbytes, note in (
+            ("iter_proj", iproj, 65 * n, "65 B/pixel"),
+            ("refine_matches", refine, 128 * n, "128 B/pixel; VALU-bound (1.16 G f16 FMA)"),
+            ("track_gn", gn, 29 * n * iters, f"29 B/pixel/iteration x {iters} iterations "
+                                             "(init + persistent GN + finish launches)")):
+        ms = replay_ms(fn, dev)
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        res[name] = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gbs / HBM_PEAK_GBS, "us_per_launch": ms * 1e3,
+                     "algorithmic_bytes": nbytes, "bytes_rule": note}
+    return res
 
 
 def capture(fn, dev, priority=0):
@@ -370,54 +434,119 @@ def pmc_traffic():
     """HBM bytes of the GEMM launches of one pair inference, from the committed rocprofv3
     PMC passes (tools/pmc_traffic.py over FETCH_SIZE / WRITE_SIZE runs of this bench; PMC
     counters cannot be read from inside the timed run).  None if absent."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_gemm_traffic.json")
-    if not os.path.exists(path):
-        return None
-    g = json.load(open(path))["gemm"]
-    return g
+    for name in ("r02_pmc_gemm_traffic.json", "r01_pmc_gemm_traffic.json"):
+        path = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(path):
+            g = dict(json.load(open(path))["gemm"])
+            g["source"] = "profiles/" + name
+            return g
+    return None
 
 
-def cpu_baseline():
-    """The reference-equivalent CPU path on this box's host cores, bounded sample:
-    the fp32 PyTorch restatement of the pair inference at 224x224 (configs[0] plumbing
-    case) scaled by FLOPs to 384x512, plus the C oracle of matching and the
-    numpy tracker on one 384x512 frame."""
+def host_cpu():
+    """Host CPU model and thread count (the GPU box's /proc/cpuinfo; lscpu's 'Model name')."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"model": model, "logical_cpus": os.cpu_count()}
+
+
+def cpu_baseline(seq):
+    """The reference-equivalent CPU path on this box's host cores, measured at the config's
+    size (no extrapolation): one tracked 384x512 frame of the same sequence — the fp32
+    PyTorch restatement of the pair inference (oracle/vit_ref.py: MonST3R encoder + both
+    decoders + 4 DPT heads + local features, same seeded weights, keyframe features cached
+    as the reference caches them) + the C oracle of the projective matching (OpenMP) + the
+    numpy tracker GN, on frame 1's stand-in outputs."""
     import numpy as np
     from monst3r_slam_amd import synthetic as syn
     from monst3r_slam_amd import weights as Wt
     from monst3r_slam_amd.config import default_config
+    from oracle import frontend_ref as FR
     from oracle import oracle as O
-    from oracle import tracker_ref as TR
     from oracle import vit_ref as V
     torch.set_flush_denormal(True)
     nthreads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(nthreads)
+    os.environ.setdefault("OMP_NUM_THREADS", str(nthreads))
     am, aM = Wt.MONST3R, Wt.MAST3R
     sdm = Wt.make_state_dict(am, 0)
     sdM = Wt.make_state_dict(aM, 1)
-    g = torch.Generator().manual_seed(1)
-    img_i = torch.rand(1, 3, 224, 224, generator=g) * 2 - 1
-    img_j = torch.rand(1, 3, 224, 224, generator=g) * 2 - 1
-    t0 = time.perf_counter()
-    V.asymmetric_inference(sdm, am, sdM, aM, img_i, img_j)
-    t_vit224 = time.perf_counter() - t0
-    # pair FLOPs 384x512 vs 224x224 (both encoders at 224: one extra encoder pass there)
-    scale = 2324.8 / (2324.8 * (196 / 768) + 523.0 * 196 / 768)
-    t_vit = t_vit224 * scale
+    img_i = seq.img[1].cpu()
+    img_j = seq.img[0].cpu()
+    with torch.no_grad():
+        feat_j = V.encode(sdm, am, img_j)           # the keyframe's cached features
+        t0 = time.perf_counter()
+        V.asymmetric_inference(sdm, am, sdM, aM, img_i, img_j, feat_j=feat_j)
+        t_vit = time.perf_counter() - t0
     O.build()
-    X11, X21, D11, D21 = syn.pair(H, W, seed=0)
-    p = syn.tracking_problem(H, W, seed=0)
+    cfg = default_config()
+    Tt, Tj = seq.T_gt_np[1], seq.T_gt_np[0]
+    Trel = syn.sim3_mul(syn.sim3_inv(Tt), Tj)
+    X = np.stack([seq.Xcam[1].cpu().numpy(),
+                  syn.sim3_act(Trel, seq.Xcam[0].cpu().numpy())]).reshape(2, H, W, 3)
+    C = np.stack([seq.C_own[1].cpu().numpy(), seq.C_other[1].cpu().numpy()]).reshape(2, H, W)
+    Q = np.stack([seq.Q_own[1].cpu().numpy(), seq.Q_other[1].cpu().numpy()]).reshape(2, H, W)
+    D = np.stack([seq.D16[1].cpu().numpy(), seq.D16[0].cpu().numpy()]).reshape(2, H, W, 24)
+    T0 = np.array([0, 0, 0, 0, 0, 0, 1, 1], np.float32)
+    orc = FR.SequenceOracle(seq.Xcam[0].cpu().numpy(), seq.C_own[0].cpu().numpy()[:, None],
+                            T0, cfg)
     t0 = time.perf_counter()
-    O.match(X11[None], X21[None], D11[None], D21[None])
-    TR.opt_pose_ray_dist_sim3(p["Xf"], p["Xk"], p["T_WCf"], p["T_WCk"], p["Qk"], p["valid"],
-                              default_config()["tracking"])
-    t_match = time.perf_counter() - t0
+    orc.step(X.astype(np.float32), C, D, Q)
+    t_track = time.perf_counter() - t0
     del np
-    return {"value": 1.0 / (t_vit + t_match), "unit": "frames/s", "cores": nthreads,
-            "kind": "port",
-            "sample": f"fp32 torch-CPU pair inference at 224x224 ({t_vit224:.2f} s, scaled by "
-                      f"FLOPs x{scale:.2f} to 384x512) + C-oracle matching + numpy tracker GN "
-                      f"on one 384x512 frame ({t_match:.2f} s)"}
+    return {"value": 1.0 / (t_vit + t_track), "unit": "frames/s", "cores": nthreads,
+            "kind": "port", "host_cpu": host_cpu(),
+            "sample": f"one tracked 384x512 frame of the configs[2] sequence, measured (no "
+                      f"scaling): fp32 torch-CPU pair inference {t_vit:.2f} s (keyframe "
+                      f"features cached) + C-oracle matching (OpenMP) + numpy tracker GN + "
+                      f"glue {t_track:.2f} s"}
+
+
+def run_sequence(loop, graphs, steps, dev, world):
+    """Reset the loop to its INIT keyframe, then replay `steps` frames (graphs alternate
+    feature parities) bracketed by barrier + synchronize; returns seconds (max over ranks)."""
+    loop.reset(parity=0)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        if graphs is not None:
+            graphs[i % 2].replay()
+        else:
+            loop.step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def sequence_report(loop, seq, steps):
+    from monst3r_slam_amd import sequence as S
+    sm = loop.summary(count=steps)
+    ok = sm["log"][:, 2] == 0
+    ate = S.ate_vs_gt(sm["T_WC"][ok], seq.T_gt_np[1:1 + sm["frames"]][ok]) if ok.sum() >= 3 \
+        else None
+    return {"frames": sm["frames"], "keyframes": sm["keyframes_total"],
+            "keyframes_added": sm["keyframes_added"], "lost": sm["lost"],
+            "cholesky_failures": sm["cholesky_failures"],
+            "gn_recovered_launches": sm["recovered"],
+            "gn_iterations_hist": sm["gn_iterations_hist"],
+            "gn_iterations_mean": sm["gn_iterations_mean"],
+            "ate_rmse_m": ate}
 
 
 def main():
@@ -431,65 +560,39 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
-    model, tr, img_f, glue = setup(dev, rank)
+    n_frames = max(SEQ_FRAMES, args.steps, args.warmup + 2) + 1
+    model, tr, seq = setup(dev, rank, n_frames)
     model.serial = not args.streams
     tr.split_heads = not args.no_split_heads
 
+    from monst3r_slam_amd import sequence as S
     from monst3r_slam_amd.frontend import FramePipeline
     pipe = None if args.no_prefetch else FramePipeline(tr, (H, W), args.side_priority)
-
-    def step(k=0):
-        """One tracked frame: pair inference on the frame image (encoder output prefetched
-        by the previous step unless --no-prefetch; this step encodes the next frame on the
-        side stream), then matching + GN + fusion on the synthetic scene's pointmaps."""
-        main = torch.cuda.current_stream(dev)
-        feat_i = None
-        if pipe is not None:
-            pipe.side.wait_stream(main)
-            with torch.cuda.stream(pipe.side):
-                model.encode(img_f, out=pipe.feat[(k + 1) % 2])   # every frame is img_f
-            feat_i = pipe.feat[k % 2]
-        out = model.pair(img_f, feat_j=tr.kf.feat, feat_i=feat_i, split_heads=tr.split_heads)
-        res = tr.track_outputs(glue)
-        model.join()
-        if pipe is not None:
-            main.wait_stream(pipe.side)
-        res["pair"] = out
-        return res
-
-    if pipe is not None:
-        pipe.prime(img_f, 0)
+    loop = S.SequenceLoop(tr, seq, pipe)
+    loop.reset(parity=0)
     for w in range(args.warmup):
-        step(2 * w)
+        loop.step(w)
     torch.cuda.synchronize(dev)
     # two graphs with the feature double-buffer parities swapped, replayed alternately
-    g_steps = None if args.eager else [capture(lambda: step(0), dev, args.main_priority),
-                                       capture(lambda: step(1), dev, args.main_priority)]
-    g_pair = None if args.eager else capture(lambda: model.pair(img_f, feat_j=tr.kf.feat), dev)
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        if g_steps is not None:
-            g_steps[i % 2].replay()
-        else:
-            step(i)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    graphs = None if args.eager else [capture(lambda: loop.step(0), dev, args.main_priority),
+                                      capture(lambda: loop.step(1), dev, args.main_priority)]
+    elapsed = run_sequence(loop, graphs, args.steps, dev, world)
 
     if rank == 0:
-        res = step(0)
-        gn_info = [int(v) for v in res["info"].tolist()]   # iterations, fail, converged
-        pair_ms = time_replays(g_pair, dev, max(5, args.steps // 2)) if g_pair else None
-        roof = gemm_roofline(model, img_f, tr.kf.feat, dev)
+        seq_rep = sequence_report(loop, seq, args.steps)
+        full = None
+        if args.steps != SEQ_FRAMES:
+            el200 = run_sequence(loop, graphs, SEQ_FRAMES, dev, 1)
+            full = dict(sequence_report(loop, seq, SEQ_FRAMES), frames_per_s=SEQ_FRAMES / el200,
+                        ms_per_frame=el200 / SEQ_FRAMES * 1e3)
+        g_pair = None if args.eager else capture(
+            lambda: model.pair(loop.img_cur, feat_j=tr.kf.feat), dev)
+        pair_ms = time_replays(g_pair, dev, 20) if g_pair else None
+        del g_pair
+        res = loop.step(0)                       # eager: buffers of one frame for the rooflines
+        torch.cuda.synchronize(dev)
+        kroof = kernel_rooflines(tr, res["pair"], dev)
+        roof = gemm_roofline(model, loop.img_cur, tr.kf.feat, dev)
         pmc = pmc_traffic()
         ms = elapsed / args.steps * 1e3
         line = {
@@ -504,23 +607,26 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (seeded random images and weights, no checkpoints offline; "
-                    "matching/GN/fusion on the analytic pointmaps of the synthetic scene)",
-            "config": {"workload": "tracking step 384x512: MonST3R+MASt3R pair inference + "
-                                   "projective matching + Sim3 ray GN (configs[1]+[2])",
+            "data": "synthetic (seeded random weights, no checkpoints offline; a rendered "
+                    "384x512 room sequence staged in HBM: the ViT runs on every frame's image, "
+                    "matching / GN / fusion / keyframe replacement on the scene's geometry)",
+            "config": {"workload": f"configs[2]: tracking loop over frames 1..{args.steps} of "
+                                   f"the synthetic {SEQ_FRAMES}-frame 384x512 sequence (MonST3R+"
+                                   "MASt3R pair inference + projective matching + Sim3 ray GN "
+                                   "+ keyframe fusion / replacement)",
                        "schedule": ("serial" if pipe is None else
                                     "next frame's encoder prefetched on a side stream") +
                                    ("" if args.no_split_heads else
                                     "; MASt3R DPT heads on a side stream"),
                        "h": H, "w": W, "models": "MonST3R ViT-L/B dpt + MASt3R ViT-L/B catmlp+dpt",
                        "parallelism": f"replicas{world}"},
+            "sequence": seq_rep,
             "pair_inference_ms": pair_ms,
-            "tracker_gn": {"iterations": gn_info[0], "fail": gn_info[1], "converged": gn_info[2]},
             "roofline": {"bound": "mfma", "achieved": roof["tflops"], "peak": BF16_DENSE_TFLOPS,
                          "unit": "TFLOP/s", "frac": roof["tflops"] / BF16_DENSE_TFLOPS,
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                          "traffic_unit": "HBM bytes per GEMM launch (PMC FETCH_SIZE x2 + "
-                                         "WRITE_SIZE, profiles/r01_pmc_gemm_traffic.json)",
+                                         "WRITE_SIZE, " + (pmc or {}).get("source", "") + ")",
                          "traffic_per_pair_bytes": pmc["hbm_bytes_per_pair"] if pmc else None,
                          "l2_hit_rate": pmc["l2_hit_rate"] if pmc else None,
                          "kernel": "gemm_kernel (bf16 MFMA GEMM / implicit conv)",
@@ -530,14 +636,17 @@ def main():
                          "gemm_ms_per_pair": roof["gemm_ms"],
                          "gemm_gflop_per_pair": roof["gemm_flops"] / 1e9,
                          "avg_launch_us": roof["avg_launch_us"]},
+            "kernel_rooflines": kroof,
         }
+        if full is not None:
+            line["c3_sequence_200"] = full
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline()
+            line["cpu_baseline"] = cpu_baseline(seq)
     if not args.no_c5 and rank == 0:
-        line["fp8_dynmask_512"] = c5_bench(model, dev, max(5, args.steps // 2))
+        line["fp8_dynmask_512"] = c5_bench(model, dev, 15)
     if not args.no_retrieval and rank == 0:
         line["keyframe_retrieval"] = retrieval_bench(
-            dev, max(5, args.steps // 2), cpu=not args.no_cpu_baseline and world == 1)
+            dev, 15, cpu=not args.no_cpu_baseline and world == 1)
     if not args.no_graph:
         kg = keyframe_graph_bench(model, dev, world, args.graph_steps)
         if rank == 0:

@@ -137,7 +137,10 @@ int m3s_gauss_newton_points(float* d_Twc, const float* d_Xs, const float* d_Cs,
  * Twc_k, Twc_f f32[8] (lietorch Sim3 data).  Xf, Xk f32[N,3]; Qk f32[N]; valid u8[N].
  * Out: T_WCf f32[8] and T_CkCf f32[8] (device), info i32[4] (device):
  *   info[0] iterations run, info[1] 1 if Cholesky failed (frame lost, tracker2.py:234),
- *   info[2] 1 if converged.
+ *   info[2] 1 if converged, info[3] iterations run by the single-workgroup recovery path
+ *   (0 normally; > 0 when the persistent launch lost co-residency next to concurrent
+ *   kernels and stopped at a barrier timeout — the result is still the GN solution, never
+ *   a Cholesky failure).
  * workspace: m3s_track_workspace_bytes(N) bytes.
  * ------------------------------------------------------------------------- */
 size_t m3s_track_workspace_bytes(int64_t n);
@@ -424,6 +427,44 @@ int m3s_ivf_search(const uint32_t* d_qpacked, const int32_t* d_qwords, const int
                    const int32_t* d_img_start, int64_t n_images, int64_t D, float alpha,
                    float similarity_threshold, int32_t* d_word_map, double* d_scores,
                    void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * Streaming tracking-loop plumbing (configs[2], the main loop main_monster_slam.py:247-332
+ * with FrameTracker2.track, tracker2.py:70-270), graph-replayable: the frame index
+ * d_frame and the keyframe's frame index d_kf_frame live on the device.
+ *
+ * m3s_seq_gather: frame min(*d_frame + offset, nframes-1) of a staged sequence
+ *   (frame_bytes per frame, 16-B multiple, 16-B aligned) -> d_dst.
+ * m3s_seq_pair_outputs: the synthetic scene's stand-in for the pair inference outputs of
+ *   monst3r_asymmetric_inference (monst3r_utils.py:255-297) — trained weights are absent,
+ *   random weights carry no geometry.  Staged per frame f: Xcam f32[F][n][3] (own camera),
+ *   C_own/C_other/Q_own/Q_other f32[F][n], D16 f16[F][n][24], T_gt f32[F][8] (camera to
+ *   world).  Writes X f32[2][n][3] = {Xcam[t], T_gt[t]^-1 T_gt[j] Xcam[j]},
+ *   C = {C_own[t], C_other[t]}, Q likewise, D16 f16[2][n][24] = {D16[t], D16[j]} with
+ *   t = *d_frame, j = *d_kf_frame.
+ * m3s_seq_advance: after the tracking glue (flags u8[2] = {new_kf, lost}, info i32[4] of
+ *   m3s_track_rays, T_WCf f32[8]): log row t (i32[8] = iterations, new_kf, lost,
+ *   keyframe frame, Cholesky failure, recovered iterations; f32[8] T_WCf) if t < nlog;
+ *   T_prev = T_WCf unless lost; on new_kf the frame becomes the keyframe
+ *   (keyframes.append(frame), main_monster_slam.py:319-321): kf_X = Xff f32[n][3],
+ *   kf_C = Cff f32[n], kf_N = 1, kf_T = T_WCf, kf_feat = feat_i (feat_bytes), idx_f2k =
+ *   identity (reset_idx_f2k, tracker2.py:256-257), *d_kf_frame = t; then *d_frame = t + 1.
+ * ------------------------------------------------------------------------- */
+int m3s_seq_gather(const void* d_src, int64_t frame_bytes, const int* d_frame, int offset,
+                   int nframes, void* d_dst, void* stream);
+
+int m3s_seq_pair_outputs(const float* d_Xcam, const float* d_C_own, const float* d_C_other,
+                         const float* d_Q_own, const float* d_Q_other, const void* d_D16,
+                         const float* d_T_gt, const int* d_frame, const int* d_kf_frame,
+                         int nframes, int64_t n, float* d_X, float* d_C, void* d_D16_out,
+                         float* d_Q, void* stream);
+
+int m3s_seq_advance(const uint8_t* d_flags, const int* d_info, const float* d_T_WCf,
+                    const float* d_Xff, const float* d_Cff, const void* d_feat_i,
+                    int64_t feat_bytes, int64_t n, float* d_kf_X, float* d_kf_C, float* d_kf_N,
+                    float* d_kf_T, void* d_kf_feat, int64_t* d_idx_f2k, float* d_T_prev,
+                    int* d_frame, int* d_kf_frame, int* d_log_i, float* d_log_T, int nlog,
+                    void* stream);
 
 #ifdef __cplusplus
 }

@@ -70,6 +70,11 @@ SIGNATURES = {
     "m3s_retr_quantize": (_I, [_P, _P, _I64, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P]),
     "m3s_asmk_aggregate": (_I, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P]),
     "m3s_ivf_search": (_I, [_P, _P, _P, _I64, _P, _P, _P, _I64, _I64, _F, _F, _P, _P, _P]),
+    "m3s_seq_gather": (_I, [_P, _I64, _P, _I, _I, _P, _P]),
+    "m3s_seq_pair_outputs": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I64, _P, _P, _P, _P,
+                                  _P]),
+    "m3s_seq_advance": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
+                             _P, _P, _P, _I, _P]),
 }
 
 

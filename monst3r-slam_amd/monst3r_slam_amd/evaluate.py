@@ -122,3 +122,11 @@ def ate(est_path, ref_path, with_scale=True, max_diff=0.01):
     s, R, t = umeyama(src, dst, with_scale)
     err = dst - (s * (R @ src.T).T + t)
     return float(np.sqrt((err ** 2).sum(1).mean())), len(pairs)
+
+
+def ate_arrays(est_xyz, ref_xyz, with_scale=True):
+    """ATE rmse of already associated translations [N, 3] (as `ate`, without the files)."""
+    src, dst = np.asarray(est_xyz, np.float64), np.asarray(ref_xyz, np.float64)
+    s, R, t = umeyama(src, dst, with_scale)
+    err = dst - (s * (R @ src.T).T + t)
+    return float(np.sqrt((err ** 2).sum(1).mean()))

@@ -29,8 +29,10 @@ class Keyframe:
         self.T_WC = T_WC.astype(np.float32).copy()
 
 
-def track_outputs(X, C, D16, Q, kf: Keyframe, idx_init, cfg_m, cfg_t):
-    """X [2,H,W,3], C [2,H,W], D16 f16 [2,H,W,24], Q [2,H,W] → dict (mutates kf)."""
+def track_outputs(X, C, D16, Q, kf: Keyframe, idx_init, cfg_m, cfg_t, T_init=None):
+    """X [2,H,W,3], C [2,H,W], D16 f16 [2,H,W,24], Q [2,H,W] → dict (mutates kf).
+    T_init: the frame's initial pose (the previous frame's, main_monster_slam.py:272-277);
+    None → the keyframe's."""
     H, W = X.shape[1:3]
     n = H * W
     idx, valid = O.match(X[0:1], X[1:2], D16[0:1], D16[1:2], idx_init)
@@ -49,7 +51,8 @@ def track_outputs(X, C, D16, Q, kf: Keyframe, idx_init, cfg_m, cfg_t):
         res["lost"] = True
         return res
     try:
-        T_WCf, T_CkCf, iters = TR.opt_pose_ray_dist_sim3(Xf, kf.X_canon, kf.T_WC, kf.T_WC,
+        T0 = kf.T_WC if T_init is None else np.asarray(T_init, np.float32)
+        T_WCf, T_CkCf, iters = TR.opt_pose_ray_dist_sim3(Xf, kf.X_canon, T0, kf.T_WC,
                                                          Qk[:, 0], valid_opt[:, 0], cfg_t)
     except TR.CholeskyError:
         res["lost"] = True
@@ -65,3 +68,28 @@ def track_outputs(X, C, D16, Q, kf: Keyframe, idx_init, cfg_m, cfg_t):
     res.update(T_WCf=T_WCf, T_CkCf=T_CkCf, iters=iters,
                new_kf=bool(min(match_frac_k, unique_frac_f) < cfg_t["match_frac_thresh"]))
     return res
+
+
+class SequenceOracle:
+    """The main loop's TRACKING branch bookkeeping (main_monster_slam.py:247-332): the frame
+    starts from the previous tracked pose (a lost frame keeps it), a new keyframe is the
+    frame itself (keyframes.append(frame): X_canon = Xff, C = Cff, N = 1 after its first
+    update_pointmap, T_WC = T_WCf) and resets idx_f2k (tracker2.py:256-257)."""
+
+    def __init__(self, X0, C0, T0, cfg):
+        self.kf = Keyframe(X0, C0, T0)
+        self.idx = None
+        self.T_prev = np.asarray(T0, np.float32).copy()
+        self.cfg = cfg
+
+    def step(self, X, C, D16, Q):
+        n = X.shape[1] * X.shape[2]
+        r = track_outputs(X, C, D16, Q, self.kf, self.idx, self.cfg["matching"],
+                          self.cfg["tracking"], T_init=self.T_prev)
+        self.idx = r["idx"][None]
+        if not r["lost"]:
+            self.T_prev = r["T_WCf"].astype(np.float32).copy()
+        if r["new_kf"]:
+            self.kf = Keyframe(X[0].reshape(n, 3), C[0].reshape(n, 1), r["T_WCf"])
+            self.idx = None
+        return r

@@ -19,7 +19,9 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+#include <immintrin.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -169,7 +171,7 @@ void ref_iter_proj(const float* rays, const float* pts, const float* p_init, flo
 }
 
 /* ---- refine_matches (matching_kernels.cu:25-81) --------------------------- */
-void ref_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
+static void refine_soft(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
                         int64_t* p1_new, int64_t b, int64_t h, int64_t w, int64_t n,
                         int64_t fdim, int radius, int dilation_max) {
   for (int64_t bi = 0; bi < b; bi++) {
@@ -213,6 +215,103 @@ void ref_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t*
       p1_new[2 * q + 1] = v_new;
     }
   }
+}
+
+/* Same arithmetic with the x86 AVX2 + F16C conversions (VCVTPS2PH with explicit round-to-nearest-
+ * even: the IEEE rounding float_to_half implements; VCVTPH2PS is exact) and the half
+ * operands widened to float once.  Inputs of the conversions are never f32 denormals here
+ * (products of two halves are >= 2^-48 in magnitude or exactly 0), so MXCSR.DAZ/FTZ do not
+ * change results.  tests/test_oracle_matching.py checks both paths agree bit for bit. */
+__attribute__((target("avx2,f16c"))) static inline __m256 rh8(__m256 x) {
+  return _mm256_cvtph_ps(_mm256_cvtps_ph(x, _MM_FROUND_TO_NEAREST_INT | _MM_FROUND_NO_EXC));
+}
+
+/* Eight candidates' sequential half chains side by side (each lane keeps its own k order);
+ * the argmax then scans the scores in the reference's candidate order. */
+__attribute__((target("avx2,f16c"))) static void refine_f16c(
+    const uint16_t* D11, const uint16_t* D21, const int64_t* p1, int64_t* p1_new, int64_t b,
+    int64_t h, int64_t w, int64_t n, int64_t fdim, int radius, int dilation_max) {
+  float* F11 = (float*)malloc(sizeof(float) * (size_t)(b * h * w * fdim));
+  float* F21 = (float*)malloc(sizeof(float) * (size_t)(b * n * fdim));
+  for (int64_t i = 0; i < b * h * w * fdim; i++) F11[i] = _cvtsh_ss(D11[i]);
+  for (int64_t i = 0; i < b * n * fdim; i++) F21[i] = _cvtsh_ss(D21[i]);
+  const int maxc = (2 * radius + 1) * (2 * radius + 1) + 8;
+  for (int64_t bi = 0; bi < b; bi++) {
+    const float* F11b = F11 + bi * h * w * fdim;
+#ifdef _OPENMP
+#pragma omp parallel
+#endif
+    {
+      int* offs = (int*)malloc(sizeof(int) * (size_t)maxc);
+      int* cu = (int*)malloc(sizeof(int) * (size_t)maxc);
+      int* cv = (int*)malloc(sizeof(int) * (size_t)maxc);
+      float* sc = (float*)malloc(sizeof(float) * (size_t)maxc);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 256)
+#endif
+      for (int64_t i = 0; i < n; i++) {
+        const int64_t q = bi * n + i;
+        int64_t u0 = p1[2 * q], v0 = p1[2 * q + 1];
+        float max_score = 0.0f; /* value-initialised c10::Half: +0.0 */
+        int64_t u_new = u0, v_new = v0;
+        const float* a = F21 + q * fdim;
+        for (int d = dilation_max; d > 0; d--) {
+          const int rd = radius * d;
+          const int diam = 2 * rd + 1;
+          int m = 0;
+          for (int ii = 0; ii < diam; ii += d)
+            for (int jj = 0; jj < diam; jj += d) {
+              const int64_t u = u0 - rd + ii;
+              const int64_t v = v0 - rd + jj;
+              if (v >= 0 && v < h && u >= 0 && u < w) {
+                offs[m] = (int)((v * w + u) * fdim);
+                cu[m] = (int)u;
+                cv[m] = (int)v;
+                m++;
+              }
+            }
+          for (int j = m; j < ((m + 7) & ~7); j++) offs[j] = m ? offs[0] : 0;
+          for (int m0 = 0; m0 < m; m0 += 8) {
+            const __m256i idx = _mm256_loadu_si256((const __m256i*)(offs + m0));
+            __m256 score = _mm256_setzero_ps();
+            for (int64_t k = 0; k < fdim; k++) {
+              const __m256 c = _mm256_i32gather_ps(F11b + k, idx, 4);
+              const __m256 prod = rh8(_mm256_mul_ps(_mm256_set1_ps(a[k]), c));
+              score = rh8(_mm256_add_ps(score, prod));
+            }
+            _mm256_storeu_ps(sc + m0, score);
+          }
+          for (int j = 0; j < m; j++)
+            if (sc[j] > max_score) {
+              max_score = sc[j];
+              u_new = cu[j];
+              v_new = cv[j];
+            }
+          u0 = u_new;
+          v0 = v_new;
+        }
+        p1_new[2 * q] = u_new;
+        p1_new[2 * q + 1] = v_new;
+      }
+      free(offs);
+      free(cu);
+      free(cv);
+      free(sc);
+    }
+  }
+  free(F11);
+  free(F21);
+}
+
+/* ORACLE_SOFT_HALF=1 (or a CPU without AVX2/F16C) selects the bit-level software path. */
+void ref_refine_matches(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
+                        int64_t* p1_new, int64_t b, int64_t h, int64_t w, int64_t n,
+                        int64_t fdim, int radius, int dilation_max) {
+  const char* e = getenv("ORACLE_SOFT_HALF");
+  if ((!e || atoi(e) == 0) && __builtin_cpu_supports("f16c") && __builtin_cpu_supports("avx2"))
+    refine_f16c(D11, D21, p1, p1_new, b, h, w, n, fdim, radius, dilation_max);
+  else
+    refine_soft(D11, D21, p1, p1_new, b, h, w, n, fdim, radius, dilation_max);
 }
 
 /* ---- matching prep (matching.py:25-49, image.py:5-38) ---------------------

@@ -27,3 +27,24 @@ def dev():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="session")
+def parity_log():
+    """Append measured parity statistics (one JSON object per call) to
+    $M3S_PARITY_LOG (default gpurun_out/parity_stats.jsonl) so the numbers behind each
+    tolerance survive `pytest -q`; copied into profiles/ per round."""
+    import json
+    import time
+    path = os.environ.get("M3S_PARITY_LOG", os.path.join(ROOT, "gpurun_out",
+                                                          "parity_stats.jsonl"))
+
+    def log(test, **stats):
+        try:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            with open(path, "a") as f:
+                f.write(json.dumps(dict(test=test, time=time.strftime("%Y-%m-%dT%H:%M:%S"),
+                                        **stats), default=float) + "\n")
+        except OSError:
+            pass
+    return log

@@ -17,6 +17,15 @@ pytestmark = pytest.mark.gpu
 G = os.path.join(os.path.dirname(__file__), "golden", "graph_small.npz")
 
 
+_LOG = []
+
+
+@pytest.fixture(autouse=True)
+def _bind_log(parity_log):
+    _LOG[:] = [parity_log]
+    yield
+
+
 def _check(X, C, D, Q, gX, gC, gD, gQ, tag):
     rel_X = (X - gX).norm(dim=-1) / gX.norm(dim=-1).clamp_min(1e-6)
     rel_C = (C - gC).abs() / gC.abs()
@@ -26,6 +35,8 @@ def _check(X, C, D, Q, gX, gC, gD, gQ, tag):
               C_med=float(rel_C.median()), D_cos_med=float(cos.median()),
               D_cos_min=float(cos.min()), Q_med=float(rel_Q.median()))
     print(tag, st)
+    if _LOG:
+        _LOG[0](tag, **st)
     # bf16 MFMA network vs fp32 reference: the tolerances of test_gpu_vit._compare_pair
     assert st["X_med"] < 0.03 and st["X_p99"] < 0.15, st
     assert st["C_med"] < 0.03, st

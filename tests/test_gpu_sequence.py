@@ -96,3 +96,61 @@ def test_frame_pipeline_matches_serial_tracking(dev):
     for k, (ra, rb) in enumerate(zip(a, b)):
         for x, y in zip(ra, rb):
             assert torch.equal(x, y), k
+
+
+def test_c3_sequence_384x512_vs_oracle(dev, parity_log):
+    """configs[2] at its real size: 32 tracked 384x512 frames of the synthetic room sequence
+    (monst3r_slam_amd.sequence) through SequenceLoop — stand-in pair outputs, matching seeded
+    by the previous frame, pose solve from the previous pose, keyframe fusion, keyframe
+    replacement + idx_f2k reset on new_kf, a planted unusable frame (lost) — compared frame
+    by frame with the numpy/C oracle of the same main loop (oracle.frontend_ref
+    .SequenceOracle): match indices / validity bit-exact, lost / new-keyframe decisions
+    equal, |dT_WCf| <= 1e-4, the keyframe state (fused or replaced) within the glue test's
+    tolerances.  The sequence must actually replace its keyframe and lose the planted frame."""
+    from monst3r_slam_amd import sequence as S
+    from monst3r_slam_amd.config import default_config
+    from monst3r_slam_amd.frontend import Tracker
+    from oracle import frontend_ref as FR
+    cfg = default_config()
+    F, lost_at = 33, 12
+    seq = S.SyntheticSequence(F, 384, 512, device=dev, period=100, lost_frames=(lost_at,))
+    tr = Tracker(model=None, cfg=cfg)
+    loop = S.SequenceLoop(tr, seq)
+    loop.reset()
+    T0 = np.array([0, 0, 0, 0, 0, 0, 1, 1], np.float32)
+    o = FR.SequenceOracle(seq.Xcam[0].cpu().numpy(), seq.C_own[0].reshape(-1, 1).cpu().numpy(),
+                          T0, cfg)
+    n_new, n_lost, dT_max = 0, 0, 0.0
+    for f in range(1, F):
+        res = loop.step()
+        out = res["pair"]
+        X, C = out["X"].cpu().numpy(), out["C"].cpu().numpy()
+        D16, Q = out["D16"].cpu().numpy(), out["Q"].cpu().numpy()
+        ref = o.step(X, C, D16, Q)
+        assert np.array_equal(res["idx_f2k"].cpu().numpy(), ref["idx"]), f
+        assert np.array_equal(res["valid_match"].cpu().numpy(), ref["valid"]), f
+        lost, new_kf = bool(res["lost"]), bool(res["new_kf"])
+        assert lost == ref["lost"] and new_kf == ref["new_kf"], f
+        assert lost == (f == lost_at), f
+        n_new += new_kf
+        n_lost += lost
+        if not lost:
+            dT = float(np.abs(res["T_WCf"].cpu().numpy() - ref["T_WCf"]).max())
+            dT_max = max(dT_max, dT)
+            assert dT <= 1e-4, (f, dT)
+        np.testing.assert_allclose(tr.kf.X_canon.cpu().numpy(), o.kf.X_canon, rtol=1e-4,
+                                   atol=1e-5)
+        np.testing.assert_allclose(tr.kf.C.cpu().numpy(), o.kf.C, rtol=1e-6)
+        assert float(tr.kf.N) == o.kf.N, f
+        np.testing.assert_allclose(tr.kf.T_WC.cpu().numpy(), o.kf.T_WC, atol=1e-4)
+        if new_kf:   # idx_f2k reset to the identity for the next frame
+            assert np.array_equal(tr.idx_f2k[0].cpu().numpy(), np.arange(384 * 512))
+    assert n_new >= 1 and n_lost == 1
+    summ = loop.summary()
+    assert summ["keyframes_added"] == n_new and summ["lost"] == 1
+    ate = S.ate_vs_gt(summ["T_WC"][summ["log"][:, 2] == 0],
+                      seq.T_gt_np[1:][summ["log"][:, 2] == 0])
+    assert ate < 5e-3, ate
+    parity_log("test_c3_sequence_384x512_vs_oracle", frames=F - 1, new_keyframes=n_new,
+               lost=1, idx_valid="bit-exact", max_abs_dT=dT_max, tol_dT=1e-4, ate_m=ate,
+               gn_iterations_hist=summ["gn_iterations_hist"])

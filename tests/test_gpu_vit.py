@@ -192,7 +192,7 @@ def _cos(a, b):
     return F.cosine_similarity(a.float(), b.float(), dim=-1)
 
 
-def _compare_pair(out, X, C, D, Q, tag):
+def _compare_pair(out, X, C, D, Q, tag, log=None):
     rel_X = ((out["X"] - X).norm(dim=-1) / X.norm(dim=-1).clamp_min(1e-6))
     rel_C = ((out["C"] - C).abs() / C.abs())
     cos_D = _cos(out["D"], D)
@@ -201,6 +201,8 @@ def _compare_pair(out, X, C, D, Q, tag):
                  C_med=float(rel_C.median()), D_cos_min=float(cos_D.min()),
                  D_cos_med=float(cos_D.median()), Q_med=float(rel_Q.median()))
     print(tag, stats)
+    if log is not None:
+        log(tag, **stats)
     # bf16 ViT vs fp32 reference (TF32 in the reference): stated tolerances
     assert stats["X_med"] < 0.03 and stats["X_p99"] < 0.15, stats
     assert stats["C_med"] < 0.03, stats
@@ -210,16 +212,16 @@ def _compare_pair(out, X, C, D, Q, tag):
     assert torch.equal(out["D16"], out["D"].half())
 
 
-def test_small_model_vs_reference_goldens(dev):
+def test_small_model_vs_reference_goldens(dev, parity_log):
     from monst3r_slam_amd import model as Mdl
     g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "vit_small.npz")))
     m, _ = Mdl.build(dev, small=True)
     t = lambda k: torch.from_numpy(g[k]).to(dev)  # noqa: E731
     out = m.pair(t("img_i"), img_j=t("img_j"))
-    _compare_pair(out, t("X"), t("C"), t("D"), t("Q"), "small-vs-golden")
+    _compare_pair(out, t("X"), t("C"), t("D"), t("Q"), "small-vs-golden", parity_log)
 
 
-def test_full_model_vs_fp32_restatement(dev):
+def test_full_model_vs_fp32_restatement(dev, parity_log):
     from monst3r_slam_amd import model as Mdl
     from oracle import vit_ref as V
     m, (sdm, am, sdM, aM) = Mdl.build(dev)
@@ -231,7 +233,7 @@ def test_full_model_vs_fp32_restatement(dev):
     sdm = {k: v.to(dev) for k, v in sdm.items()}
     sdM = {k: v.to(dev) for k, v in sdM.items()}
     X, C, D, Q, _, _ = V.asymmetric_inference(sdm, am, sdM, aM, img_i, img_j)
-    _compare_pair(out, X, C, D, Q, "full-vs-fp32")
+    _compare_pair(out, X, C, D, Q, "full-vs-fp32", parity_log)
 
 
 @pytest.mark.parametrize("splits,ks", [("1", "1"), ("3", "1"), ("5", "1"), ("1", "2"),
@@ -405,7 +407,7 @@ def test_attention_fp8_out(ops, dev, monkeypatch, splits):
     assert _rel(out, ref) < 0.05
 
 
-def test_fp8_model_vs_fp32_restatement_512(dev):
+def test_fp8_model_vs_fp32_restatement_512(dev, parity_log):
     """the fp8 transformer path (e4m3 activations + per-row weight scales on
     the scaled MFMA; heads in bf16) at 512x512 against the fp32 restatement.  Stated fp8
     tolerances (looser than the bf16 path's in _compare_pair): pointmap median relative
@@ -430,6 +432,7 @@ def test_fp8_model_vs_fp32_restatement_512(dev):
                  C_med=float(rel_C.median()), D_cos_med=float(cos_D.median()),
                  D_cos_min=float(cos_D.min()), Q_med=float(rel_Q.median()))
     print("fp8-512-vs-fp32", stats)
+    parity_log("fp8-512-vs-fp32", **stats)
     assert stats["X_med"] < 0.08 and stats["C_med"] < 0.08, stats
     assert stats["D_cos_med"] > 0.97 and stats["Q_med"] < 0.15, stats
     m.set_fp8(False)

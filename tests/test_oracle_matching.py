@@ -87,3 +87,37 @@ def test_refine_tie_first_candidate_wins(oracle):
     out = oracle.refine_matches(D11, D21[:, :1], p1, 3, 5)
     # level d=5 picks (17,17); level 4 re-centred at (17,17) finds only equal scores
     np.testing.assert_array_equal(out[0, 0], [17, 17])
+
+
+@pytest.mark.parametrize("flush", [False, True])
+def test_refine_f16c_path_equals_software_half(oracle, monkeypatch, flush):
+    """The oracle's AVX2/F16C refine (hardware RNE conversions, 8 candidate chains side by
+    side) returns the same matches as the bit-level software Half arithmetic, including
+    scores in the half-subnormal range and with the FTZ/DAZ mode torch.set_flush_denormal
+    sets."""
+    import torch
+    rng = np.random.default_rng(5)
+    b, h, w = 2, 24, 40
+    D11 = rng.normal(size=(b, h, w, 24)).astype(np.float32)
+    D21 = rng.normal(size=(b, h * w, 24)).astype(np.float32)
+    D11[0] *= 3e-3                      # products ~1e-5: subnormal half partial sums
+    D11[1, :, :8] = (np.sign(D11[1, :, :8]) * 6e-8)
+    D11, D21 = D11.astype(np.float16), D21.astype(np.float16)
+    p1 = np.stack([rng.integers(0, w, size=(b, h * w)), rng.integers(0, h, size=(b, h * w))], -1)
+    prev = torch.set_flush_denormal(flush)
+    try:
+        monkeypatch.setenv("ORACLE_SOFT_HALF", "1")
+        soft = oracle.refine_matches(D11, D21, p1, 3, 5)
+        monkeypatch.setenv("ORACLE_SOFT_HALF", "0")
+        fast = oracle.refine_matches(D11, D21, p1, 3, 5)
+    finally:
+        torch.set_flush_denormal(False)
+    del prev
+    assert np.array_equal(soft, fast)
+    X11, X21, E11, E21 = syn.pair(48, 64, seed=3)
+    p = np.stack([rng.integers(0, 64, size=(1, 48 * 64)), rng.integers(0, 48, size=(1, 48 * 64))], -1)
+    monkeypatch.setenv("ORACLE_SOFT_HALF", "1")
+    soft = oracle.refine_matches(E11[None].astype(np.float16), E21.reshape(1, -1, 24), p, 3, 5)
+    monkeypatch.setenv("ORACLE_SOFT_HALF", "0")
+    fast = oracle.refine_matches(E11[None].astype(np.float16), E21.reshape(1, -1, 24), p, 3, 5)
+    assert np.array_equal(soft, fast)
