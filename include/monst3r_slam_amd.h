@@ -220,7 +220,7 @@ enum {
                              epilogue forms LN(x) W^T + b = rstd (acc - mean c1[n]) + c2[n]
                              with mean / rstd from the producer's stats (Chan's combination
                              of the groups, fixed order), c1 = ln_c1 (row sums of B) and
-                             bias = c2 = b + W beta.  GEMM mode; no split-K, no fp8 */
+                             bias = c2 = b + W beta.  GEMM mode; no fp8 */
 };
 
 typedef struct {
@@ -256,12 +256,17 @@ typedef struct {
                                               (the decoder's norm_y of the other side)     */
   const float* ln_c1;                      /* LN_FOLD: f32 [N] per weight batch (strideBias) */
   float ln_eps;                            /* LN_FOLD: LayerNorm eps                       */
+  int32_t* tile_counters;                  /* split-K: i32 per (batch, output tile), all zero
+                                              on entry and left zero (device; the caller
+                                              zeroes it once; one per concurrent stream)   */
+  int32_t tile_counters_len;               /* entries; split-K needs batch x tiles of them  */
 } m3s_gemm_desc;
 
 /* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 8 == 0; conv: Cin % 32 == 0.
  * A, B 16-B aligned, lda/ldb/batch strides % 8 == 0; per-batch operand spans < 2 GiB.
- * With a workspace, GEMMs whose tile grid cannot fill the chip (M = 768 tokens) split K
- * over workgroups into f32 partials; a reduce kernel then applies the epilogue.
+ * With a workspace and tile counters, GEMMs whose tile grid cannot fill the chip (M = 768
+ * tokens) split K over workgroups into f32 partials; the last split of each tile sums them
+ * in split order (deterministic) and applies the epilogue — one launch.
  * ROPE (croco/pos_embed.py RoPE2D as applied in croco/blocks.py:64-66, 110-112) rotates
  * the q / k columns in the epilogue, replacing a separate pass over q and k. */
 int m3s_vit_gemm(const m3s_gemm_desc* desc, void* stream);

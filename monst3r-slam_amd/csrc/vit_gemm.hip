@@ -18,8 +18,11 @@
 // Epilogue: accumulators → LDS f32 tile → row-contiguous 8-column vectors per thread:
 //   bias, GELU(erf), 2D RoPE (croco RoPE2D, via a per-token cos/sin table), f32/bf16
 //   residual, ReLU, f32/bf16 store, ConvTranspose(k=s) scatter — 16-B loads/stores.
-// Split-K (tile grids that cannot fill 256 CUs): grid.z = batch x splits, f32 partial tiles
-//   to a workspace, then a reduce kernel applies the same epilogue (fixed order, no atomics).
+// Split-K (tile grids that cannot fill 256 CUs): batch x splits groups of workgroups; each
+//   writes its f32 partial tile to a workspace and bumps the tile's counter (agent-scope
+//   release); the LAST split of a tile (acquire) sums the partials in split order — fixed,
+//   so deterministic whichever workgroup finishes last — and runs the normal epilogue (any
+//   flag set, LayerNorm fold included).  One launch; counters return to zero.
 // Implicit conv (MODE 1, MODE 2 = ReLU on A): per K-tile the tap (ky, kx) and channel
 //   offset are block-uniform (Cin % BK == 0); ReLU is applied to the A fragments in
 //   registers (v_pk_max_i16 on the bf16 bits).
@@ -56,6 +59,8 @@ struct Args {
   int splits;
   int vec;                 // 8-wide vector epilogue allowed (alignment / N % 8 checked on host)
   float* ws;               // split-K partials [batch*splits][M][N]
+  int* cnt;                // split-K tile counters [batch][tiles] (zero between launches)
+  int fused;               // split-K: 1 = the last split reduces + epilogue, 0 = reduce kernel
   const float* rope_tab;   // [tokens][2 (y,x)][2 (cos,sin)][16]
   int rope_cols, rope_tokens;
   int wmod;                // > 0: weights / bias of batch g % wmod
@@ -656,16 +661,19 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
   const int en = n0 + ec;
   const int fl = EPI >= 0 ? EPI : a.flags;
   const bool vec = EPI >= 0 ? true : (a.vec != 0);
-  const bool vec_path = !SPLIT && vec && en < a.N;
+  const bool vec_path = vec && en < a.N;
   float e_b[8], e_pb[8], e_x[EG][16];
   float e_c1[8], e_pc1[8], e_mu[EG], e_rs[EG];  // LN_FOLD: c1 columns, row mean / rstd
   // LN_FOLD: the 16 lanes of a row group own rows er0 + v·RSTEP (v < NV ≤ 16); lane v
   // combines the statistics of row v once, the others read it by lane shuffle
   float ln_mu = 0.f, ln_rs = 0.f;
   static_assert(NV <= 16, "one row per lane of the group");
-  if ((fl & M3S_EPI_LN_FOLD) && !SPLIT && (lane & 15) < NV)
-    ln_row_stats(a, g ^ a.a_xor, min(m0 + er0 + (lane & 15) * RSTEP, a.M - 1), a.K >> 7, ln_mu,
-                 ln_rs);
+  auto ln_setup = [&]() {
+    if ((fl & M3S_EPI_LN_FOLD) && (lane & 15) < NV)
+      ln_row_stats(a, g ^ a.a_xor, min(m0 + er0 + (lane & 15) * RSTEP, a.M - 1), a.K >> 7,
+                   ln_mu, ln_rs);
+  };
+  if (!SPLIT) ln_setup();
   Epi e = make_epi(a, g);
   e.flags = fl;
   const bool e_rope = (fl & M3S_EPI_ROPE) && en < a.rope_cols;
@@ -699,7 +707,8 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
       }
     }
   };
-  if (vec_path) {
+  auto epi_setup = [&]() {
+    if (!vec_path) return;
     int co;
     (void)out_offset(e, m0, en, co);
 #pragma unroll
@@ -724,7 +733,8 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
       }
     }
     e_prefetch(0);
-  }
+  };
+  if (!SPLIT) epi_setup();   // split-K: only the tile's last split needs the operands
   M3S_T(t_e0);
   block_sync_lds();
   M3S_T(t_e1);
@@ -783,8 +793,11 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
     return;
   }
 
-  if (SPLIT) {
-    float* P = a.ws + (int64_t)zz * a.M * a.N;
+  if constexpr (SPLIT) {
+    // publish this split's partial tile; the tile's last split sums them all
+    __shared__ int s_last;
+    const int64_t per_b = (int64_t)a.M * a.N;
+    float* P = a.ws + (int64_t)zz * per_b;
 #pragma unroll 4
     for (int v = 0; v < NV; v++) {
       const int idx = v * NT + tid;
@@ -800,25 +813,51 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
         for (int t = 0; t < 8 && n + t < a.N; t++) dst[t] = src[t];
       }
     }
-#ifdef M3S_GEMM_STAMPS
+    if (!a.fused) return;  // splitk_reduce_kernel follows
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (tid == 0) {
-      M3S_T(t_end);
-      long long* o = g_m3s_stamps + (int64_t)blockIdx.x * 12;
-      o[8] = t_e0 - t_loop;
-      o[9] = t_e1 - t_e0;
-      o[10] = t_e2 - t_e1;
-      o[11] = t_end - t_e2;
-      o[0] = t_pro - t_start;
-      o[1] = s_wait;
-      o[2] = s_bar;
-      o[3] = s_comp;
-      o[4] = t_end - t_loop;
-      o[5] = nk;
-      o[6] = t_end - t_start;
-      o[7] = t_start;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      int* ctr = a.cnt + (int64_t)g * nwg + wgid;
+      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == a.splits - 1;
+      if (s_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#endif
-    return;
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    ln_setup();
+    epi_setup();
+    const float* P0 = a.ws + (int64_t)g * a.splits * per_b;
+#pragma unroll 2
+    for (int v = 0; v < NV; v++) {
+      const int idx = v * NT + tid;
+      const int row = idx / VPR, c = (idx % VPR) * 8;
+      const int m = m0 + row, n = n0 + c;
+      if (m >= a.M || n >= a.N) continue;
+      float* dst = cs + row * C::CST + c;
+      float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < a.splits; k++) {
+        float y[8];
+        if (k == split) {  // this workgroup's own partial is still in LDS
+          *reinterpret_cast<float4*>(&y[0]) = *reinterpret_cast<const float4*>(dst);
+          *reinterpret_cast<float4*>(&y[4]) = *reinterpret_cast<const float4*>(dst + 4);
+        } else if (vec) {
+          const float* q = P0 + k * per_b + (int64_t)m * a.N + n;
+          *reinterpret_cast<float4*>(&y[0]) = *reinterpret_cast<const float4*>(q);
+          *reinterpret_cast<float4*>(&y[4]) = *reinterpret_cast<const float4*>(q + 4);
+        } else {
+          const float* q = P0 + k * per_b + (int64_t)m * a.N + n;
+#pragma unroll
+          for (int t = 0; t < 8; t++) y[t] = n + t < a.N ? q[t] : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; t++) x[t] += y[t];
+      }
+      *reinterpret_cast<float4*>(dst) = make_float4(x[0], x[1], x[2], x[3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);
+    }
+    block_sync_lds();
   }
   if (vec_path) {
     const float sg = (en & 16) ? 1.f : -1.f;
@@ -934,7 +973,8 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
 #endif
 }
 
-// Sum the split-K partials (fixed order) and apply the epilogue; 8 columns per thread.
+// Unfused split-K: sum the partials (fixed order) and apply the epilogue; 8 columns per
+// thread, the whole chip reducing (the fused path reduces a tile on one CU).
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
   const int vpr = (a.N + 7) / 8;
   const int64_t vid = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -993,16 +1033,16 @@ enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7, T96 = 8, T9
 //   residual, +ReLU.  Any other combination (or an unaligned shape) runs the generic
 //   run-time-flag epilogue.  Each set exists with and without bias.
 template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, int E,
-          bool F8 = false>
+          bool F8 = false, bool SP = false>
 bool try_epi(Args& a, dim3 grid, hipStream_t s, int key) {
   if (key == E) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, E, F8>), grid,
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, SP, E, F8>), grid,
                        dim3(NT), 0, s, a);
     return true;
   }
   if (key == (E | M3S_EPI_BIAS)) {
     hipLaunchKernelGGL(
-        (gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, E | M3S_EPI_BIAS, F8>), grid,
+        (gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, SP, E | M3S_EPI_BIAS, F8>), grid,
         dim3(NT), 0, s, a);
     return true;
   }
@@ -1010,10 +1050,11 @@ bool try_epi(Args& a, dim3 grid, hipStream_t s, int key) {
 }
 
 // the same, biased set only (the LayerNorm-fold sets always carry a bias)
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, int E>
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, int E,
+          bool SP = false>
 bool try_epi_b(Args& a, dim3 grid, hipStream_t s, int key) {
   if (key != (E | M3S_EPI_BIAS)) return false;
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, E | M3S_EPI_BIAS>),
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, SP, E | M3S_EPI_BIAS>),
                      grid, dim3(NT), 0, s, a);
   return true;
 }
@@ -1037,44 +1078,54 @@ void launch_main_f8(Args& a, dim3 grid, hipStream_t s) {
                      dim3(NT), 0, s, a);
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE>
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, bool SP = false>
 void launch_main(Args& a, dim3 grid, hipStream_t s) {
   const int key = (a.flags & ~(M3S_PRO_RELU | (a.bias ? 0 : M3S_EPI_BIAS)));
   if (a.vec) {
     if (MODE == 0) {
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0>(a, grid, s, key)) return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_ROPE>(a, grid, s, key)) return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_GELU>(a, grid, s, key)) return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32>(
-              a, grid, s, key))
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0, false, SP>(a, grid, s, key)) return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_ROPE, false, SP>(a, grid, s, key))
         return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_OUT_F32>(a, grid, s, key)) return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_GELU, false, SP>(a, grid, s, key))
+        return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, false,
+                  SP>(a, grid, s, key))
+        return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_OUT_F32, false, SP>(a, grid, s,
+                                                                                    key))
+        return;
       // LayerNorm fold (the ViT blocks' norm → projection pairs): consumers qkv / q / kv
       // (+RoPE) and fc1 (+GELU), producers the residual GEMMs and the embeddings
       if constexpr (BN == 128 && BK == 64 && (BM == 64 || BM == 96 || BM == 128) && OCC <= 2 &&
                     (BM != 96 || OCC == 1)) {
         constexpr int LF = M3S_EPI_LN_FOLD, LS = M3S_EPI_LN_STATS;
-        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_ROPE>(a, grid, s, key))
+        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_ROPE, SP>(a, grid, s,
+                                                                                     key))
           return;
-        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_GELU>(a, grid, s, key))
+        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_GELU, SP>(a, grid, s,
+                                                                                     key))
           return;
         if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE,
-                      LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32>(a, grid, s, key))
+                      LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, SP>(a, grid, s, key))
           return;
-        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LS | M3S_EPI_OUT_F32>(a, grid, s, key))
+        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LS | M3S_EPI_OUT_F32, SP>(a, grid, s,
+                                                                                        key))
           return;
       }
     } else {
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0>(a, grid, s, key)) return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RES_BF16>(a, grid, s, key)) return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RELU>(a, grid, s, key)) return;
-      if constexpr (BN == 128)
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0, false, SP>(a, grid, s, key)) return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RES_BF16, false, SP>(a, grid, s,
+                                                                                     key))
+        return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RELU, false, SP>(a, grid, s, key))
+        return;
+      if constexpr (BN == 128 && !SP)
         if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RELU | M3S_EPI_DPT_OUT>(
                 a, grid, s, key))
           return;
     }
   }
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, -1>), grid,
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, SP, -1>), grid,
                      dim3(NT), 0, s, a);
 }
 
@@ -1102,24 +1153,25 @@ int launch(Args& a, int batch, hipStream_t s) {
     a.nmajor = 0;
   }
   if (split) {
-    // split implicit convs: the 64x128 config only (the small DPT levels, host-chosen)
-    constexpr bool CONV_SPLIT = BM == 64 && BN == 128 && STAGES == 3 && OCC == 2 && !F8;
-    if (a.mode != 0 && !CONV_SPLIT) return M3S_ERR_INVALID_ARG;
-    if constexpr (CONV_SPLIT) {
-      if (a.mode != 0 && (a.flags & M3S_PRO_RELU))
-        hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 2, true, -1, F8>), grid,
-                           dim3(NT), 0, s, a);
-      else if (a.mode != 0)
-        hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 1, true, -1, F8>), grid,
-                           dim3(NT), 0, s, a);
+    // split-K (fused last-split epilogue): 128^2 GEMM tiles, 64x128 GEMM / conv tiles
+    constexpr bool CAN = !F8 && ((BM == 128 && BN == 128 && BK == 64) ||
+                                 (BM == 64 && BN == 128 && STAGES == 3 && OCC == 2));
+    if constexpr (CAN) {
+      if (a.mode == 0)
+        launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 0, true>(a, grid, s);
+      else if (a.flags & M3S_PRO_RELU)
+        launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 2, true>(a, grid, s);
+      else
+        launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 1, true>(a, grid, s);
+    } else {
+      return M3S_ERR_INVALID_ARG;
     }
-    if (a.mode == 0)
-      hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true, -1, F8>), grid,
-                         dim3(NT), 0, s, a);
-    M3S_LAUNCH_CHECK();
-    const int64_t nv = (int64_t)a.M * ((a.N + 7) / 8);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(m3s_div_up(nv, 256), (unsigned)batch),
-                       dim3(256), 0, s, a);
+    if (!a.fused) {
+      M3S_LAUNCH_CHECK();
+      const int64_t nv = (int64_t)a.M * ((a.N + 7) / 8);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(m3s_div_up(nv, 256), (unsigned)batch),
+                         dim3(256), 0, s, a);
+    }
   } else if constexpr (F8) {
     launch_main_f8<BM, BN, BK, WM, WN, STAGES, OCC>(a, grid, s);
   } else if (a.mode == 0) {
@@ -1131,6 +1183,25 @@ int launch(Args& a, int batch, hipStream_t s) {
   }
   M3S_LAUNCH_CHECK();
   return M3S_OK;
+}
+
+// Per-shape launch choices measured on MI355X (tools/gemm_autotune.py): exact match on the
+// descriptor's (M, N, K, batch, flags, mode); everything else takes the heuristic below.
+struct TunedShape {
+  int M, N, K, batch, flags, mode, cfg, splits, fused;
+};
+const TunedShape kTuned[] = {
+#include "gemm_table.inc"
+    {0, 0, 0, 0, 0, 0, 0, 0, 0}};
+
+const TunedShape* tuned_for(const m3s_gemm_desc* d) {
+  static const bool off = getenv("M3S_GEMM_NO_TABLE") != nullptr;
+  if (off) return nullptr;
+  for (const TunedShape& t : kTuned)
+    if (t.M == d->M && t.N == d->N && t.K == d->K && t.batch == d->batch && t.flags == d->flags &&
+        t.mode == d->mode)
+      return &t;
+  return nullptr;
 }
 
 int forced_tile() {
@@ -1209,6 +1280,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   a.ct_gw = d->ct_gw;
   a.splits = 1;
   a.ws = reinterpret_cast<float*>(d->workspace);
+  a.cnt = d->tile_counters;
   a.rope_tab = d->rope_table;
   a.rope_cols = d->rope_cols;
   a.rope_tokens = d->rope_tokens;
@@ -1276,6 +1348,8 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   const int64_t tiles128 = (int64_t)((d->M + 127) / 128) * ((d->N + 127) / 128) * d->batch;
   const int nk = (int)((eK + 63) / 64);     // K-tiles of 128 bytes per row
   int cfg = forced_tile();
+  const TunedShape* tuned = (cfg == 0 && !getenv("M3S_GEMM_SPLITS")) ? tuned_for(d) : nullptr;
+  if (tuned) cfg = tuned->cfg;
   if (cfg == 0 && f8) {
     // fp8 (tools/fp8_tune.py, S = 768 / 1024 shapes): a K-tile holds 128 e4m3 values, so
     // the short-K latency regime comes sooner; 64x128 tiles at 2/CU win below ~1.5 waves
@@ -1312,6 +1386,8 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   if (!conv && cfg == T128K32) cfg = T128;
   if (conv && d->Cin % 64 == 0 && cfg == T128K32) cfg = T128;
   int splits = d->split_k;
+  if (tuned && splits <= 0) splits = tuned->splits;
+  if (const char* e = getenv("M3S_GEMM_SPLITS")) splits = atoi(e);  // tuning override
   if (splits <= 0) {
     splits = 1;
     if (!conv && (cfg == T128 || cfg == T128O2))
@@ -1323,9 +1399,22 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
       while (tiles64 * splits * 2 <= 512 && nk / (splits * 2) >= 8) splits *= 2;
     }
   }
-  const bool can_split = (!conv || (cfg == T64 && !(d->flags & M3S_EPI_DPT_OUT))) &&
-                         !(d->flags & M3S_EPI_CONVT) && !ln_fold && d->workspace &&
+  // fused split-K: 128^2 GEMM tiles or 64x128 GEMM / conv tiles, a workspace for the f32
+  // partials and one zeroed counter per (batch, tile)
+  const int bm = (cfg == T64) ? 64 : 128;
+  const int64_t tiles_cfg = (int64_t)((d->M + bm - 1) / bm) * ((d->N + 127) / 128) * d->batch;
+  const bool split_cfg = (!conv && (cfg == T128 || cfg == T128O2 || cfg == T64)) ||
+                         (conv && cfg == T64);
+  // fused (last split reduces the tile on its CU: one launch, but that CU streams all the
+  // partials) vs a separate reduce kernel spread over the chip; the LayerNorm-fold epilogue
+  // needs the fused path (the reduce kernel has no fold)
+  int fused = ln_fold ? 1 : (tuned ? tuned->fused : 0);
+  if (const char* e = getenv("M3S_GEMM_FUSED")) fused = atoi(e) != 0 || ln_fold;  // tuning
+  const bool can_split = split_cfg && !f8 && !(d->flags & (M3S_EPI_CONVT | M3S_EPI_DPT_OUT)) &&
+                         d->workspace &&
+                         (!fused || (d->tile_counters && tiles_cfg <= (int64_t)d->tile_counters_len)) &&
                          (int64_t)splits * d->batch * d->M * d->N * 4 <= d->workspace_bytes;
+  a.fused = fused;
   if (splits > 1 && can_split) a.splits = splits;
   if (f8) {
     switch (cfg) {

@@ -97,7 +97,8 @@ class GemmDesc(ctypes.Structure):
                 ("dpt_conf_min", ctypes.c_float), ("col_scale", _P),
                 ("stride_col_scale", _I64), ("C2", _P), ("stats", _P),
                 ("stats_groups", ctypes.c_int32), ("a_batch_xor", ctypes.c_int32),
-                ("ln_c1", _P), ("ln_eps", ctypes.c_float)]
+                ("ln_c1", _P), ("ln_eps", ctypes.c_float),
+                ("tile_counters", _P), ("tile_counters_len", ctypes.c_int32)]
 
 
 (EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT,

@@ -54,9 +54,11 @@ class Ops:
         self.lib = _lib.load()
         self.dev = dev
         self.record = None  # list → (descriptor, flops, fp8) per GEMM launch (bench roofline)
-        # f32 split-K / attention-split scratch, one per stream (the M = 768 GEMMs split K
-        # when their grid cannot fill 256 CUs; concurrent streams must not share it)
+        # f32 split-K / attention-split scratch and the split-K tile counters (zeroed once,
+        # left zero by the kernels), one set per stream (the M = 768 GEMMs split K when
+        # their grid cannot fill 256 CUs; concurrent streams must not share them)
         self._ws = {}
+        self._cnt = {}
 
     @property
     def ws(self):
@@ -66,6 +68,15 @@ class Ops:
             w = torch.empty(64 << 20, dtype=torch.uint8, device=self.dev)
             self._ws[sid] = w
         return w
+
+    @property
+    def counters(self):
+        sid = torch.cuda.current_stream(self.dev).cuda_stream
+        c = self._cnt.get(sid)
+        if c is None:
+            c = torch.zeros(1 << 16, dtype=torch.int32, device=self.dev)
+            self._cnt[sid] = c
+        return c
 
     def _s(self):
         return _lib.stream(self.dev)
@@ -90,6 +101,8 @@ class Ops:
         d.M, d.N, d.K, d.batch, d.flags = M, N, K, batch, flags
         ws = self.ws
         d.workspace, d.workspace_bytes, d.split_k = _p(ws), ws.numel(), split_k
+        cnt = self.counters
+        d.tile_counters, d.tile_counters_len = _p(cnt), cnt.numel()
         d.weight_mod = wmod
         if fp8 is not None:
             d.flags |= _lib.IN_FP8

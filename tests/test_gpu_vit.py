@@ -494,13 +494,17 @@ def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k):
                                                   (768, 3072, 768, 4, 0, "gelu"),
                                                   (768, 4096, 1024, 1, 0, "gelu"),
                                                   (200, 384, 256, 2, 1, "none")])
-def test_gemm_ln_fold_consumer(ops, dev, M, N, K, batch, axor, epi):
+@pytest.mark.parametrize("split", ["0", "3"])
+def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi, split):
     """LN_FOLD: LN(x) Wᵀ + b computed as rstd (bf16(x) (W∘γ)ᵀ − mean c1) + c2 from the
     producer's statistics, vs torch fp32 LayerNorm → Linear (→ RoPE / GELU) on x of
     problem g ^ axor; x carries a mean offset (the cancellation the fold must survive).
-    Tolerance 1e-2 of the output scale (bf16 operands, as the unfolded GEMM tests)."""
+    Tolerance 1e-2 of the output scale (bf16 operands, as the unfolded GEMM tests).
+    split "3": K split over 3 workgroups per tile, the fold applied by the last split."""
     from monst3r_slam_amd import _lib
     from monst3r_slam_amd.model import ln_fold, LN_EPS
+    if split != "0":
+        monkeypatch.setenv("M3S_GEMM_SPLITS", split)
     from oracle import vit_ref as V
     g = torch.Generator(device=dev).manual_seed(12)
     x = torch.randn(batch, M, K, device=dev, generator=g) * 1.5 + 0.7
@@ -580,3 +584,60 @@ def test_cross_attention_kv_batch_xor(ops, dev):
     o2 = torch.empty_like(o)
     ops.attn(q, D, S * D, kvs, kvs[:, :, D:], 2 * D, S * 2 * D, o2, D, S * D, B, heads, S, S)
     assert torch.equal(o, o2)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 7])
+@pytest.mark.parametrize("splits", [2, 3, 5])
+@pytest.mark.parametrize("epi", ["gelu", "res_stats", "rope", "f32"])
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_gemm_fused_splitk(ops, dev, monkeypatch, tile, splits, epi, fused):
+    """Split-K, fused (the last split of a tile sums the partials and runs the epilogue) and
+    unfused (reduce kernel), on 128^2, 64x128 and 2-per-CU 128^2 tiles with uneven K shares
+    and a ragged M tile: equal to the unsplit GEMM within f32 summation-order rounding,
+    bit-identical run to run (partials summed in split order whichever workgroup arrives
+    last), and the tile counters are left zero."""
+    from monst3r_slam_amd import _lib
+    from oracle import vit_ref as V
+    monkeypatch.setenv("M3S_GEMM_TILE", str(tile))
+    monkeypatch.setenv("M3S_GEMM_FUSED", fused)
+    M, N, K, b = 768 if epi == "rope" else 700, 768, 1216, 2
+    g = torch.Generator(device=dev).manual_seed(40 + splits)
+    A = torch.randn(b, M, K, device=dev, generator=g).bfloat16()
+    B = (torch.randn(b, N, K, device=dev, generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(b, N, device=dev, generator=g)
+    R = torch.randn(b, M, N, device=dev, generator=g)
+
+    def run(sp):
+        monkeypatch.setenv("M3S_GEMM_SPLITS", str(sp))
+        kw = dict(sA=M * K, sB=N * K, sC=M * N, bias=bias, sBias=N)
+        if epi == "gelu":
+            C = torch.empty(b, M, N, device=dev, dtype=torch.bfloat16)
+            ops.gemm(A, B, C, M, N, K, b, flags=_lib.EPI_GELU, **kw)
+            return (C,)
+        if epi == "rope":
+            C = torch.empty(b, M, N, device=dev, dtype=torch.bfloat16)
+            pos = V.positions(1, 24, 32, dev)[0].contiguous()
+            ops.gemm(A, B, C, M, N, K, b, rope=(ops.rope_table(pos, 100.0), 512, M), **kw)
+            return (C,)
+        if epi == "f32":
+            C = torch.empty(b, M, N, device=dev)
+            ops.gemm(A, B, C, M, N, K, b, flags=_lib.EPI_OUT_F32, **kw)
+            return (C,)
+        C = torch.empty(b, M, N, device=dev)
+        xb = torch.empty(b, M, N, device=dev, dtype=torch.bfloat16)
+        st = torch.empty((b, M, N // 128, 2), device=dev)
+        ops.gemm(A, B, C, M, N, K, b, R=R, sR=M * N, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32,
+                 ln_stats=(xb, st), **kw)
+        return C, xb, st
+
+    ref = run(1)
+    out1 = run(splits)
+    out2 = run(splits)
+    torch.cuda.synchronize()
+    for x, y in zip(out1, out2):
+        assert torch.equal(x, y), "split-K result must not depend on arrival order"
+    tol = 1e-2 if ref[0].dtype == torch.bfloat16 else 1e-5
+    assert _rel(out1[0], ref[0]) < tol
+    if epi == "res_stats":
+        assert torch.equal(out1[1], out1[0].bfloat16())
+    assert int(ops.counters.abs().sum()) == 0
