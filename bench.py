@@ -257,7 +257,7 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
     frames.img[:n_kf] = imgs
     frames.X[:n_kf] = torch.from_numpy(sc["Xs"]).to(dev)
     frames.C[:n_kf] = torch.from_numpy(sc["Cs"]).to(dev)
-    frames.N[:n_kf] = 1
+    frames.set_counts(range(n_kf), N=1)
     frames.img_true_shape[:n_kf] = torch.tensor([[H, W]], dtype=torch.int32, device=dev)
     frames.n_size = n_kf
     T0 = torch.from_numpy(sc["Twc"]).to(dev).reshape(n_kf, 1, 8)

@@ -43,25 +43,42 @@ class Keyframes:
         self.feat = torch.zeros(buffer, 1, S, feat_dim, dtype=torch.bfloat16, device=dev)
         self.pos = torch.zeros(buffer, 1, S, 2, dtype=torch.int64, device=dev)
         self.K = torch.zeros(3, 3, device=dev)
+        # host mirrors of the per-keyframe counters: __getitem__ needs no device read
+        self._h_id = [0] * buffer
+        self._h_N = [0] * buffer
+        self._h_Nu = [0] * buffer
 
     def __len__(self):
         return self.n_size
 
+    def set_counts(self, idx, N=1, N_updates=1, frame_id=None):
+        """Set the update counts (and dataset index) of keyframes idx (list / range) on the
+        device slabs and their host mirrors together (bulk loads that bypass __setitem__)."""
+        for i in idx:
+            self._h_N[i], self._h_Nu[i] = int(N), int(N_updates)
+            if frame_id is not None:
+                self._h_id[i] = int(frame_id)
+        ix = torch.as_tensor(list(idx), device=self.device)
+        self.N[ix] = int(N)
+        self.N_updates[ix] = int(N_updates)
+
     def __getitem__(self, idx) -> U.Frame:
         idx = int(idx)
-        f = U.Frame(int(self.dataset_idx[idx]), self.img[idx], self.img_true_shape[idx],
+        f = U.Frame(self._h_id[idx], self.img[idx], self.img_true_shape[idx],
                     self.img_true_shape[idx], None, self.T_WC[idx])
         f.X_canon, f.C, f.feat, f.pos = self.X[idx], self.C[idx], self.feat[idx], self.pos[idx]
-        f.N, f.N_updates = int(self.N[idx]), int(self.N_updates[idx])
+        f.N, f.N_updates = self._h_N[idx], self._h_Nu[idx]
         f.K = self.K
         return f
 
     def __setitem__(self, idx, fr: U.Frame):
         idx = int(idx)
+        self._h_id[idx], self._h_N[idx], self._h_Nu[idx] = int(fr.frame_id), int(fr.N), \
+            int(fr.N_updates)
         self.dataset_idx[idx] = fr.frame_id
         self.img[idx] = fr.img
         self.img_true_shape[idx] = fr.img_true_shape
-        self.T_WC[idx] = fr.T_WC.reshape(1, 8)
+        self.T_WC[idx] = _pose_data(fr.T_WC).reshape(1, 8)
         self.X[idx] = fr.X_canon
         self.C[idx] = fr.C
         self.N[idx] = fr.N
@@ -77,8 +94,13 @@ class Keyframes:
         self[self.n_size] = fr
 
     def update_T_WCs(self, T_WCs, idx):
-        """frame.py: update_T_WCs — T_WCs [k,1,8] (Sim3 data), idx [k]."""
-        self.T_WC[idx] = T_WCs.reshape(-1, 1, 8)
+        """frame.py: update_T_WCs — T_WCs [k,1,8] (Sim3 or its data), idx [k]."""
+        self.T_WC[idx] = _pose_data(T_WCs).reshape(-1, 1, 8)
+
+
+def _pose_data(T):
+    """Sim3 object (lietorch / monst3r_slam_amd.lie) or raw [..., 8] data → the data."""
+    return T.data if not isinstance(T, torch.Tensor) and hasattr(T, "data") else T
 
 
 class FactorGraph:
@@ -162,10 +184,13 @@ class FactorGraph:
         return ii, jj, idx_ii2jj, valid_match, Q_ii2jj
 
     def get_poses_points(self, unique_kf_idx):
-        kfs = [self.frames[i] for i in unique_kf_idx]
-        Xs = torch.stack([k.X_canon for k in kfs])
-        T_WCs = torch.stack([k.T_WC for k in kfs])            # [P,1,8]
-        Cs = torch.stack([k.get_average_conf() for k in kfs])
+        """global_opt2.py:120-127 as gathers on the keyframe slabs (no per-keyframe host
+        round trip): X_canon, T_WC [P,1,8], average confidence C / N."""
+        fr = self.frames
+        idx = unique_kf_idx.to(fr.X.device)
+        Xs = fr.X[idx]
+        T_WCs = fr.T_WC[idx]
+        Cs = fr.C[idx] / fr.N[idx].to(fr.C.dtype)[:, None, None]
         return Xs, T_WCs, Cs
 
     def solve_GN_rays(self):

@@ -918,6 +918,40 @@ class PairModel:
         return dict(X=pts[0:2], C=conf[0:2], D16=desc16, D=desc, Q=dconf, feat_i=feat_i,
                     mast3r_X=pts[2:4], mast3r_C=conf[2:4])
 
+    # ---- one view's heads (d3r/model.py:192-196 `_downstream_head`, per model) ----
+    def single_head(self, dec, model, side, H, W):
+        """The heads of ONE decoded view: dec = {h0, h6, h9, h12} bf16 [1,S,*] (the decoder
+        outputs at the DPT hooks, d3r/heads/dpt_head.py:110), model 0 = MonST3R (pts3d,
+        conf), 1 = MASt3R (+ desc, desc_conf from the catmlp local features), side 0/1 =
+        head1/head2.  Fresh tensors.  The batched pair / symmetric paths run all problems of
+        a pair in one launch; this is the reference model's per-view API."""
+        a = self.a
+        gh, gw = H // a.patch, W // a.patch
+        S, E, D = gh * gw, a.enc_dim, a.dec_dim
+        tag = f"api{model}{side}"
+        self._tag = tag
+        pts = self._buf("api_pts", (1, H, W, 3), F32)
+        conf = self._buf("api_conf", (1, H, W), F32)
+        self._tag = None
+        hk = {k: dec[k].reshape(1, S, -1).to(BF16).contiguous() for k in ("h0", "h6", "h9", "h12")}
+        self._dpt(hk, gh, gw, H, W, 1, model * 2 + side, 1, tag, pts, conf)
+        out = {"pts3d": pts.clone(), "conf": conf.clone()}
+        if model == 1:
+            # the local-feature MLP reads model 1 of a pair layout [model][side]: place this
+            # view in both sides' slots and keep the one whose weights are this side's
+            self._tag = tag
+            h0 = self._buf("api_h0", (4, S, E), BF16)
+            h12 = self._buf("api_h12", (4, S, D), BF16)
+            h0[2:4].copy_(hk["h0"].expand(2, S, E))
+            h12[2:4].copy_(hk["h12"].expand(2, S, D))
+            self._wm = 4
+            desc, _, dconf, ev = self._local_features({"h0": h0, "h12": h12}, 1, S, E, D, H, W)
+            self._wait(ev)
+            self._tag = None
+            out["desc"] = desc[side:side + 1].clone()
+            out["desc_conf"] = dconf[side:side + 1].clone()
+        return out
+
     # ---- monst3r_inference_mono (monst3r_utils.py:187-211) ----
     def mono(self, feat, H, W):
         """Self-pair decode of one frame's features feat bf16 [1,S,E] by MonST3R alone (2

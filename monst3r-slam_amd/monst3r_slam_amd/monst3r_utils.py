@@ -55,6 +55,59 @@ class ModelHandle:
     def share_memory(self):        # main_monster_slam.py:206-207 (single process here)
         return self
 
+    # ---- the reference model's methods (d3r/model.py:127-196), one model at a time ----
+    def _encoder_model(self) -> Mdl.PairModel:
+        """MonST3R's encoder is the pair model's; MASt3R's own encoder (used only when a
+        caller encodes with the MASt3R handle) is packed on first use."""
+        if self.kind == "monst3r":
+            return self.pair_model()
+        if getattr(self, "_enc_model", None) is None:
+            mon = _REGISTRY.get(str(self.device), {}).get("monst3r")
+            other_sd, other_arch = (mon.sd, mon.arch) if mon is not None else (self.sd, self.arch)
+            self._enc_model = Mdl.PairModel(Mdl.PackedWeights(self.sd, self.arch, other_sd,
+                                                              other_arch, self.device),
+                                            self.device)
+        return self._enc_model
+
+    def _encode_image(self, image, true_shape):
+        """d3r/model.py:127-139 → (feat [B,S,E] bf16, pos [B,S,2] int64, None)."""
+        pm = self._encoder_model()
+        feat, pos = pm.encode(image.to(self.device, torch.float32))
+        return feat.clone(), pos.clone(), None
+
+    def _decoder(self, f1, pos1, f2, pos2):
+        """d3r/model.py:171-190 → (dec1, dec2): per view the 13 block outputs of this model's
+        decoder; the MI355X decoder keeps only those the heads read — [0] (encoder tokens),
+        [6], [9], [12] (dec_norm) — the other entries are None."""
+        pm = self.pair_model()
+        a = pm.a
+        B, S = f1.shape[0], f1.shape[1]
+        gh = int(pos1[0, :, 0].max()) + 1       # row count from the grid positions
+        gw = S // gh
+        hooks = pm.decode_multi(f1.to(Mdl.BF16).reshape(B, S, a.enc_dim),
+                                f2.to(Mdl.BF16).reshape(B, S, a.enc_dim), gh, gw, models=2)
+        m = 0 if self.kind == "monst3r" else 1
+        idx = torch.arange(B, device=self.device) * 4 + m * 2   # z = (g*2 + model)*2 + side
+        views = []
+        for side in (0, 1):
+            dec = [None] * (a.dec_depth + 1)
+            for k in (0, 6, 9, 12):
+                dec[k] = hooks[f"h{k}"][idx + side].clone()
+            views.append(dec)
+        return views[0], views[1]
+
+    def _downstream_head(self, head_num, decout, img_shape):
+        """d3r/model.py:192-196: head 1 / 2 of this model on one view's decoder outputs
+        (bf16 heads; the reference runs them in f32, tolerances in tests/test_gpu_vit.py)."""
+        pm = self.pair_model()
+        H, W = _hw(img_shape)
+        m = 0 if self.kind == "monst3r" else 1
+        outs = []
+        for b in range(decout[0].shape[0]):
+            dec = {f"h{k}": decout[k][b:b + 1] for k in (0, 6, 9, 12)}
+            outs.append(pm.single_head(dec, m, head_num - 1, H, W))
+        return {k: torch.cat([o[k] for o in outs]) for k in outs[0]}
+
     def pair_model(self) -> Mdl.PairModel:
         reg = _REGISTRY.get(str(self.device), {})
         mon, mas = reg.get("monst3r"), reg.get("mast3r")
@@ -261,6 +314,34 @@ def _rearrange_pair(X, C, D, Q):
 def monst3r_match_asymmetric(mast3r, monst3r, frame_i, frame_j, idx_i2j_init=None):
     """:483-508 → (idx_i2j, valid_match_j, Xii, Cii, Qii, Xji, Cji, Qji)."""
     X, C, D, Q = monst3r_asymmetric_inference(mast3r, monst3r, frame_i, frame_j)
+    b = X.shape[0] // 2
+    idx_i2j, valid_match_j = matching.match(X[:b], X[b:], D[:b], D[b:],
+                                            idx_1_to_2_init=idx_i2j_init)
+    Xs, Cs, _, Qs = _rearrange_pair(X, C, D, Q)
+    return idx_i2j, valid_match_j, Xs[0], Cs[0], Qs[0], Xs[1], Cs[1], Qs[1]
+
+
+def monst3r_asymmetric_inference_with_dynamic_mask(mast3r, monst3r, frame_i, frame_j,
+                                                   dynamic_mask_i=None, dynamic_mask_j=None):
+    """:344-445 without the debug image dumps: the pair outputs with C / Q := 0 and D := 0
+    where frame i's (view ii) or frame j's (view ji) dynamic mask is set."""
+    X, C, D, Q = monst3r_asymmetric_inference(mast3r, monst3r, frame_i, frame_j)
+    b = X.shape[0] // 2
+    for mask, sl in ((dynamic_mask_i, slice(0, b)), (dynamic_mask_j, slice(b, 2 * b))):
+        if mask is None:
+            continue
+        _, Cm, Dm, Qm = apply_dynamic_mask_to_pointmaps(X[sl], C[sl], mask, D[sl], Q[sl])
+        C, D, Q = C.clone(), D.clone(), Q.clone()
+        C[sl], D[sl], Q[sl] = Cm, Dm, Qm
+    return X, C, D, Q
+
+
+def monst3r_match_asymmetric_with_dynamic_mask(mast3r, monst3r, frame_i, frame_j,
+                                               dynamic_mask_i=None, dynamic_mask_j=None,
+                                               idx_i2j_init=None):
+    """:448-480 → (idx_i2j, valid_match_j, Xii, Cii, Qii, Xji, Cji, Qji)."""
+    X, C, D, Q = monst3r_asymmetric_inference_with_dynamic_mask(
+        mast3r, monst3r, frame_i, frame_j, dynamic_mask_i, dynamic_mask_j)
     b = X.shape[0] // 2
     idx_i2j, valid_match_j = matching.match(X[:b], X[b:], D[:b], D[b:],
                                             idx_1_to_2_init=idx_i2j_init)

@@ -1,0 +1,52 @@
+"""GPU: the reference model objects' own methods on the MI355X handles (SURVEY §8b:
+`_encode_image`, `_decoder`, `_downstream_head`, d3r/model.py:127-196) reproduce what
+monst3r_asymmetric_inference (monst3r_utils.py:255-297) computes through the batched pair
+path, on the reduced-width models: pointmaps / confidences / descriptors of both views and
+both models, and the `mast3r_slam` package resolves to the same functions."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_model_methods_reproduce_pair_inference(dev):
+    from monst3r_slam_amd import monst3r_utils as U
+    from monst3r_slam_amd import weights as Wt
+    mon = U.load_monst3r(device=dev, arch=Wt.small(Wt.MONST3R))
+    mas = U.load_mast3r(device=dev, arch=Wt.small(Wt.MAST3R))
+    g = torch.Generator(device=dev).manual_seed(5)
+    H, W = 96, 128
+    img_i = torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1
+    img_j = torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1
+    shape = torch.tensor([[H, W]], device=dev)
+    fi, pi, _ = mon._encode_image(img_i, shape)
+    fj, pj, _ = mon._encode_image(img_j, shape)
+    # reference path: both decoders on MonST3R's encoder features (monst3r_utils.py:262-290)
+    d1, d2 = mon._decoder(fi, pi, fj, pj)
+    r11 = mon._downstream_head(1, d1, shape)
+    r21 = mon._downstream_head(2, d2, shape)
+    e1, e2 = mas._decoder(fi, pi, fj, pj)
+    m11 = mas._downstream_head(1, e1, shape)
+    m21 = mas._downstream_head(2, e2, shape)
+    assert len(d1) == 13 and d1[5] is None and d1[12] is not None
+    fr_i = U.Frame(0, img_i, shape, shape, None)
+    fr_j = U.Frame(1, img_j, shape, shape, None)
+    X, C, D, Q = U.monst3r_asymmetric_inference(mas, mon, fr_i, fr_j)
+    torch.testing.assert_close(fr_i.feat, fi)
+    for got, ref in ((r11["pts3d"][0], X[0]), (r21["pts3d"][0], X[1]), (r11["conf"][0], C[0]),
+                     (r21["conf"][0], C[1]), (m11["desc"][0], D[0]), (m21["desc"][0], D[1]),
+                     (m11["desc_conf"][0], Q[0]), (m21["desc_conf"][0], Q[1])):
+        # same kernels and operands; only the problem batching (tile grid) differs
+        torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
+    # MASt3R's own encoder (different weights) is available through its handle too
+    fm, _, _ = mas._encode_image(img_i, shape)
+    assert fm.shape == fi.shape and not torch.equal(fm, fi)
+
+
+def test_shim_package_resolves_to_the_mi355x_functions():
+    import mast3r_slam.matching as SM
+    import mast3r_slam.monst3r_utils as SU
+    from monst3r_slam_amd import matching as M
+    from monst3r_slam_amd import monst3r_utils as U
+    assert SM.match is M.match and SU.monst3r_match_asymmetric is U.monst3r_match_asymmetric
+    assert SU.monst3r_inference_mono is U.monst3r_inference_mono

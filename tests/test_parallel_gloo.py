@@ -59,8 +59,10 @@ def _worker(rank, world, port, q):
                 torch.bfloat16), None
 
         P.shard_keyframe_features(frames, range(6), enc)
-        q.put((rank, {k: v.clone() for k, v in r.items()}, added, g.ii.clone(), g.jj.clone(),
-               frames.feat[:6].float().clone()))
+        # numpy payloads travel by value: torch tensors would travel as shared-memory handles
+        # whose owner may exit before the parent opens them (connection reset)
+        q.put((rank, {k: v.numpy() for k, v in r.items()}, bool(added), g.ii.numpy(),
+               g.jj.numpy(), frames.feat[:6].float().numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -90,6 +92,8 @@ def test_sharded_edges_match_single_process(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, r, added, ii, jj, feats in res:
+        r = {k: torch.from_numpy(v) for k, v in r.items()}
+        ii, jj, feats = torch.from_numpy(ii), torch.from_numpy(jj), torch.from_numpy(feats)
         for k in ref:
             assert torch.equal(r[k], ref[k].to(r[k].dtype)), (rank, k)
         assert added == ref_added
