@@ -40,13 +40,14 @@ def _exp(xi):
     th2 = (phi * phi).sum(-1)
     th = th2.sqrt()
     small = th2 < _EPS
-    th_s = torch.where(small, torch.ones_like(th), th)
-    imag = torch.where(small, 0.5 - th2 / 48.0 + th2 * th2 / 3840.0, torch.sin(0.5 * th_s) / th_s)
-    real = torch.where(small, 1.0 - th2 / 8.0 + th2 * th2 / 384.0, torch.cos(0.5 * th_s))
+    th_q = torch.where(small, torch.ones_like(th), th)     # so3 exp: Taylor below th^2 < EPS
+    imag = torch.where(small, 0.5 - th2 / 48.0 + th2 * th2 / 3840.0, torch.sin(0.5 * th_q) / th_q)
+    real = torch.where(small, 1.0 - th2 / 8.0 + th2 * th2 / 384.0, torch.cos(0.5 * th_q))
     q = torch.cat([imag[..., None] * phi, real[..., None]], -1)
     scale = torch.exp(sigma)
     sg_small = sigma.abs() < _EPS
-    th_small = th.abs() < _EPS
+    th_small = th.abs() < _EPS                              # sim3 V: Taylor below th < EPS
+    th_s = torch.where(th_small, torch.ones_like(th), th)
     sg_s = torch.where(sg_small, torch.ones_like(sigma), sigma)
     C = torch.where(sg_small, torch.ones_like(sigma), (scale - 1.0) / sg_s)
     a = scale * torch.sin(th_s)
