@@ -62,10 +62,10 @@ class ModelHandle:
         if self.kind == "monst3r":
             return self.pair_model()
         if getattr(self, "_enc_model", None) is None:
-            mon = _REGISTRY.get(str(self.device), {}).get("monst3r")
-            other_sd, other_arch = (mon.sd, mon.arch) if mon is not None else (self.sd, self.arch)
-            self._enc_model = Mdl.PairModel(Mdl.PackedWeights(self.sd, self.arch, other_sd,
-                                                              other_arch, self.device),
+            # MASt3R's state dict in both slots: the encoder slot takes its encoder (its key
+            # set is MonST3R's plus the local-feature MLP the second slot needs)
+            self._enc_model = Mdl.PairModel(Mdl.PackedWeights(self.sd, self.arch, self.sd,
+                                                              self.arch, self.device),
                                             self.device)
         return self._enc_model
 

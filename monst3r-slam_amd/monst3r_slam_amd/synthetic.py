@@ -122,11 +122,15 @@ def pointmap_pair_batch(b, h, w, seed=0):
     return np.stack(Xs), np.stack(Ys), np.stack(Ds), np.stack(Es)
 
 
-def keyframe_graph(P=5, h=48, w=64, seed=0, noise=1e-3, perturb=0.01):
+def keyframe_graph(P=5, h=48, w=64, seed=0, noise=1e-3, perturb=0.01, pairs=None,
+                   two_way=False):
     """Backend GN test problem: P keyframes observing the same world points Xw (the view-0
     surface) under a smooth Sim3 trajectory; keyframe k's pointmap is T_k^-1 Xw (+ noise),
     so the true correspondence of every edge is the identity index (90 % marked valid).
-    Edges (i, i+1), (i, i+2).  Initial poses 1..P-1 perturbed by ~`perturb`."""
+    Edges (i, i+1), (i, i+2) — or, with `pairs=n`, the first n pairs (i, i+g) by gap
+    g = 1, 2, ... (the covisibility bands a keyframe graph holds), each also as (j, i) when
+    `two_way` (FactorGraph.add_factors' two-way packing).  Initial poses 1..P-1 perturbed
+    by ~`perturb`."""
     rng = np.random.default_rng(seed)
     K = intrinsics(h, w)
     N = h * w
@@ -138,7 +142,12 @@ def keyframe_graph(P=5, h=48, w=64, seed=0, noise=1e-3, perturb=0.01):
     Xw = backproject(depth_surface(h, w, seed), K).reshape(-1, 3)
     Xs = np.stack([sim3_act(sim3_inv(T), Xw) for T in T_gt]).astype(np.float32)
     Xs = Xs * (1.0 + noise * rng.normal(size=Xs.shape[:-1] + (1,))).astype(np.float32)
-    edges = [(i, i + 1) for i in range(P - 1)] + [(i, i + 2) for i in range(P - 2)]
+    if pairs is None:
+        edges = [(i, i + 1) for i in range(P - 1)] + [(i, i + 2) for i in range(P - 2)]
+    else:
+        edges = [(i, i + g) for g in range(1, P) for i in range(P - g)][:pairs]
+    if two_way:
+        edges = edges + [(j, i) for i, j in edges]
     ii = np.array([e[0] for e in edges], np.int64)
     jj = np.array([e[1] for e in edges], np.int64)
     E = len(edges)

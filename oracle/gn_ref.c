@@ -384,6 +384,9 @@ int ref_gauss_newton(const gn_params* prm, float* Twc, const float* Xs, const fl
   int itr;
   memset(dx_out, 0, sizeof(float) * (n > 0 ? n : 0));
   for (itr = 0; itr < max_iter; itr++) {
+    /* edges are independent (each sums its own points in order): OpenMP over edges keeps
+     * every per-edge sum, hence the result, identical to the serial loop */
+#pragma omp parallel for schedule(dynamic)
     for (int64_t e = 0; e < E; e++)
       edge_system(prm, Twc, Xs, Cs, rii[e], rjj[e], idx + e * N, valid_match + e * N, Q + e * N,
                   N, Hs + e * 196, gs + e * 14);

