@@ -29,1161 +29,28 @@
 // XCD-aware bijective tile order (cdna_hip_programming.md T1).
 #include <stdlib.h>
 #include <algorithm>
-#include <type_traits>
-#include "vit_common.h"
+#include "vit_gemm_kern.h"
+
+// the launchers are instantiated in vit_gemm_i*.hip (parallel compilation)
+#ifndef M3S_GEMM_STAMPS
+namespace m3s_gemm {
+extern template int launch<128, 128, 64, 2, 2, 3, 1>(Args&, int, hipStream_t);
+extern template int launch<128, 128, 32, 2, 2, 4, 2>(Args&, int, hipStream_t);
+extern template int launch<256, 128, 64, 2, 2, 3, 1>(Args&, int, hipStream_t);
+extern template int launch<128, 128, 64, 2, 2, 2, 2>(Args&, int, hipStream_t);
+extern template int launch<96, 128, 64, 1, 4, 3, 1>(Args&, int, hipStream_t);
+extern template int launch<96, 128, 64, 1, 4, 2, 2>(Args&, int, hipStream_t);
+extern template int launch<64, 128, 64, 2, 2, 6, 1>(Args&, int, hipStream_t);
+extern template int launch<128, 128, 64, 2, 2, 4, 1>(Args&, int, hipStream_t);
+extern template int launch<64, 128, 64, 2, 2, 3, 2>(Args&, int, hipStream_t);
+extern template int launch<64, 128, 64, 2, 2, 3, 2, true>(Args&, int, hipStream_t);
+extern template int launch<128, 128, 64, 2, 2, 2, 2, true>(Args&, int, hipStream_t);
+extern template int launch<128, 128, 64, 2, 2, 3, 1, true>(Args&, int, hipStream_t);
+}  // namespace m3s_gemm
+#endif
 
 namespace {
-
-constexpr int NT = 256;
-constexpr uint32_t OOB = 0x80000000u;      // any voffset ≥ num_records reads as zero
-constexpr int32_t NUM_RECORDS = 0x7ffffff0;
-
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-
-struct Args {
-  const bf16_t* A;
-  int64_t lda, sA;
-  const bf16_t* B;
-  int64_t ldb, sB;
-  void* C;
-  int64_t ldc, sC;
-  const float* bias;
-  int64_t sBias;
-  const void* R;
-  int64_t ldr, sR;
-  int M, N, K, flags, mode;
-  int Hin, Win, Cin, Hout, Wout, stride;
-  int ct_s, ct_cout, ct_gw;
-  int tiles_m, tiles_n;
-  int nmajor;              // tile order within a group (see gemm_kernel)
-  int splits;
-  int vec;                 // 8-wide vector epilogue allowed (alignment / N % 8 checked on host)
-  float* ws;               // split-K partials [batch*splits][M][N]
-  int* cnt;                // split-K tile counters [batch][tiles] (zero between launches)
-  int fused;               // split-K: 1 = the last split reduces + epilogue, 0 = reduce kernel
-  const float* rope_tab;   // [tokens][2 (y,x)][2 (cos,sin)][16]
-  int rope_cols, rope_tokens;
-  int wmod;                // > 0: weights / bias of batch g % wmod
-  const float* dpt_w4;     // DPT_OUT tail (see m3s_gemm_desc)
-  const float* dpt_b4;
-  float* dpt_pts;
-  float* dpt_conf;
-  float dpt_conf_min;
-  const float* cscale;     // IN_FP8: per-column dequant scale, batch stride sCscale
-  int64_t sCscale;
-  bf16_t* C2;              // LN_STATS: bf16 copy of C
-  float* stats;            // LN_STATS out / LN_FOLD in: [batch][M][groups] x (mean, M2)
-  int a_xor;               // LN_FOLD: A and stats of batch g ^ a_xor
-  const float* ln_c1;      // LN_FOLD: row sums of the gamma-folded weight (stride sBias)
-  float ln_eps;
-};
-
-// Row statistics of a LN_FOLD consumer from the producer's per-128-column (mean_t, M2_t)
-// groups (all of equal size, so no pairwise weights): mean = Σ mean_t / G,
-// M2 = Σ M2_t + 128 Σ (mean_t − mean)², biased variance M2 / (128 G) as nn.LayerNorm.
-// Fixed order → deterministic.  mu / rstd of row m of batch gs; groups ≤ 8.
-__device__ __forceinline__ void ln_row_stats(const Args& a, int64_t gs, int m, int groups,
-                                             float& mu, float& rs) {
-  const float2* st = reinterpret_cast<const float2*>(a.stats) + (gs * a.M + m) * groups;
-  float2 s[8];
-#pragma unroll
-  for (int t = 0; t < 8; t++) s[t] = t < groups ? st[t] : make_float2(0.f, 0.f);
-  float sm = 0.f, m2 = 0.f;
-#pragma unroll
-  for (int t = 0; t < 8; t++) sm += s[t].x;
-  const float mean = sm / (float)groups;
-#pragma unroll
-  for (int t = 0; t < 8; t++) {
-    const float d = t < groups ? s[t].x - mean : 0.f;
-    m2 += fmaf(128.f * d, d, s[t].y);
-  }
-  mu = mean;
-  rs = 1.0f / sqrtf(m2 / (128.f * (float)groups) + a.ln_eps);
-}
-
-// Sum over the 16 lanes of a DPP row (xor 1, xor 2 in the quad, then half-row and row
-// mirrors pair every lane with the other half): 4 VALU ops with DPP operands.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float x) {
-  return __builtin_bit_cast(
-      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
-}
-
-__device__ __forceinline__ float sum16(float v) {
-  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f<0x141>(v);  // row_half_mirror
-  v += dpp_f<0x140>(v);  // row_mirror
-  return v;
-}
-
-// LN_STATS producer: (mean, M2) of the 128 columns [n, n + 128) of row m held by 16
-// consecutive lanes (8 values each; n = 8·(lane % 16) + group base), written by the
-// group's first lane.  All 16 lanes of a group are active together (rows are uniform).
-__device__ __forceinline__ void ln_group_stats(const Args& a, int64_t g, int m, int n,
-                                               const float* x) {
-  float s = 0.f;
-#pragma unroll
-  for (int t = 0; t < 8; t++) s += x[t];
-  s = sum16(s);
-  const float mean = s * (1.0f / 128.0f);
-  float q = 0.f;
-#pragma unroll
-  for (int t = 0; t < 8; t++) {
-    const float d = x[t] - mean;
-    q = fmaf(d, d, q);
-  }
-  q = sum16(q);
-  if ((threadIdx.x & 15) == 0) {
-    const int groups = a.N >> 7;
-    reinterpret_cast<float2*>(a.stats)[(g * a.M + m) * groups + (n >> 7)] = make_float2(mean, q);
-  }
-}
-
-__device__ __forceinline__ void store_bf16x8(bf16_t* p, const float* x) {
-  bf16x8 o;
-#pragma unroll
-  for (int t = 0; t < 8; t++) o[t] = f2bf(x[t]);
-  *reinterpret_cast<bf16x8*>(p) = o;
-}
-
-// ---------------------------------------------------------------------------------------
-// epilogue
-// ---------------------------------------------------------------------------------------
-struct Epi {
-  const float* bias;
-  const char* R;
-  char* C;
-  int flags;
-  int64_t ldc, ldr;
-  int ct_s, ct_cout, ct_gw;
-  const float* rope_tab;
-  int rope_cols, rope_tokens;
-};
-
-__device__ __forceinline__ Epi make_epi(const Args& a, int g) {
-  Epi e;
-  const bool out32 = a.flags & M3S_EPI_OUT_F32;
-  const bool res32 = a.flags & M3S_EPI_RES_F32;
-  const int64_t gw = a.wmod > 0 ? g % a.wmod : g;
-  e.bias = (a.bias && (a.flags & M3S_EPI_BIAS)) ? a.bias + gw * a.sBias : nullptr;
-  e.R = a.R ? reinterpret_cast<const char*>(a.R) + (int64_t)g * a.sR * (res32 ? 4 : 2) : nullptr;
-  const int osz = out32 ? 4 : ((a.flags & M3S_EPI_OUT_FP8) ? 1 : 2);
-  e.C = reinterpret_cast<char*>(a.C) + (int64_t)g * a.sC * osz;
-  e.flags = a.flags;
-  e.ldc = a.ldc;
-  e.ldr = a.ldr;
-  e.ct_s = a.ct_s;
-  e.ct_cout = a.ct_cout;
-  e.ct_gw = a.ct_gw;
-  e.rope_tab = a.rope_tab;
-  e.rope_cols = a.rope_cols;
-  e.rope_tokens = a.rope_tokens;
-  return e;
-}
-
-// output element offset of (m, n) (ConvTranspose scatter: n = (a*s + b)*Cout + co)
-__device__ __forceinline__ int64_t out_offset(const Epi& e, int m, int n, int& co) {
-  if (e.flags & M3S_EPI_CONVT) {
-    co = n % e.ct_cout;
-    const int ab = n / e.ct_cout;
-    const int ca = ab / e.ct_s, cb = ab - ca * e.ct_s;
-    const int ti = m / e.ct_gw, tj = m - ti * e.ct_gw;
-    const int64_t oy = (int64_t)ti * e.ct_s + ca, ox = (int64_t)tj * e.ct_s + cb;
-    return (oy * ((int64_t)e.ct_gw * e.ct_s) + ox) * e.ct_cout + co;
-  }
-  co = n;
-  return (int64_t)m * e.ldc + n;
-}
-
-// RoPE2D on an 8-column group [n, n+8) of one head (head dim 64 = [y | x] halves; in a
-// half, pairs (i, i+16)): v are the group's values, p the partner group's (n ^ 16).
-__device__ __forceinline__ void rope8(const Epi& e, float* v, const float* p, int m, int n) {
-  const int s = m % e.rope_tokens;
-  const int half = (n >> 5) & 1;
-  const int i0 = n & 15;
-  const float* t = e.rope_tab + ((int64_t)s * 2 + half) * 32;
-  const float4 c0 = *reinterpret_cast<const float4*>(t + i0);
-  const float4 c1 = *reinterpret_cast<const float4*>(t + i0 + 4);
-  const float4 s0 = *reinterpret_cast<const float4*>(t + 16 + i0);
-  const float4 s1 = *reinterpret_cast<const float4*>(t + 16 + i0 + 4);
-  const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-  const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-  const float sg = (n & 16) ? 1.f : -1.f;  // lower: u c - v s; upper: v c + u s
-#pragma unroll
-  for (int i = 0; i < 8; i++) v[i] = v[i] * cs[i] + sg * p[i] * sn[i];
-}
-
-// 8 consecutive columns [n, n+8) of row m; p = partner columns (n ^ 16) for RoPE or null.
-__device__ __forceinline__ void epi_vec8(const Epi& e, float* v, float* p, int m, int n) {
-  int co;
-  const int64_t off = out_offset(e, m, n, co);
-  if (e.bias) {
-    const float4 b0 = *reinterpret_cast<const float4*>(e.bias + co);
-    const float4 b1 = *reinterpret_cast<const float4*>(e.bias + co + 4);
-    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
-    v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-  }
-  if (e.flags & M3S_EPI_GELU) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = gelu_erf(v[i]);
-  }
-  if ((e.flags & M3S_EPI_ROPE) && n < e.rope_cols) {
-    const int pn = n ^ 16;
-    if (e.bias) {
-      const float4 b0 = *reinterpret_cast<const float4*>(e.bias + pn);
-      const float4 b1 = *reinterpret_cast<const float4*>(e.bias + pn + 4);
-      p[0] += b0.x; p[1] += b0.y; p[2] += b0.z; p[3] += b0.w;
-      p[4] += b1.x; p[5] += b1.y; p[6] += b1.z; p[7] += b1.w;
-    }
-    rope8(e, v, p, m, n);
-  }
-  if (e.flags & M3S_EPI_RES_F32) {
-    const float* r = reinterpret_cast<const float*>(e.R) + (int64_t)m * e.ldr + n;
-    const float4 r0 = *reinterpret_cast<const float4*>(r);
-    const float4 r1 = *reinterpret_cast<const float4*>(r + 4);
-    v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
-    v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
-  }
-  if (e.flags & M3S_EPI_RES_BF16) {
-    const bf16x8 r = *reinterpret_cast<const bf16x8*>(
-        reinterpret_cast<const bf16_t*>(e.R) + (int64_t)m * e.ldr + n);
-#pragma unroll
-    for (int i = 0; i < 8; i++) v[i] += bf2f(r[i]);
-  }
-  if (e.flags & M3S_EPI_RELU) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = fmaxf(v[i], 0.f);
-  }
-  if (e.flags & M3S_EPI_OUT_F32) {
-    float* c = reinterpret_cast<float*>(e.C) + off;
-    *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
-    *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
-  } else if (e.flags & M3S_EPI_OUT_FP8) {
-    *reinterpret_cast<uint2*>(e.C + off) = make_uint2(pack4_fp8(v[0], v[1], v[2], v[3]),
-                                                      pack4_fp8(v[4], v[5], v[6], v[7]));
-  } else {
-    bf16x8 o;
-#pragma unroll
-    for (int i = 0; i < 8; i++) o[i] = f2bf(v[i]);
-    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16_t*>(e.C) + off) = o;
-  }
-}
-
-// one element (tails / unaligned shapes); p = partner value (RoPE) incl. its bias
-__device__ __forceinline__ void epi_one(const Epi& e, float v, float p, int m, int n) {
-  int co;
-  const int64_t off = out_offset(e, m, n, co);
-  if (e.bias) v += e.bias[co];
-  if (e.flags & M3S_EPI_GELU) v = gelu_erf(v);
-  if ((e.flags & M3S_EPI_ROPE) && n < e.rope_cols) {
-    if (e.bias) p += e.bias[n ^ 16];
-    const int s = m % e.rope_tokens, half = (n >> 5) & 1, i = n & 15;
-    const float* t = e.rope_tab + ((int64_t)s * 2 + half) * 32;
-    v = v * t[i] + ((n & 16) ? 1.f : -1.f) * p * t[16 + i];
-  }
-  if (e.flags & M3S_EPI_RES_F32) v += reinterpret_cast<const float*>(e.R)[(int64_t)m * e.ldr + n];
-  if (e.flags & M3S_EPI_RES_BF16)
-    v += bf2f(reinterpret_cast<const bf16_t*>(e.R)[(int64_t)m * e.ldr + n]);
-  if (e.flags & M3S_EPI_RELU) v = fmaxf(v, 0.f);
-  if (e.flags & M3S_EPI_OUT_F32) reinterpret_cast<float*>(e.C)[off] = v;
-  else if (e.flags & M3S_EPI_OUT_FP8) e.C[off] = (char)(pack4_fp8(v, 0.f, 0.f, 0.f) & 0xff);
-  else reinterpret_cast<bf16_t*>(e.C)[off] = f2bf(v);
-}
-
-// ---------------------------------------------------------------------------------------
-// main kernel
-// ---------------------------------------------------------------------------------------
-template <int BM, int BN, int BK, int STAGES>
-struct Cfg {
-  static constexpr int CPR = BK / 8;                 // 16-B chunks per row
-  static constexpr int RPB = 256 / (BK * 2);         // rows per 256-B LDS bank row
-  static constexpr int A_CH = BM * CPR / NT;         // DMA chunks per thread per K-tile
-  static constexpr int B_CH = BN * CPR / NT;
-  static constexpr int L = A_CH + B_CH;              // vmcnt units per K-tile
-  static constexpr int A_BYTES = BM * BK * 2;
-  static constexpr int ST_BYTES = (BM + BN) * BK * 2;
-  static constexpr int CST = BN + 4;                 // epilogue f32 row stride
-  static constexpr int EPI_BYTES = BM * CST * 4;
-  static constexpr int LDS_BYTES = STAGES * ST_BYTES > EPI_BYTES ? STAGES * ST_BYTES : EPI_BYTES;
-};
-
-__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(
-      r, (__attribute__((address_space(3))) void*)(lds), 16, voff, 0, 0, 0);
-}
-
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  // the builtin (not inline asm) so the compiler's own wait-count tracking sees the DMA
-  // retired — otherwise it later waits vmcnt(0) before every ds_read of the epilogue,
-  // i.e. behind each preceding global store.  gfx9 encoding: vmcnt[3:0] | vmcnt[5:4]<<14,
-  // expcnt[6:4] = 7, lgkmcnt[11:8] = 15 (no wait on those).
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
-}
-
-__device__ __forceinline__ void block_sync_lds() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ bf16x8 relu_frag(bf16x8 x) {
-  // bf16 ReLU on the bit patterns: negative values are negative int16s (−0 → +0)
-  s16x2* w = reinterpret_cast<s16x2*>(&x);
-  const s16x2 z = {0, 0};
-#pragma unroll
-  for (int i = 0; i < 4; i++) w[i] = __builtin_elementwise_max(w[i], z);
-  return x;
-}
-
-// Optional in-kernel timeline (build with -DM3S_GEMM_STAMPS, tools/gemm_stamps.py): wave 0
-// of each workgroup accumulates s_memtime deltas per phase into g_m3s_stamps[block][8].
-#ifdef M3S_GEMM_STAMPS
-__device__ long long* g_m3s_stamps;
-#define M3S_T(v) long long v = (long long)__builtin_amdgcn_s_memtime()
-#else
-#define M3S_T(v)
-#endif
-
-// EPI >= 0: the epilogue flag set, fixed at compile time (straight-line epilogue code, and
-// the 8-wide vector path assumed); EPI < 0: flags read at run time.
-// F8: A and B hold OCP fp8 e4m3 bytes.  K / lda / ldb / strides then arrive in 2-byte units
-// (host halves them), so the LDS-DMA ring, swizzle and row bytes are those of the bf16
-// kernel; only the fragments differ: a 32x32x64 scaled MFMA consumes 64 bytes of a row per
-// phase, lane half h holding bytes [32h, 32h + 32) (two swizzled 16-B chunks).
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, bool SPLIT,
-          int EPI, bool F8 = false>
-__global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
-  M3S_T(t_start);
-  using C = Cfg<BM, BN, BK, STAGES>;
-  constexpr int TM = BM / WM / 32;            // 32x32 accumulators per wave (M)
-  constexpr int TN = BN / WN / 32;
-  static_assert(C::A_CH >= 1 && C::B_CH >= 1, "tile too small for 256 threads");
-  static_assert((C::A_CH * NT) % C::CPR == 0 && 32 % (C::RPB * C::CPR) == 0, "swizzle");
-  static_assert(C::L * (STAGES - 2) <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
-
-  // 1-D grid over (batch x split) groups x tiles.  Workgroups are dispatched to the 8
-  // XCDs round-robin by linear id; the bijective remap gives each XCD a contiguous range
-  // of remapped ids (cdna_hip_programming.md T1), so neighbouring tiles share its L2.
-  // Within a group the tile order is M-major (an XCD sweeps N for one A band: A reused)
-  // or N-major (an XCD sweeps the M bands of a few weight columns: B reused), whichever
-  // the host estimated to fetch fewer bytes.
-  const int nwg = a.tiles_m * a.tiles_n;
-  const int total = gridDim.x;
-  const int orig = blockIdx.x;
-  int wid_lin = orig;
-  if (total >= 16) {
-    const int q = total / 8, r = total % 8, xcd = orig % 8;
-    wid_lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-  }
-  const int zz = wid_lin / nwg;
-  const int wgid = wid_lin - zz * nwg;
-  int tm, tn;
-  if (a.nmajor) {
-    tn = wgid / a.tiles_m;
-    tm = wgid - tn * a.tiles_m;
-  } else {
-    tm = wgid / a.tiles_n;
-    tn = wgid - tm * a.tiles_n;
-  }
-  const int g = SPLIT ? zz / a.splits : zz;
-  const int split = SPLIT ? zz - g * a.splits : 0;
-  const int m0 = tm * BM;
-  const int n0 = tn * BN;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(a.A + (int64_t)(g ^ a.a_xor) * a.sA), (short)0, NUM_RECORDS, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(a.B + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sB), (short)0,
-      NUM_RECORDS, 0x00020000);
-
-  // per-thread DMA chunks: chunk q = i*NT + tid lands at LDS row q / CPR, slot q % CPR and
-  // carries logical K-chunk slot ^ swz(row)
-  uint32_t a_off[C::A_CH];
-  int a_kc[C::A_CH], a_iy[C::A_CH], a_ix[C::A_CH];
-#pragma unroll
-  for (int i = 0; i < C::A_CH; i++) {
-    const int q = i * NT + tid;
-    const int r = q / C::CPR, p = q % C::CPR;
-    const int kc = (p ^ ((r / C::RPB) % C::CPR)) * 8;
-    const int m = m0 + r;
-    a_kc[i] = kc;
-    if (MODE == 0) {
-      a_off[i] = m < a.M ? (uint32_t)(((int64_t)m * a.lda + kc) * 2) : OOB;
-      a_iy[i] = a_ix[i] = 0;
-    } else {
-      const int oy = m / a.Wout, ox = m - oy * a.Wout;
-      a_iy[i] = m < a.M ? oy * a.stride - 1 : -(1 << 20);  // OOB rows never pass the bounds test
-      a_ix[i] = ox * a.stride - 1;
-      a_off[i] = 0;
-    }
-  }
-  uint32_t b_off[C::B_CH];
-  int b_kc[C::B_CH];
-#pragma unroll
-  for (int i = 0; i < C::B_CH; i++) {
-    const int q = i * NT + tid;
-    const int r = q / C::CPR, p = q % C::CPR;
-    const int kc = (p ^ ((r / C::RPB) % C::CPR)) * 8;
-    const int n = n0 + r;
-    b_kc[i] = kc;
-    b_off[i] = n < a.N ? (uint32_t)(((int64_t)n * a.ldb + kc) * 2) : OOB;
-  }
-
-  // One DMA chunk j (< A_CH: A, else B) of K-tile k0 into stage buffer sb.  The conv tap
-  // (ky, kx) / channel offset ci0 are block-uniform per K-tile.
-  auto issue_chunk = [&](int j, int k0, char* sb, int ky, int kx, int ci0) {
-    if (j < C::A_CH) {
-      uint32_t vo;
-      if (MODE == 0) {
-        vo = (k0 + a_kc[j] < a.K) ? a_off[j] + (uint32_t)k0 * 2 : OOB;
-      } else {
-        const int iy = a_iy[j] + ky, ix = a_ix[j] + kx;
-        const bool ok = (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-        vo = ok ? (uint32_t)((((int64_t)iy * a.Win + ix) * a.Cin + ci0 + a_kc[j]) * 2) : OOB;
-      }
-      glds16(rA, sb + (j * NT + wid * 64) * 16, vo);
-    } else {
-      const int i = j - C::A_CH;
-      const uint32_t vo = (k0 + b_kc[i] < a.K) ? b_off[i] + (uint32_t)k0 * 2 : OOB;
-      glds16(rB, sb + C::A_BYTES + (i * NT + wid * 64) * 16, vo);
-    }
-  };
-  auto tap_of = [&](int k0, int& ky, int& kx, int& ci0) {
-    ky = kx = ci0 = 0;
-    if (MODE != 0) {
-      const int tap = k0 / a.Cin;  // Cin % BK == 0
-      ci0 = k0 - tap * a.Cin;
-      ky = tap / 3;
-      kx = tap - ky * 3;
-    }
-  };
-  auto issue = [&](int ktile, int stage) {
-    const int k0 = ktile * BK;
-    int ky, kx, ci0;
-    tap_of(k0, ky, kx, ci0);
-#pragma unroll
-    for (int j = 0; j < C::L; j++) issue_chunk(j, k0, lds + stage * C::ST_BYTES, ky, kx, ci0);
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; i++)
-#pragma unroll
-    for (int j = 0; j < TN; j++)
-#pragma unroll
-      for (int r = 0; r < 16; r++) acc[i][j][r] = 0.f;
-
-  const int fr = lane & 31;
-  const int fh = lane >> 5;
-  const int fsw = (fr / C::RPB) % C::CPR;     // row swizzle of this lane's fragment rows
-  int nk = (a.K + BK - 1) / BK;
-  int kbase = 0;
-  if (SPLIT) {
-    const int per = (nk + a.splits - 1) / a.splits;
-    kbase = split * per;
-    nk = min(per, nk - kbase);
-    if (nk < 0) nk = 0;
-  }
-
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; s++)
-    if (s < nk) issue(kbase + s, s);
-  M3S_T(t_pro);
-#ifdef M3S_GEMM_STAMPS
-  long long s_wait = 0, s_bar = 0, s_comp = 0;
-#endif
-
-  // K loop.  Fragments are double-buffered in registers: a phase (16 of the K-tile's BK)
-  // issues the LDS reads of the NEXT phase, its share of the DMA of tile kt+STAGES-1, then
-  // its MFMAs; the last phase issues its MFMAs first, then retires tile kt+1 (counted
-  // vmcnt + barrier: the MFMAs keep the matrix pipe busy meanwhile) and reads tile kt+1's
-  // first fragments.  The steady-state loop (every tile prefetches) is branch-free, so the
-  // scheduler sees whole phases; sched_group_barrier pins the read / DMA / MFMA order.
-  constexpr int KK = F8 ? BK / 32 : BK / 16;  // MFMA phases per K-tile
-  constexpr int NR = (TM + TN) * (F8 ? 2 : 1); // ds_read_b128 per phase
-  constexpr int NM = TM * TN;                 // MFMAs per phase
-  using frag_t = std::conditional_t<F8, i32x8, bf16x8>;
-  frag_t fa[2][TM], fb[2][TN];
-  auto read_frags = [&](int buf, const char* sA, int kk) {
-    const char* sB = sA + C::A_BYTES;
-    if constexpr (F8) {
-      const int s0 = ((kk * 4 + 2 * fh) ^ fsw) * 16, s1 = ((kk * 4 + 2 * fh + 1) ^ fsw) * 16;
-#pragma unroll
-      for (int i = 0; i < TM; i++) {
-        const char* row = sA + (wm * (BM / WM) + i * 32 + fr) * (BK * 2);
-        const int4 lo = *reinterpret_cast<const int4*>(row + s0);
-        const int4 hi = *reinterpret_cast<const int4*>(row + s1);
-        fa[buf][i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      }
-#pragma unroll
-      for (int j = 0; j < TN; j++) {
-        const char* row = sB + (wn * (BN / WN) + j * 32 + fr) * (BK * 2);
-        const int4 lo = *reinterpret_cast<const int4*>(row + s0);
-        const int4 hi = *reinterpret_cast<const int4*>(row + s1);
-        fb[buf][j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      }
-    } else {
-      const int slot = ((kk * 2 + fh) ^ fsw) * 16;
-#pragma unroll
-      for (int i = 0; i < TM; i++) {
-        fa[buf][i] = *reinterpret_cast<const bf16x8*>(
-            sA + (wm * (BM / WM) + i * 32 + fr) * (BK * 2) + slot);
-        if (MODE == 2) fa[buf][i] = relu_frag(fa[buf][i]);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; j++)
-        fb[buf][j] = *reinterpret_cast<const bf16x8*>(
-            sB + (wn * (BN / WN) + j * 32 + fr) * (BK * 2) + slot);
-    }
-  };
-  auto mfmas = [&](int cur) {
-#pragma unroll
-    for (int i = 0; i < TM; i++)
-#pragma unroll
-      for (int j = 0; j < TN; j++) {
-        if constexpr (F8)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
-              fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0, 0, 0, 0);
-        else
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][i], fb[cur][j], acc[i][j],
-                                                              0, 0, 0);
-      }
-  };
-  auto stage_of = [&](int t) { return lds + (t % STAGES) * C::ST_BYTES; };
-  // retire the oldest DMA tile, leaving `ahead` (≤ STAGES - 2) younger tiles in flight
-  auto wait_ahead = [&](int ahead) {
-    if (STAGES >= 6 && ahead >= 4) vm_wait<C::L * (STAGES >= 6 ? 4 : 0)>();
-    else if (STAGES >= 5 && ahead >= 3) vm_wait<C::L * (STAGES >= 5 ? 3 : 0)>();
-    else if (STAGES >= 4 && ahead >= 2) vm_wait<C::L * 2>();
-    else if (ahead >= 1) vm_wait<C::L>();
-    else vm_wait<0>();
-  };
-  if (nk > 0) {
-    wait_ahead(min(nk - 1, STAGES - 2));
-    block_sync_lds();
-    read_frags(0, lds, 0);
-  }
-
-  const int nsteady = nk - (STAGES - 1);      // kt < nsteady: tile kt+STAGES-1 exists
-  int kt = 0;
-  for (; kt < nsteady; kt++) {
-    M3S_T(t0);
-    M3S_T(t1);
-    M3S_T(t2);
-    const int pk0 = (kbase + kt + STAGES - 1) * BK;
-    char* psb = lds + ((kt + STAGES - 1) % STAGES) * C::ST_BYTES;
-    int pky, pkx, pci0;
-    tap_of(pk0, pky, pkx, pci0);
-    const char* sA = stage_of(kt);
-#pragma unroll
-    for (int kk = 0; kk < KK; kk++) {
-      const int cur = kk & 1;
-      if (kk + 1 < KK) {
-        read_frags(cur ^ 1, sA, kk + 1);
-#pragma unroll
-        for (int j = 0; j < C::L; j++)
-          if (j * KK / C::L == kk) issue_chunk(j, pk0, psb, pky, pkx, pci0);
-        mfmas(cur);
-        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
-      } else {
-#pragma unroll
-        for (int j = 0; j < C::L; j++)
-          if (j * KK / C::L == kk) issue_chunk(j, pk0, psb, pky, pkx, pci0);
-        mfmas(cur);
-        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
-        // retire tile kt+1: tiles kt+2 .. kt+STAGES-1 (STAGES-2 of them) stay in flight
-        vm_wait<C::L * (STAGES - 2)>();
-        block_sync_lds();
-        read_frags(cur ^ 1, stage_of(kt + 1), 0);
-      }
-    }
-#ifdef M3S_GEMM_STAMPS
-    M3S_T(t3);
-    s_wait += t1 - t0;
-    s_bar += t2 - t1;
-    s_comp += t3 - t2;
-#endif
-  }
-  // tail: the last STAGES-1 tiles (nothing left to prefetch)
-  for (; kt < nk; kt++) {
-    const char* sA = stage_of(kt);
-#pragma unroll
-    for (int kk = 0; kk < KK; kk++) {
-      const int cur = kk & 1;
-      if (kk + 1 < KK) {
-        read_frags(cur ^ 1, sA, kk + 1);
-        mfmas(cur);
-      } else {
-        mfmas(cur);
-        if (kt + 1 < nk) {
-          wait_ahead(min(nk - 2 - kt, STAGES - 2));
-          block_sync_lds();
-          read_frags(cur ^ 1, stage_of(kt + 1), 0);
-        }
-      }
-    }
-  }
-  M3S_T(t_loop);
-  if constexpr (F8) {  // dequant: acc(i, j) *= col_scale[n] (n = this lane's column)
-    const float* cs_g = a.cscale + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sCscale;
-#pragma unroll
-    for (int j = 0; j < TN; j++) {
-      const int n = n0 + wn * (BN / WN) + j * 32 + fr;
-      const float sc = n < a.N ? cs_g[n] : 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; i++)
-#pragma unroll
-        for (int r = 0; r < 16; r++) acc[i][j][r] *= sc;
-    }
-  }
-
-  // ---- epilogue through LDS: f32 tile [BM][CST] ----
-  constexpr int VPR = BN / 8;                 // 8-column vectors per row
-  constexpr int NV = BM * VPR / NT;           // vectors per thread
-  constexpr int RSTEP = NT / VPR;             // rows between one thread's vectors
-  static_assert(NT % VPR == 0, "epilogue layout");
-  // Vector path: a thread owns columns [n, n+8) of rows r0 + v*RSTEP.  Its bias and, per
-  // group of EG vectors, the residual (or RoPE cos/sin) operands are loaded ahead of use —
-  // the first group before the LDS round trip — so their latency is overlapped.
-  // EG must divide NV (96-row tiles have NV = 6: groups of 4 would run past the tile into
-  // the next tile's rows)
-  constexpr int EG = NV % 4 == 0 ? 4 : NV % 3 == 0 ? 3 : NV % 2 == 0 ? 2 : 1;
-  const int ec = (tid % VPR) * 8, er0 = tid / VPR;
-  const int en = n0 + ec;
-  const int fl = EPI >= 0 ? EPI : a.flags;
-  const bool vec = EPI >= 0 ? true : (a.vec != 0);
-  const bool vec_path = vec && en < a.N;
-  float e_b[8], e_pb[8], e_x[EG][16];
-  float e_c1[8], e_pc1[8], e_mu[EG], e_rs[EG];  // LN_FOLD: c1 columns, row mean / rstd
-  // LN_FOLD: the 16 lanes of a row group own rows er0 + v·RSTEP (v < NV ≤ 16); lane v
-  // combines the statistics of row v once, the others read it by lane shuffle
-  float ln_mu = 0.f, ln_rs = 0.f;
-  static_assert(NV <= 16, "one row per lane of the group");
-  auto ln_setup = [&]() {
-    if ((fl & M3S_EPI_LN_FOLD) && (lane & 15) < NV)
-      ln_row_stats(a, g ^ a.a_xor, min(m0 + er0 + (lane & 15) * RSTEP, a.M - 1), a.K >> 7,
-                   ln_mu, ln_rs);
-  };
-  if (!SPLIT) ln_setup();
-  Epi e = make_epi(a, g);
-  e.flags = fl;
-  const bool e_rope = (fl & M3S_EPI_ROPE) && en < a.rope_cols;
-  auto e_prefetch = [&](int v0) {
-#pragma unroll
-    for (int u = 0; u < EG; u++) {
-      const int m = min(m0 + er0 + (v0 + u) * RSTEP, a.M - 1);  // rows ≥ M are not stored
-      if (fl & M3S_EPI_LN_FOLD) {  // row v0 + u's statistics, held by lane v0 + u of the row group
-        const int src = (lane & ~15) | (v0 + u);
-        e_mu[u] = __shfl(ln_mu, src, 64);
-        e_rs[u] = __shfl(ln_rs, src, 64);
-      }
-#pragma unroll
-      for (int t = 0; t < 16; t++) e_x[u][t] = 0.f;
-      if (fl & M3S_EPI_RES_F32) {
-        const float* r = reinterpret_cast<const float*>(e.R) + (int64_t)m * e.ldr + en;
-        *reinterpret_cast<float4*>(&e_x[u][0]) = *reinterpret_cast<const float4*>(r);
-        *reinterpret_cast<float4*>(&e_x[u][4]) = *reinterpret_cast<const float4*>(r + 4);
-      } else if (fl & M3S_EPI_RES_BF16) {
-        const bf16x8 r = *reinterpret_cast<const bf16x8*>(
-            reinterpret_cast<const bf16_t*>(e.R) + (int64_t)m * e.ldr + en);
-#pragma unroll
-        for (int t = 0; t < 8; t++) e_x[u][t] = bf2f(r[t]);
-      } else if (e_rope) {  // RoPE GEMMs carry no residual: cos → [0, 8), sin → [8, 16)
-        const float* tb = e.rope_tab +
-                          ((int64_t)(m % e.rope_tokens) * 2 + ((en >> 5) & 1)) * 32 + (en & 15);
-        *reinterpret_cast<float4*>(&e_x[u][0]) = *reinterpret_cast<const float4*>(tb);
-        *reinterpret_cast<float4*>(&e_x[u][4]) = *reinterpret_cast<const float4*>(tb + 4);
-        *reinterpret_cast<float4*>(&e_x[u][8]) = *reinterpret_cast<const float4*>(tb + 16);
-        *reinterpret_cast<float4*>(&e_x[u][12]) = *reinterpret_cast<const float4*>(tb + 20);
-      }
-    }
-  };
-  auto epi_setup = [&]() {
-    if (!vec_path) return;
-    int co;
-    (void)out_offset(e, m0, en, co);
-#pragma unroll
-    for (int t = 0; t < 8; t++) e_b[t] = e_pb[t] = 0.f;
-    if (e.bias) {
-      *reinterpret_cast<float4*>(&e_b[0]) = *reinterpret_cast<const float4*>(e.bias + co);
-      *reinterpret_cast<float4*>(&e_b[4]) = *reinterpret_cast<const float4*>(e.bias + co + 4);
-      if (e_rope) {
-        *reinterpret_cast<float4*>(&e_pb[0]) = *reinterpret_cast<const float4*>(e.bias + (en ^ 16));
-        *reinterpret_cast<float4*>(&e_pb[4]) =
-            *reinterpret_cast<const float4*>(e.bias + (en ^ 16) + 4);
-      }
-    }
-    if (fl & M3S_EPI_LN_FOLD) {
-      const float* c1 = a.ln_c1 + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sBias;
-      *reinterpret_cast<float4*>(&e_c1[0]) = *reinterpret_cast<const float4*>(c1 + en);
-      *reinterpret_cast<float4*>(&e_c1[4]) = *reinterpret_cast<const float4*>(c1 + en + 4);
-      if (e_rope) {
-        *reinterpret_cast<float4*>(&e_pc1[0]) = *reinterpret_cast<const float4*>(c1 + (en ^ 16));
-        *reinterpret_cast<float4*>(&e_pc1[4]) =
-            *reinterpret_cast<const float4*>(c1 + (en ^ 16) + 4);
-      }
-    }
-    e_prefetch(0);
-  };
-  if (!SPLIT) epi_setup();   // split-K: only the tile's last split needs the operands
-  M3S_T(t_e0);
-  block_sync_lds();
-  M3S_T(t_e1);
-  float* cs = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int i = 0; i < TM; i++)
-#pragma unroll
-    for (int j = 0; j < TN; j++)
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        cs[row * C::CST + wn * (BN / WN) + j * 32 + fr] = acc[i][j][r];
-      }
-  block_sync_lds();
-  M3S_T(t_e2);
-
-  if constexpr (EPI >= 0 && (EPI & M3S_EPI_DPT_OUT) != 0) {
-    // fused DPT tail: one pixel (row) per thread, all BN = 128 channels in the LDS tile
-    static_assert(BN == 128 && !SPLIT, "DPT_OUT needs the full 128-channel row in one tile");
-    const int gw = a.wmod > 0 ? g % a.wmod : g;
-    const float* w4 = a.dpt_w4 + (int64_t)gw * 512;
-    const float* b4 = a.dpt_b4 + (int64_t)gw * 4;
-    const float* cb = (EPI & M3S_EPI_BIAS) ? a.bias + (int64_t)gw * a.sBias : nullptr;
-    for (int row = tid; row < BM; row += NT) {
-      const int m = m0 + row;
-      if (m >= a.M) break;
-      float o4[4] = {b4[0], b4[1], b4[2], b4[3]};
-      const float* src = cs + row * C::CST;
-#pragma unroll 4
-      for (int c = 0; c < 128; c += 4) {
-        float4 x = *reinterpret_cast<const float4*>(src + c);
-        if (cb) {
-          x.x += cb[c];
-          x.y += cb[c + 1];
-          x.z += cb[c + 2];
-          x.w += cb[c + 3];
-        }
-        x.x = fmaxf(x.x, 0.f);
-        x.y = fmaxf(x.y, 0.f);
-        x.z = fmaxf(x.z, 0.f);
-        x.w = fmaxf(x.w, 0.f);
-#pragma unroll
-        for (int oo = 0; oo < 4; oo++)
-          o4[oo] += w4[oo * 128 + c] * x.x + w4[oo * 128 + c + 1] * x.y +
-                    w4[oo * 128 + c + 2] * x.z + w4[oo * 128 + c + 3] * x.w;
-      }
-      // reg_dense_depth('exp') + conf ('exp', conf_min): as dpt_out_kernel (vit_misc.hip)
-      const float d = sqrtf(o4[0] * o4[0] + o4[1] * o4[1] + o4[2] * o4[2]);
-      const float sc = expm1f(d) / fmaxf(d, 1e-8f);
-      float* P = a.dpt_pts + ((int64_t)g * a.M + m) * 3;
-      P[0] = o4[0] * sc;
-      P[1] = o4[1] * sc;
-      P[2] = o4[2] * sc;
-      a.dpt_conf[(int64_t)g * a.M + m] = a.dpt_conf_min + expf(o4[3]);
-    }
-    return;
-  }
-
-  if constexpr (SPLIT) {
-    // publish this split's partial tile; the tile's last split sums them all
-    __shared__ int s_last;
-    const int64_t per_b = (int64_t)a.M * a.N;
-    float* P = a.ws + (int64_t)zz * per_b;
-#pragma unroll 4
-    for (int v = 0; v < NV; v++) {
-      const int idx = v * NT + tid;
-      const int row = idx / VPR, c = (idx % VPR) * 8;
-      const int m = m0 + row, n = n0 + c;
-      if (m >= a.M || n >= a.N) continue;
-      const float* src = cs + row * C::CST + c;
-      float* dst = P + (int64_t)m * a.N + n;
-      if (vec) {
-        *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
-        *reinterpret_cast<float4*>(dst + 4) = *reinterpret_cast<const float4*>(src + 4);
-      } else {
-        for (int t = 0; t < 8 && n + t < a.N; t++) dst[t] = src[t];
-      }
-    }
-    if (!a.fused) return;  // splitk_reduce_kernel follows
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      int* ctr = a.cnt + (int64_t)g * nwg + wgid;
-      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = old == a.splits - 1;
-      if (s_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    ln_setup();
-    epi_setup();
-    const float* P0 = a.ws + (int64_t)g * a.splits * per_b;
-#pragma unroll 2
-    for (int v = 0; v < NV; v++) {
-      const int idx = v * NT + tid;
-      const int row = idx / VPR, c = (idx % VPR) * 8;
-      const int m = m0 + row, n = n0 + c;
-      if (m >= a.M || n >= a.N) continue;
-      float* dst = cs + row * C::CST + c;
-      float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < a.splits; k++) {
-        float y[8];
-        if (k == split) {  // this workgroup's own partial is still in LDS
-          *reinterpret_cast<float4*>(&y[0]) = *reinterpret_cast<const float4*>(dst);
-          *reinterpret_cast<float4*>(&y[4]) = *reinterpret_cast<const float4*>(dst + 4);
-        } else if (vec) {
-          const float* q = P0 + k * per_b + (int64_t)m * a.N + n;
-          *reinterpret_cast<float4*>(&y[0]) = *reinterpret_cast<const float4*>(q);
-          *reinterpret_cast<float4*>(&y[4]) = *reinterpret_cast<const float4*>(q + 4);
-        } else {
-          const float* q = P0 + k * per_b + (int64_t)m * a.N + n;
-#pragma unroll
-          for (int t = 0; t < 8; t++) y[t] = n + t < a.N ? q[t] : 0.f;
-        }
-#pragma unroll
-        for (int t = 0; t < 8; t++) x[t] += y[t];
-      }
-      *reinterpret_cast<float4*>(dst) = make_float4(x[0], x[1], x[2], x[3]);
-      *reinterpret_cast<float4*>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);
-    }
-    block_sync_lds();
-  }
-  if (vec_path) {
-    const float sg = (en & 16) ? 1.f : -1.f;
-    const bool has_res = fl & (M3S_EPI_RES_F32 | M3S_EPI_RES_BF16);
-    const bool rope_now = e_rope && !has_res;
-    // per group: all LDS reads first, then the math and the global stores (a ds_read issued
-    // after a global store waits for that store: the compiler cannot prove it does not
-    // alias the LDS-DMA ring — one such wait per group instead of one per vector)
-#pragma unroll
-    for (int v0 = 0; v0 < NV; v0 += EG) {
-      if (v0 > 0) e_prefetch(v0);
-      float xv[EG][8], pv[EG][8];
-#pragma unroll
-      for (int u = 0; u < EG; u++) {
-        const int row = er0 + (v0 + u) * RSTEP;
-        const float* src = cs + row * C::CST + ec;
-        *reinterpret_cast<float4*>(&xv[u][0]) = *reinterpret_cast<const float4*>(src);
-        *reinterpret_cast<float4*>(&xv[u][4]) = *reinterpret_cast<const float4*>(src + 4);
-        if (rope_now) {
-          const float* psrc = cs + row * C::CST + (ec ^ 16);
-          *reinterpret_cast<float4*>(&pv[u][0]) = *reinterpret_cast<const float4*>(psrc);
-          *reinterpret_cast<float4*>(&pv[u][4]) = *reinterpret_cast<const float4*>(psrc + 4);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < EG; u++) {
-        const int m = m0 + er0 + (v0 + u) * RSTEP;
-        if (m >= a.M) continue;
-        float* x = xv[u];
-        if (fl & M3S_EPI_LN_FOLD) {  // LN(x) W^T + b = rstd (acc - mean c1) + c2
-#pragma unroll
-          for (int t = 0; t < 8; t++) x[t] = fmaf(e_rs[u], fmaf(-e_mu[u], e_c1[t], x[t]), e_b[t]);
-          if (rope_now) {  // the partner columns' final values
-#pragma unroll
-            for (int t = 0; t < 8; t++)
-              pv[u][t] = fmaf(e_rs[u], fmaf(-e_mu[u], e_pc1[t], pv[u][t]), e_pb[t]);
-          }
-        } else {
-#pragma unroll
-          for (int t = 0; t < 8; t++) x[t] += e_b[t];
-          if (rope_now) {
-#pragma unroll
-            for (int t = 0; t < 8; t++) pv[u][t] += e_pb[t];
-          }
-        }
-        if (fl & M3S_EPI_GELU) {
-#pragma unroll
-          for (int t = 0; t < 8; t++) x[t] = gelu_erf(x[t]);
-        }
-        if (rope_now) {
-#pragma unroll
-          for (int t = 0; t < 8; t++)
-            x[t] = x[t] * e_x[u][t] + sg * pv[u][t] * e_x[u][8 + t];
-        }
-        if (has_res) {
-#pragma unroll
-          for (int t = 0; t < 8; t++) x[t] += e_x[u][t];
-        }
-        if (fl & M3S_EPI_RELU) {
-#pragma unroll
-          for (int t = 0; t < 8; t++) x[t] = fmaxf(x[t], 0.f);
-        }
-        int co;
-        const int64_t off = out_offset(e, m, en, co);
-        if (fl & M3S_EPI_OUT_F32) {
-          float* cp = reinterpret_cast<float*>(e.C) + off;
-          *reinterpret_cast<float4*>(cp) = make_float4(x[0], x[1], x[2], x[3]);
-          *reinterpret_cast<float4*>(cp + 4) = make_float4(x[4], x[5], x[6], x[7]);
-          if (fl & M3S_EPI_LN_STATS) {  // the next LayerNorm's input: bf16 copy + row stats
-            store_bf16x8(a.C2 + (int64_t)g * a.sC + off, x);
-            ln_group_stats(a, g, m, en, x);
-          }
-        } else if (fl & M3S_EPI_OUT_FP8) {
-          *reinterpret_cast<uint2*>(e.C + off) = make_uint2(pack4_fp8(x[0], x[1], x[2], x[3]),
-                                                            pack4_fp8(x[4], x[5], x[6], x[7]));
-        } else {
-          bf16x8 o;
-#pragma unroll
-          for (int t = 0; t < 8; t++) o[t] = f2bf(x[t]);
-          *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16_t*>(e.C) + off) = o;
-        }
-      }
-    }
-  } else if (!vec) {
-    const bool rope = fl & M3S_EPI_ROPE;
-    for (int v = 0; v < NV; v++) {
-      const int idx = v * NT + tid;
-      const int row = idx / VPR, c = (idx % VPR) * 8;
-      const int m = m0 + row, n = n0 + c;
-      if (m >= a.M || n >= a.N) continue;
-      const float* src = cs + row * C::CST + c;
-      const float* psrc = cs + row * C::CST + (c ^ 16);
-      for (int t = 0; t < 8 && n + t < a.N; t++) epi_one(e, src[t], rope ? psrc[t] : 0.f, m, n + t);
-    }
-  }
-#ifdef M3S_GEMM_STAMPS
-  if (tid == 0) {
-    M3S_T(t_end);
-    long long* o = g_m3s_stamps + (int64_t)blockIdx.x * 12;
-      o[8] = t_e0 - t_loop;
-      o[9] = t_e1 - t_e0;
-      o[10] = t_e2 - t_e1;
-      o[11] = t_end - t_e2;
-    o[0] = t_pro - t_start;
-    o[1] = s_wait;
-    o[2] = s_bar;
-    o[3] = s_comp;
-    o[4] = t_end - t_loop;
-    o[5] = nk;
-    o[6] = t_end - t_start;
-    o[7] = t_start;
-  }
-#endif
-}
-
-// Unfused split-K: sum the partials (fixed order) and apply the epilogue; 8 columns per
-// thread, the whole chip reducing (the fused path reduces a tile on one CU).
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
-  const int vpr = (a.N + 7) / 8;
-  const int64_t vid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int g = blockIdx.y;
-  if (vid >= (int64_t)a.M * vpr) return;
-  const int m = (int)(vid / vpr);
-  const int n = (int)(vid - (int64_t)m * vpr) * 8;
-  const int64_t per_b = (int64_t)a.M * a.N;
-  const Epi e = make_epi(a, g);
-  const float* P = a.ws + (int64_t)g * a.splits * per_b + (int64_t)m * a.N;
-  const bool rope = (a.flags & M3S_EPI_ROPE) && n < a.rope_cols;
-  float x[8], p[8];
-  if (a.vec) {
-#pragma unroll
-    for (int t = 0; t < 8; t++) x[t] = p[t] = 0.f;
-    for (int k = 0; k < a.splits; k++) {
-      const float* q = P + k * per_b;
-      const float4 u0 = *reinterpret_cast<const float4*>(q + n);
-      const float4 u1 = *reinterpret_cast<const float4*>(q + n + 4);
-      x[0] += u0.x; x[1] += u0.y; x[2] += u0.z; x[3] += u0.w;
-      x[4] += u1.x; x[5] += u1.y; x[6] += u1.z; x[7] += u1.w;
-      if (rope) {
-        const float4 w0 = *reinterpret_cast<const float4*>(q + (n ^ 16));
-        const float4 w1 = *reinterpret_cast<const float4*>(q + (n ^ 16) + 4);
-        p[0] += w0.x; p[1] += w0.y; p[2] += w0.z; p[3] += w0.w;
-        p[4] += w1.x; p[5] += w1.y; p[6] += w1.z; p[7] += w1.w;
-      }
-    }
-    epi_vec8(e, x, p, m, n);  // x now holds the stored values
-    if (a.flags & M3S_EPI_LN_STATS) {
-      store_bf16x8(a.C2 + (int64_t)g * a.sC + (int64_t)m * a.ldc + n, x);
-      ln_group_stats(a, g, m, n, x);
-    }
-  } else {
-    for (int t = 0; t < 8 && n + t < a.N; t++) {
-      float s = 0.f, ps = 0.f;
-      for (int k = 0; k < a.splits; k++) {
-        s += P[k * per_b + n + t];
-        if (rope) ps += P[k * per_b + ((n + t) ^ 16)];
-      }
-      epi_one(e, s, ps, m, n + t);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// tile configurations
-// ---------------------------------------------------------------------------------------
-// (4- and 5-stage 128x128 / 6-stage 64x128 rings were measured on the M = 768 shapes at
-// ±3 % of these — tools/gemm_depth.py — and dropped: the first-tile latency, not the ring
-// depth, bounds those blocks)
-enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7, T96 = 8, T96O2 = 9 };
-
-// Epilogue flag sets compiled as straight-line variants (8-wide vector path), per mode:
-//   GEMM: bf16 out, +RoPE, +GELU, f32 residual → f32, f32 out;  conv: bf16 out, +bf16
-//   residual, +ReLU.  Any other combination (or an unaligned shape) runs the generic
-//   run-time-flag epilogue.  Each set exists with and without bias.
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, int E,
-          bool F8 = false, bool SP = false>
-bool try_epi(Args& a, dim3 grid, hipStream_t s, int key) {
-  if (key == E) {
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, SP, E, F8>), grid,
-                       dim3(NT), 0, s, a);
-    return true;
-  }
-  if (key == (E | M3S_EPI_BIAS)) {
-    hipLaunchKernelGGL(
-        (gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, SP, E | M3S_EPI_BIAS, F8>), grid,
-        dim3(NT), 0, s, a);
-    return true;
-  }
-  return false;
-}
-
-// the same, biased set only (the LayerNorm-fold sets always carry a bias)
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, int E,
-          bool SP = false>
-bool try_epi_b(Args& a, dim3 grid, hipStream_t s, int key) {
-  if (key != (E | M3S_EPI_BIAS)) return false;
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, SP, E | M3S_EPI_BIAS>),
-                     grid, dim3(NT), 0, s, a);
-  return true;
-}
-
-// fp8 operands (GEMM mode): the epilogue sets the ViT uses — qkv / q / kv (+RoPE), fc1
-// (+GELU, fp8 out for the next fp8 GEMM), proj / fc2 (f32 residual), plain bf16 / f32
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC>
-void launch_main_f8(Args& a, dim3 grid, hipStream_t s) {
-  const int key = a.flags & ~(M3S_IN_FP8 | (a.bias ? 0 : M3S_EPI_BIAS));
-  if (a.vec) {
-    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_ROPE, true>(a, grid, s, key)) return;
-    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_GELU | M3S_EPI_OUT_FP8, true>(
-            a, grid, s, key))
-      return;
-    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, true>(
-            a, grid, s, key))
-      return;
-    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, 0, true>(a, grid, s, key)) return;
-  }
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, false, -1, true>), grid,
-                     dim3(NT), 0, s, a);
-}
-
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, bool SP = false>
-void launch_main(Args& a, dim3 grid, hipStream_t s) {
-  const int key = (a.flags & ~(M3S_PRO_RELU | (a.bias ? 0 : M3S_EPI_BIAS)));
-  if (a.vec) {
-    if (MODE == 0) {
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0, false, SP>(a, grid, s, key)) return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_ROPE, false, SP>(a, grid, s, key))
-        return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_GELU, false, SP>(a, grid, s, key))
-        return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, false,
-                  SP>(a, grid, s, key))
-        return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_OUT_F32, false, SP>(a, grid, s,
-                                                                                    key))
-        return;
-      // LayerNorm fold (the ViT blocks' norm → projection pairs): consumers qkv / q / kv
-      // (+RoPE) and fc1 (+GELU), producers the residual GEMMs and the embeddings
-      if constexpr (BN == 128 && BK == 64 && (BM == 64 || BM == 96 || BM == 128) && OCC <= 2 &&
-                    (BM != 96 || OCC == 1)) {
-        constexpr int LF = M3S_EPI_LN_FOLD, LS = M3S_EPI_LN_STATS;
-        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_ROPE, SP>(a, grid, s,
-                                                                                     key))
-          return;
-        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_GELU, SP>(a, grid, s,
-                                                                                     key))
-          return;
-        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE,
-                      LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, SP>(a, grid, s, key))
-          return;
-        if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LS | M3S_EPI_OUT_F32, SP>(a, grid, s,
-                                                                                        key))
-          return;
-      }
-    } else {
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0, false, SP>(a, grid, s, key)) return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RES_BF16, false, SP>(a, grid, s,
-                                                                                     key))
-        return;
-      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RELU, false, SP>(a, grid, s, key))
-        return;
-      if constexpr (BN == 128 && !SP)
-        if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RELU | M3S_EPI_DPT_OUT>(
-                a, grid, s, key))
-          return;
-    }
-  }
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, SP, -1>), grid,
-                     dim3(NT), 0, s, a);
-}
-
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, bool F8 = false>
-int launch(Args& a, int batch, hipStream_t s) {
-  a.tiles_m = (a.M + BM - 1) / BM;
-  a.tiles_n = (a.N + BN - 1) / BN;
-  const bool split = a.splits > 1;
-  const int64_t groups = (int64_t)batch * (split ? a.splits : 1);
-  if ((int64_t)a.tiles_m * a.tiles_n * groups >= (1ll << 31)) return M3S_ERR_TOO_LARGE;
-  dim3 grid((unsigned)(a.tiles_m * a.tiles_n * groups));
-  // tile order: the operand bytes an XCD's L2 must fetch for its contiguous chunk of T
-  // tiles — M-major touches ceil(T / tiles_n) A bands and min(T, tiles_n) B columns,
-  // N-major ceil(T / tiles_m) B columns and min(T, tiles_m) A bands; take the smaller
-  if (a.mode == 0) {
-    const int64_t T = ((int64_t)a.tiles_m * a.tiles_n * groups + 7) / 8;
-    const double band = (double)BM * a.K * 2, col = (double)BN * a.K * 2;
-    const double costM = band * std::min<int64_t>(a.tiles_m, (T + a.tiles_n - 1) / a.tiles_n + 1) +
-                         col * std::min<int64_t>(T, a.tiles_n);
-    const double costN = col * std::min<int64_t>(a.tiles_n, (T + a.tiles_m - 1) / a.tiles_m + 1) +
-                         band * std::min<int64_t>(T, a.tiles_m);
-    a.nmajor = costN < costM;
-    if (const char* e = getenv("M3S_GEMM_ORDER")) a.nmajor = atoi(e);  // tuning override
-  } else {
-    a.nmajor = 0;
-  }
-  if (split) {
-    // split-K (fused last-split epilogue): 128^2 GEMM tiles, 64x128 GEMM / conv tiles
-    constexpr bool CAN = !F8 && ((BM == 128 && BN == 128 && BK == 64) ||
-                                 (BM == 64 && BN == 128 && STAGES == 3 && OCC == 2));
-    if constexpr (CAN) {
-      if (a.mode == 0)
-        launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 0, true>(a, grid, s);
-      else if (a.flags & M3S_PRO_RELU)
-        launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 2, true>(a, grid, s);
-      else
-        launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 1, true>(a, grid, s);
-    } else {
-      return M3S_ERR_INVALID_ARG;
-    }
-    if (!a.fused) {
-      M3S_LAUNCH_CHECK();
-      const int64_t nv = (int64_t)a.M * ((a.N + 7) / 8);
-      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(m3s_div_up(nv, 256), (unsigned)batch),
-                         dim3(256), 0, s, a);
-    }
-  } else if constexpr (F8) {
-    launch_main_f8<BM, BN, BK, WM, WN, STAGES, OCC>(a, grid, s);
-  } else if (a.mode == 0) {
-    launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 0>(a, grid, s);
-  } else if (a.flags & M3S_PRO_RELU) {
-    launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 2>(a, grid, s);
-  } else {
-    launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 1>(a, grid, s);
-  }
-  M3S_LAUNCH_CHECK();
-  return M3S_OK;
-}
+using namespace m3s_gemm;
 
 // Per-shape launch choices measured on MI355X (tools/gemm_autotune.py): exact match on the
 // descriptor's (M, N, K, batch, flags, mode); everything else takes the heuristic below.
@@ -1215,7 +82,7 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 #ifdef M3S_GEMM_STAMPS
 extern "C" int m3s_debug_set_stamps(void* p) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_m3s_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -2;
+  return hipMemcpyToSymbol(HIP_SYMBOL(m3s_gemm::g_m3s_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -2;
 }
 #endif
 
@@ -1381,7 +248,8 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
         ((tiles96 >= 160 && tiles96 <= 256) || tiles96 % 256 == 0))
       cfg = T96;
   }
-  if (cfg < 1 || cfg > 9 || cfg == 4 || cfg == 5) cfg = T128;
+  if (cfg < 1 || cfg > 11 || cfg == 4 || cfg == 5) cfg = T128;
+  if (conv && (cfg == T64D || cfg == T128D)) cfg = T64;
   if (conv && d->Cin % 64 != 0) cfg = T128K32;  // tap-uniform K-tiles need Cin % BK == 0
   if (!conv && cfg == T128K32) cfg = T128;
   if (conv && d->Cin % 64 == 0 && cfg == T128K32) cfg = T128;
@@ -1401,9 +269,10 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   }
   // fused split-K: 128^2 GEMM tiles or 64x128 GEMM / conv tiles, a workspace for the f32
   // partials and one zeroed counter per (batch, tile)
-  const int bm = (cfg == T64) ? 64 : 128;
+  const int bm = (cfg == T64 || cfg == T64D) ? 64 : 128;
   const int64_t tiles_cfg = (int64_t)((d->M + bm - 1) / bm) * ((d->N + 127) / 128) * d->batch;
-  const bool split_cfg = (!conv && (cfg == T128 || cfg == T128O2 || cfg == T64)) ||
+  const bool split_cfg = (!conv && (cfg == T128 || cfg == T128O2 || cfg == T64 || cfg == T64D ||
+                                    cfg == T128D)) ||
                          (conv && cfg == T64);
   // fused (last split reduces the tile on its CU: one launch, but that CU streams all the
   // partials) vs a separate reduce kernel spread over the chip; the LayerNorm-fold epilogue
@@ -1431,6 +300,8 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     // 96 x 128 tiles (waves 1 x 4, each 96 x 32): 768-token problems tile to 8 bands
     case T96: return launch<96, 128, 64, 1, 4, 3, 1>(a, d->batch, s);
     case T96O2: return launch<96, 128, 64, 1, 4, 2, 2>(a, d->batch, s);
+    case T64D: return launch<64, 128, 64, 2, 2, 6, 1>(a, d->batch, s);
+    case T128D: return launch<128, 128, 64, 2, 2, 4, 1>(a, d->batch, s);
     default: return launch<64, 128, 64, 2, 2, 3, 2>(a, d->batch, s);
   }
 }

@@ -90,7 +90,7 @@ class SyntheticSequence:
                  lost_frames=(), tex_freq=25.0):
         dev = torch.device(device)
         self.n_frames, self.h, self.w, self.n = n_frames, h, w, h * w
-        self.device = dev
+        self.device, self.period = dev, period
         # fx = fy = 400 at 512 wide; scaled with the width for smaller runs
         self.K = syn.intrinsics(h, w)
         self.K[0, 0] = self.K[1, 1] = 400.0 * w / 512.0

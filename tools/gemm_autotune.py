@@ -23,7 +23,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "monst3r-slam_amd")]
 import bench  # noqa: E402
 from monst3r_slam_amd import model as Mdl  # noqa: E402
 
-TILES = {1: "128x128", 2: "64x128 2/CU", 7: "128x128 2/CU", 8: "96x128"}
+TILES = {1: "128x128", 2: "64x128 2/CU", 7: "128x128 2/CU", 8: "96x128",
+         10: "64x128 6-stage", 11: "128x128 4-stage"}
 SPLITS = (1, 2, 3, 4, 6, 8)
 
 
@@ -71,6 +72,9 @@ def main():
     ap.add_argument("--write-table", action="store_true")
     ap.add_argument("--graph", action="store_true", help="also the mono / symmetric shapes")
     ap.add_argument("--min-gain", type=float, default=0.03)
+    ap.add_argument("--tiles", type=lambda v: [int(t) for t in v.split(",")], default=None,
+                    help="restrict the sweep to these tile configs")
+    ap.add_argument("--gemm-only-m", type=int, default=0, help="only launch classes with this M")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     m, _ = Mdl.build(dev)
@@ -80,11 +84,15 @@ def main():
     res = []
     for key, lst in groups.items():
         M, N, K, batch, flags, mode = key
+        if args.gemm_only_m and M != args.gemm_only_m:
+            continue
         base = time_group(m, dev, lst, {})
         best = (base, None)
         tried = {}
         for tile in TILES:
-            if mode == 1 and tile == 8:
+            if mode == 1 and tile in (8, 10, 11):
+                continue
+            if args.tiles and tile not in args.tiles:
                 continue
             for sp in SPLITS:
                 for fu in ((0, 1) if sp > 1 else (0,)):
