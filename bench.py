@@ -267,6 +267,8 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
     def step():
         frames.T_WC[:n_kf] = T0
         P.shard_keyframe_features(frames, range(n_kf), model.encode, group)
+        # the newest keyframe's pointmap, fused on the tracking rank, reaches every rank
+        P.all_gather_keyframes(frames, [n_kf - 1], [0], group)
         graph = P.ShardedFactorGraph(h, h, frames, device=dev, group=group)
         graph.add_factors(ii, jj, min_match_frac=0.0)
         graph.solve_GN_rays()
@@ -297,7 +299,9 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
             "steps": steps, "edges_accepted": int(graph.ii.numel()),
             "gflop_per_pair": 3603.6, "tflops_achieved": len(ii) * 3603.6e9 * steps / el / 1e12,
             "allgather_bytes_per_rank": int(-(-len(ii) // world) * P.record_bytes(n)),
-            "sharding": f"edges round-robin over {world} rank(s), RCCL all-gather"}
+            "sharding": f"edges round-robin over {world} rank(s), RCCL all-gather; newest "
+                        f"keyframe pointmap broadcast from the tracking rank "
+                        f"({P.keyframe_record_bytes(n) / 1e6:.1f} MB)"}
 
 
 def c5_bench(model, dev, steps):

@@ -14,6 +14,7 @@
 //    right-looking Cholesky, the two triangular solves, the retraction of poses 1..P-1
 //    and the ||dx|| < delta test — all on device, no host round trip.  A device flag
 //    makes later iterations' kernels exit at once, so max_iter launches need no sync.
+#include <climits>
 #include "common.h"
 #include "sim3.h"
 
@@ -213,19 +214,68 @@ __global__ __launch_bounds__(kEdgeThreads) void gn_edge_kernel(
 }
 
 // ranks of ii/jj in sorted unique(ii ∪ jj) (gn_kernels.cu:161-170, torch::_unique +
-// searchsorted).  Single workgroup, O(M^2) over M = 2E values held in global memory.
+// searchsorted).  Single workgroup.  Keyframe ids span a small range in practice: a
+// presence bitmap over [min, min + 2^17) in LDS, a popcount prefix per 32-bit word, then
+// rank(v) = bits set below v — O(M + range / 32).  Ids spread wider than 2^17 fall back to
+// the O(M^2) first-occurrence / count-below scan.
 __global__ __launch_bounds__(kSolveThreads) void gn_rank_kernel(const int64_t* __restrict__ ii,
                                                                const int64_t* __restrict__ jj,
                                                                int E, int* __restrict__ rank_ii,
                                                                int* __restrict__ rank_jj,
                                                                int* __restrict__ flags) {
-  const int M = 2 * E;  // E <= 65535 → M < 2^17 bits = 16 KiB of LDS
-  __shared__ unsigned first_bits[(2 * 65536) / 32];
+  constexpr int kWords = (1 << 17) / 32;
+  const int M = 2 * E;  // E <= 65535
+  __shared__ unsigned bits[kWords];
+  __shared__ int prefix[kWords + 1];
+  __shared__ long long s_min, s_max;
   __shared__ int s_unique;
-  if (threadIdx.x == 0) s_unique = 0;
-  for (int wd = threadIdx.x; wd < (M + 31) / 32; wd += blockDim.x) first_bits[wd] = 0u;
+  if (threadIdx.x == 0) {
+    s_min = LLONG_MAX;
+    s_max = LLONG_MIN;
+    s_unique = 0;
+  }
   __syncthreads();
-  // pass 1: is position p the first occurrence of its value?
+  long long lo = LLONG_MAX, hi = LLONG_MIN;
+  for (int p = threadIdx.x; p < M; p += blockDim.x) {
+    const long long v = p < E ? ii[p] : jj[p - E];
+    lo = v < lo ? v : lo;
+    hi = v > hi ? v : hi;
+  }
+  atomicMin(&s_min, lo);
+  atomicMax(&s_max, hi);
+  __syncthreads();
+  const long long base = s_min;
+  if (s_max - base < (1ll << 17)) {
+    for (int w = threadIdx.x; w < kWords; w += blockDim.x) bits[w] = 0u;
+    __syncthreads();
+    for (int p = threadIdx.x; p < M; p += blockDim.x) {
+      const int o = (int)((p < E ? ii[p] : jj[p - E]) - base);
+      atomicOr(&bits[o >> 5], 1u << (o & 31));
+    }
+    __syncthreads();
+    const int nw = (int)((s_max - base) >> 5) + 1;
+    if (threadIdx.x == 0) {  // ≤ 4096 words: a serial exclusive scan is a few µs
+      int acc = 0;
+      for (int w = 0; w < nw; w++) {
+        prefix[w] = acc;
+        acc += __popc(bits[w]);
+      }
+      prefix[nw] = acc;
+      s_unique = acc;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < M; p += blockDim.x) {
+      const int o = (int)((p < E ? ii[p] : jj[p - E]) - base);
+      const int rank = prefix[o >> 5] + __popc(bits[o >> 5] & ((1u << (o & 31)) - 1u));
+      if (p < E) rank_ii[p] = rank;
+      else rank_jj[p - E] = rank;
+    }
+    if (threadIdx.x == 0) flags[2] = s_unique;
+    return;
+  }
+  // wide id range: first occurrences (reusing the bitmap over positions), then count below
+  for (int wd = threadIdx.x; wd < (M + 31) / 32; wd += blockDim.x) bits[wd] = 0u;
+  __syncthreads();
   int local_unique = 0;
   for (int p = threadIdx.x; p < M; p += blockDim.x) {
     const int64_t v = p < E ? ii[p] : jj[p - E];
@@ -235,19 +285,18 @@ __global__ __launch_bounds__(kSolveThreads) void gn_rank_kernel(const int64_t* _
       first = (u != v);
     }
     if (first) {
-      atomicOr(&first_bits[p >> 5], 1u << (p & 31));
+      atomicOr(&bits[p >> 5], 1u << (p & 31));
       local_unique++;
     }
   }
   atomicAdd(&s_unique, local_unique);
   __syncthreads();
-  // pass 2: rank = number of distinct values below v
   for (int p = threadIdx.x; p < M; p += blockDim.x) {
     const int64_t v = p < E ? ii[p] : jj[p - E];
     int rank = 0;
     for (int q = 0; q < M; q++) {
       const int64_t u = q < E ? ii[q] : jj[q - E];
-      rank += ((u < v) && ((first_bits[q >> 5] >> (q & 31)) & 1u)) ? 1 : 0;
+      rank += ((u < v) && ((bits[q >> 5] >> (q & 31)) & 1u)) ? 1 : 0;
     }
     if (p < E) rank_ii[p] = rank;
     else rank_jj[p - E] = rank;

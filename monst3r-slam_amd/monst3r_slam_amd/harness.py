@@ -72,8 +72,9 @@ class SlamLoop:
     RetrievalDatabase."""
 
     def __init__(self, model, mast3r, monst3r, h, w, device, retriever, K=None, buffer=64,
-                 cfg=None):
+                 cfg=None, group=None):
         from . import global_opt as GO
+        from . import parallel as P
         from .config import config as _cfg
         from .frontend import Tracker
         self.cfg = cfg or _cfg
@@ -82,7 +83,14 @@ class SlamLoop:
         self.h, self.w = h, w
         self.keyframes = GO.Keyframes(h, w, buffer=buffer, device=device,
                                       feat_dim=model.a.enc_dim)
-        self.graph = GO.FactorGraph(mast3r, monst3r, self.keyframes, K, device)
+        # one process per GPU (SPMD, every rank runs this loop): the backend's edge work is
+        # sharded (ShardedFactorGraph) and the keyframe pointmaps the tracking rank (0)
+        # fused or appended are broadcast before each backend step (all_gather_keyframes)
+        self.group = group
+        self.world = P._world(group)[0]
+        self.graph = (P.ShardedFactorGraph(mast3r, monst3r, self.keyframes, K, device,
+                                           group=group) if self.world > 1
+                      else GO.FactorGraph(mast3r, monst3r, self.keyframes, K, device))
         self.retriever = retriever
         self.tracker = Tracker(model, self.cfg)
         self.mode = "INIT"
@@ -126,9 +134,16 @@ class SlamLoop:
         if idx is not None:
             self.tracker.kf.T_WC.copy_(self.keyframes.T_WC[idx, 0])
 
+    def _sync(self, idx):
+        if self.world > 1:
+            from . import parallel as P
+            dirty = sorted({idx, getattr(self, "_tracked_kf", idx)})
+            P.all_gather_keyframes(self.keyframes, dirty, [0] * len(dirty), self.group)
+
     def backend(self, idx):
         """run_backend's body for keyframe idx (main_monster_slam.py:101-149)."""
         self._writeback()
+        self._sync(idx)
         r = self.cfg["retrieval"]
         kf_idx = [idx - 1 - j for j in range(min(1, idx))]
         kf_idx += self.retriever.update(self.keyframes[idx], add_after_query=True, k=r["k"],
@@ -149,6 +164,7 @@ class SlamLoop:
         if not kf_idx:
             return False
         n = self._append_keyframe(fr)
+        self._sync(n)
         ok = self.graph.add_factors([n] * len(kf_idx), kf_idx,
                                     self.cfg["reloc"]["min_match_frac"],
                                     is_reloc=self.cfg["reloc"]["strict"])

@@ -15,6 +15,11 @@ CPU tests):
                            the acceptance rule and the GN solve then run identically on
                            every rank (the GN system is tiny; replicating it avoids a
                            broadcast of the poses).
+  all_gather_keyframes     the keyframe pointmaps (X_canon, C, N, T_WC) each rank is
+                           authoritative for — the tracking rank's fused keyframes, new
+                           keyframes — all-gathered into every rank's keyframe store before
+                           the backend reads them (3.1 MB per keyframe at 384x512), so the
+                           replicated GN sees the same pointmaps everywhere
 Each all-gather moves ceil(E/world) records per rank in ONE collective (padded), i.e.
 world-1 of every world records cross xGMI once — no per-edge messages.
 """
@@ -108,6 +113,70 @@ def shard_keyframe_features(frames, idx, encode, group=None):
     for k, i in enumerate(idx):
         frames.feat[i] = feats[k]
         frames.pos[i] = pos
+
+
+def keyframe_record_bytes(n):
+    """Bytes of one packed keyframe record: X_canon f32 [n,3], C f32 [n], N i32, T_WC f32 [8]."""
+    return (3 * n + n) * 4 + 4 + 32
+
+
+def all_gather_keyframes(frames, idx, owner, group=None):
+    """Keyframes idx[k] are authoritative on rank owner[k] (the rank that tracked / fused /
+    appended them); one all-gather of padded per-rank buffers writes every keyframe's
+    X_canon, C, N and T_WC into every rank's store (and the host count mirrors).  Ranks own
+    any subset; the ownership map must be the same on every rank."""
+    world, rank = _world(group)
+    idx, owner = [int(i) for i in idx], [int(o) for o in owner]
+    if world == 1 or not idx:
+        return
+    n = frames.h * frames.w
+    rb = keyframe_record_bytes(n)
+    if len(set(owner)) == 1:
+        # one authoritative rank (the tracking rank): a broadcast, no padded slots
+        src = owner[0]
+        buf = torch.empty((len(idx), rb), dtype=torch.uint8, device=frames.X.device)
+        if rank == src:
+            for slot, k in enumerate(idx):
+                _pack_keyframe(frames, k, buf[slot], n)
+        dist.broadcast(buf, src, group=group)
+        _unpack_keyframes(frames, idx, [buf[s] for s in range(len(idx))], n)
+        return
+    per = max(sum(1 for o in owner if o == r) for r in range(world))
+    loc = torch.zeros((max(per, 1), rb), dtype=torch.uint8, device=frames.X.device)
+    mine = [k for k, o in zip(idx, owner) if o == rank]
+    for slot, k in enumerate(mine):
+        _pack_keyframe(frames, k, loc[slot], n)
+    gathered = [torch.empty_like(loc) for _ in range(world)]
+    dist.all_gather(gathered, loc, group=group)
+    slots = [0] * world
+    recs = []
+    for o in owner:
+        recs.append(gathered[o][slots[o]])
+        slots[o] += 1
+    _unpack_keyframes(frames, idx, recs, n)
+
+
+def _pack_keyframe(frames, k, rec, n):
+    rec[:16 * n] = torch.cat((frames.X[k].reshape(-1), frames.C[k].reshape(-1))).view(torch.uint8)
+    rec[16 * n:16 * n + 4] = frames.N[k:k + 1].to(torch.int32).view(torch.uint8)
+    rec[16 * n + 4:] = frames.T_WC[k].reshape(8).contiguous().view(torch.uint8)
+
+
+def _unpack_keyframes(frames, idx, recs, n):
+    counts = {}
+    for k, rec in zip(idx, recs):
+        xc = rec[:16 * n].view(torch.float32)
+        frames.X[k].copy_(xc[:3 * n].reshape(n, 3))
+        frames.C[k].copy_(xc[3 * n:].reshape(n, 1))
+        frames.N[k] = rec[16 * n:16 * n + 4].view(torch.int32)[0]
+        frames.T_WC[k].copy_(rec[16 * n + 4:].view(torch.float32).reshape(1, 8))
+        counts[k] = rec[16 * n:16 * n + 4].view(torch.int32)
+    # host mirrors of the counts (one device read for all of them)
+    if counts:
+        ks = list(counts)
+        vals = torch.cat([counts[k] for k in ks]).tolist()
+        for k, v in zip(ks, vals):
+            frames._h_N[k] = frames._h_Nu[k] = int(v)
 
 
 class ShardedFactorGraph(FactorGraph):

@@ -79,11 +79,13 @@ def test_gn_global_ids_and_not_pd(oracle, dev):
     assert torch.count_nonzero(dx) == 0
 
 
-def test_gn_global_ids_parity(oracle, dev):
+@pytest.mark.parametrize("stride", [3, 70001])
+def test_gn_global_ids_parity(oracle, dev, stride):
+    # stride 3: ids within a 2^17 range (bitmap ranks); 70001: wider (the O(M^2) fallback)
     import mast3r_slam_backends as mb
     g = syn.keyframe_graph(P=5, h=24, w=32, seed=9)
     Twc_ref = g["Twc"].copy()
-    ii_g, jj_g = g["ii"] * 3 + 100, g["jj"] * 3 + 100
+    ii_g, jj_g = g["ii"] * stride + 100, g["jj"] * stride + 100
     oracle.gauss_newton("rays", Twc_ref, g["Xs"], g["Cs"], ii_g, jj_g, g["idx"], g["valid"],
                         g["Q"], sig0=0.003, sig1=10.0, C_thresh=0.0, Q_thresh=1.5, max_iter=4,
                         delta_thresh=1e-8)

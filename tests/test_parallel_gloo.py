@@ -103,6 +103,54 @@ def test_sharded_edges_match_single_process(world):
             assert torch.all(feats[k] == float(k)), (rank, k)
 
 
+def _kf_worker(rank, world, port, q, single):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from monst3r_slam_amd import parallel as P
+    from monst3r_slam_amd.global_opt import Keyframes
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frames = Keyframes(H, W, buffer=8, device="cpu")
+        frames.n_size = 6
+        # every rank starts from its own (stale) copy; rank r is authoritative for the
+        # keyframes it owns and writes rank-tagged values into them
+        owner = [0] * 6 if single else [0, 1, 0, 0, 1 % world, 2 % world]
+        for k in range(6):
+            v = 100.0 * rank + k
+            frames.X[k] = v
+            frames.C[k] = v + 0.5
+            frames.N[k] = rank + 1
+            frames.T_WC[k] = v + 0.25
+        P.all_gather_keyframes(frames, range(6), owner)
+        q.put((rank, frames.X[:6].numpy(), frames.C[:6].numpy(), frames.N[:6].numpy(),
+               frames.T_WC[:6].numpy(), list(frames._h_N[:6]), owner))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("single", [False, True])
+@pytest.mark.parametrize("world", [2, 3])
+def test_keyframe_pointmaps_all_gathered(world, single):
+    """all_gather_keyframes: after the collective every rank holds, for every keyframe,
+    the values of the rank that owns it; one owner (the tracking rank) → a broadcast."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_kf_worker, args=(r, world, port, q, single))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, X, C, N, T, hN, owner in res:
+        for k in range(6):
+            v = 100.0 * owner[k] + k
+            assert (X[k] == v).all() and (C[k] == v + 0.5).all(), (rank, k)
+            assert (T[k] == v + 0.25).all() and N[k] == owner[k] + 1 and hN[k] == owner[k] + 1
+
+
 def test_pack_roundtrip():
     from monst3r_slam_amd import parallel as P
     n = H * W
