@@ -63,9 +63,11 @@ const TunedShape kTuned[] = {
 
 const TunedShape* tuned_for(const m3s_gemm_desc* d) {
   static const bool off = getenv("M3S_GEMM_NO_TABLE") != nullptr;
+  static const int maxcfg = getenv("M3S_GEMM_TABLE_MAXCFG") ? atoi(getenv("M3S_GEMM_TABLE_MAXCFG"))
+                                                            : 99;  // A/B knob
   if (off) return nullptr;
   for (const TunedShape& t : kTuned)
-    if (t.M == d->M && t.N == d->N && t.K == d->K && t.batch == d->batch && t.flags == d->flags &&
+    if (t.cfg <= maxcfg && t.M == d->M && t.N == d->N && t.K == d->K && t.batch == d->batch && t.flags == d->flags &&
         t.mode == d->mode)
       return &t;
   return nullptr;

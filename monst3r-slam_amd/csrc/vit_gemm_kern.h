@@ -61,6 +61,7 @@ struct Args {
   int ct_s, ct_cout, ct_gw;
   int tiles_m, tiles_n;
   int nmajor;              // tile order within a group (see gemm_kernel)
+  int group_m;             // > 0: grouped order, group_m M-bands per group (see gemm_kernel)
   int splits;
   int vec;                 // 8-wide vector epilogue allowed (alignment / N % 8 checked on host)
   float* ws;               // split-K partials [batch*splits][M][N]
@@ -417,10 +418,25 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
     const int q = total / 8, r = total % 8, xcd = orig % 8;
     wid_lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
   }
+  // split-K keeps split-major ids: an XCD's contiguous chunk then holds ONE K-slice of a
+  // run of tiles, whose A / B slices fit its 4 MB L2 (measured: putting a tile's slices on
+  // one XCD instead — same-XCD slab reads for the reducer — fetched more from beyond L2
+  // than it saved, tools/gemm_split_probe.py)
   const int zz = wid_lin / nwg;
   const int wgid = wid_lin - zz * nwg;
   int tm, tn;
-  if (a.nmajor) {
+  if (a.group_m > 0) {
+    // grouped order: runs of group_m M-bands swept column by column, so an XCD's
+    // contiguous chunk of tiles is a compact group_m x (chunk / group_m) block (fewer
+    // distinct A bands + B columns fetched into its L2 than one row or column of tiles)
+    const int per_group = a.group_m * a.tiles_n;
+    const int grp = wgid / per_group;
+    const int first_m = grp * a.group_m;
+    const int gsz = min(a.tiles_m - first_m, a.group_m);
+    const int in = wgid - grp * per_group;
+    tm = first_m + in % gsz;
+    tn = in / gsz;
+  } else if (a.nmajor) {
     tn = wgid / a.tiles_m;
     tm = wgid - tn * a.tiles_m;
   } else {
@@ -875,33 +891,47 @@ __global__ __launch_bounds__(NT, OCC) void gemm_kernel(Args a) {
     ln_setup();
     epi_setup();
     const float* P0 = a.ws + (int64_t)g * a.splits * per_b;
-#pragma unroll 2
-    for (int v = 0; v < NV; v++) {
-      const int idx = v * NT + tid;
-      const int row = idx / VPR, c = (idx % VPR) * 8;
-      const int m = m0 + row, n = n0 + c;
-      if (m >= a.M || n >= a.N) continue;
-      float* dst = cs + row * C::CST + c;
-      float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < a.splits; k++) {
-        float y[8];
+    // slab by slab, all of this thread's vectors of a slab in flight at once (one L2
+    // round trip per slab instead of one per vector); the sum stays in split order
+    float xs[NV][8];
+#pragma unroll
+    for (int v = 0; v < NV; v++)
+#pragma unroll
+      for (int t = 0; t < 8; t++) xs[v][t] = 0.f;
+    for (int k = 0; k < a.splits; k++) {
+      float ys[NV][8];
+#pragma unroll
+      for (int v = 0; v < NV; v++) {
+        const int idx = v * NT + tid;
+        const int row = idx / VPR, c = (idx % VPR) * 8;
+        const int m = m0 + row, n = n0 + c;
+        const float* src = cs + row * C::CST + c;
         if (k == split) {  // this workgroup's own partial is still in LDS
-          *reinterpret_cast<float4*>(&y[0]) = *reinterpret_cast<const float4*>(dst);
-          *reinterpret_cast<float4*>(&y[4]) = *reinterpret_cast<const float4*>(dst + 4);
-        } else if (vec) {
+          *reinterpret_cast<float4*>(&ys[v][0]) = *reinterpret_cast<const float4*>(src);
+          *reinterpret_cast<float4*>(&ys[v][4]) = *reinterpret_cast<const float4*>(src + 4);
+        } else if (m < a.M && vec && n < a.N) {
           const float* q = P0 + k * per_b + (int64_t)m * a.N + n;
-          *reinterpret_cast<float4*>(&y[0]) = *reinterpret_cast<const float4*>(q);
-          *reinterpret_cast<float4*>(&y[4]) = *reinterpret_cast<const float4*>(q + 4);
+          *reinterpret_cast<float4*>(&ys[v][0]) = *reinterpret_cast<const float4*>(q);
+          *reinterpret_cast<float4*>(&ys[v][4]) = *reinterpret_cast<const float4*>(q + 4);
         } else {
           const float* q = P0 + k * per_b + (int64_t)m * a.N + n;
 #pragma unroll
-          for (int t = 0; t < 8; t++) y[t] = n + t < a.N ? q[t] : 0.f;
+          for (int t = 0; t < 8; t++) ys[v][t] = (m < a.M && n + t < a.N) ? q[t] : 0.f;
         }
-#pragma unroll
-        for (int t = 0; t < 8; t++) x[t] += y[t];
       }
-      *reinterpret_cast<float4*>(dst) = make_float4(x[0], x[1], x[2], x[3]);
-      *reinterpret_cast<float4*>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);
+#pragma unroll
+      for (int v = 0; v < NV; v++)
+#pragma unroll
+        for (int t = 0; t < 8; t++) xs[v][t] += ys[v][t];
+    }
+    block_sync_lds();  // every own-slab LDS read above is done before the overwrite
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      const int idx = v * NT + tid;
+      const int row = idx / VPR, c = (idx % VPR) * 8;
+      float* dst = cs + row * C::CST + c;
+      *reinterpret_cast<float4*>(dst) = make_float4(xs[v][0], xs[v][1], xs[v][2], xs[v][3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(xs[v][4], xs[v][5], xs[v][6], xs[v][7]);
     }
     block_sync_lds();
   }
@@ -1182,9 +1212,25 @@ int launch(Args& a, int batch, hipStream_t s) {
     const double costN = col * std::min<int64_t>(a.tiles_n, (T + a.tiles_m - 1) / a.tiles_m + 1) +
                          band * std::min<int64_t>(T, a.tiles_m);
     a.nmajor = costN < costM;
-    if (const char* e = getenv("M3S_GEMM_ORDER")) a.nmajor = atoi(e);  // tuning override
+    // grouped order: a chunk of T tiles as G bands x ceil(T / G) columns
+    double best = std::min(costM, costN);
+    a.group_m = 0;
+    for (int G = 2; G < a.tiles_m && G <= 16; G++) {
+      if (T > (int64_t)G * a.tiles_n) break;
+      const double c = band * G + col * (double)((T + G - 1) / G);
+      if (c < 0.9 * best) {
+        best = c;
+        a.group_m = G;
+      }
+    }
+    if (const char* e = getenv("M3S_GEMM_ORDER")) {  // tuning override: 0 / 1 / -G
+      const int v = atoi(e);
+      a.nmajor = v == 1;
+      a.group_m = v < 0 ? -v : 0;
+    }
   } else {
     a.nmajor = 0;
+    a.group_m = 0;
   }
   if (split) {
     // split-K (fused last-split epilogue): 128^2 GEMM tiles, 64x128 GEMM / conv tiles

@@ -12,7 +12,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmonst3r_slam_amd.so")
+LIB_PATH = os.environ.get("M3S_LIB_PATH") or os.path.join(_HERE, "libmonst3r_slam_amd.so")  # A/B builds
 HEADER = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "monst3r_slam_amd.h"))
 
 _P = ctypes.c_void_p

@@ -38,14 +38,19 @@ def timed(fn, reps=20):
 
 
 def main():
+    only = None
+    if len(sys.argv) > 1:   # e.g. "1:1:0,1:4:0" = (tile, splits, fused) list, fc2 shape, bias
+        only = [tuple(int(v) for v in c.split(":")) for c in sys.argv[1].split(",")]
     for (M, N, K) in ((768, 1024, 4096), (768, 1024, 1024)):
+        if only and K != 4096:
+            continue
         A = torch.randn(M, K, device=dev).bfloat16()
         B = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
         bias = torch.randn(N, device=dev)
         x = torch.randn(M, N, device=dev)
         C2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         stats = torch.empty(M, N // 128, 2, device=dev)
-        for epi in ("bias", "ln_stats"):
+        for epi in (("bias",) if only else ("bias", "ln_stats")):
             def run():
                 if epi == "bias":
                     ops.gemm(A, B, C2, M, N, K, bias=bias, flags=_lib.EPI_BIAS)
@@ -55,6 +60,8 @@ def main():
             for tile in (2, 10, 1, 11, 7):
                 for sp in (1, 2, 3, 4, 6, 8):
                     for fu in ((0, 1) if sp > 1 else (0,)):
+                        if only and (tile, sp, fu) not in only:
+                            continue
                         os.environ.update(M3S_GEMM_TILE=str(tile), M3S_GEMM_SPLITS=str(sp),
                                           M3S_GEMM_FUSED=str(fu))
                         try:
