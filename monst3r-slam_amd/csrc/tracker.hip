@@ -15,6 +15,7 @@
 // kernels) it stops with a consistent state (pose after the last completed iteration) and
 // the finish launch runs the remaining iterations in one 1024-thread workgroup; info[3]
 // reports it.  A timeout is never a Cholesky failure.
+#include <algorithm>
 #include "common.h"
 #include "sim3.h"
 
@@ -179,16 +180,36 @@ __device__ __forceinline__ void track_points(const float* T, const TrackParams& 
   }
 }
 
-// wave butterfly + LDS: the workgroup's 36 sums → out[0..35] (threads < kAcc write)
+// Reduce-scatter of the 36 sums over a wave: each butterfly step halves the values a lane
+// keeps (the lane's bit picks the half) and adds the partner's copy of that half — 32 + 16
+// + 8 + 4 + 2 + 1 shuffles for the (zero-padded) 64 values instead of 36 x 6.  Lane l < 36
+// then holds the wave's sum of value l (fixed order: deterministic).
+template <typename F>
+__device__ __forceinline__ F wave_reduce_scatter36(const F* acc) {
+  const int lane = threadIdx.x & 63;
+  F v[64];
+#pragma unroll
+  for (int j = 0; j < 64; j++) v[j] = j < kAcc ? acc[j] : F(0);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const bool hi = (lane & o) != 0;
+#pragma unroll
+    for (int j = 0; j < o; j++) {
+      const F keep = hi ? v[j + o] : v[j];
+      const F send = hi ? v[j] : v[j + o];
+      v[j] = keep + __shfl_xor(send, o, 64);
+    }
+  }
+  return v[0];   // lane l: value index l (bit k of l chose the half at step 2^k)
+}
+
+// the workgroup's 36 sums → out[0..35] (threads < kAcc write): per-wave reduce-scatter,
+// then the waves' rows summed in wave order through LDS
 template <int NT>
 __device__ __forceinline__ void block_partial(const float* acc, float* out) {
-  __shared__ float red[NT / M3S_WAVE][kAcc];
+  __shared__ float red[NT / M3S_WAVE][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int l = 0; l < kAcc; l++) {
-    const float v = m3s_wave_sum(acc[l]);
-    if (lane == 0) red[wid][l] = v;
-  }
+  red[wid][lane] = wave_reduce_scatter36<float>(acc);
   __syncthreads();
   if (threadIdx.x < kAcc) {
     float v = red[0][threadIdx.x];
@@ -243,37 +264,36 @@ __global__ __launch_bounds__(kThreads) void track_iter_kernel(
   track_solve(st, partial, (int)gridDim.x, rel_error, delta_norm);
 }
 
-// f64 reduction of nblocks partial rows in fixed order (deterministic): every thread of
-// the workgroup takes part; the 36 sums land in sacc (shared)
+// f64 reduction of nblocks partial rows in fixed order (deterministic; every workgroup
+// that runs it gets the same bits): thread (value l, group g) of the first 7 x 36 threads
+// sums rows g, g + 7, ... of column l — all its loads in flight at once — then the 7 group
+// sums of each value are added in group order.  The 36 sums land in sacc (shared).
 __device__ void reduce_partials(const float* partial, int nblocks, double* sacc) {
+  constexpr int G = kThreads / kAcc;   // 7
   const int tid = threadIdx.x;
-  __shared__ double tmp[kThreads / M3S_WAVE][kAcc];
-  // all 36 values of a partial row are loaded before any reduction (one round of L2
-  // latency instead of 36); per-l summation order unchanged: rows b = tid, tid + 256, ...,
-  // then the wave butterfly, then the waves in order
-  double v[kAcc];
-#pragma unroll
-  for (int l = 0; l < kAcc; l++) v[l] = 0.0;
-  for (int b = tid; b < nblocks; b += kThreads) {
-    float r[kAcc];
-    const float4* row = reinterpret_cast<const float4*>(partial + (size_t)b * kAcc);
-#pragma unroll
-    for (int q = 0; q < kAcc / 4; q++) {
-      const float4 f = row[q];
-      r[4 * q] = f.x; r[4 * q + 1] = f.y; r[4 * q + 2] = f.z; r[4 * q + 3] = f.w;
+  __shared__ double tmp[G][kAcc];
+  if (tid < G * kAcc) {
+    const int l = tid % kAcc, g = tid / kAcc;
+    double v = 0.0;
+    int b = g;
+    for (; b + 3 * G < nblocks; b += 4 * G) {
+      const float r0 = partial[(size_t)b * kAcc + l];
+      const float r1 = partial[(size_t)(b + G) * kAcc + l];
+      const float r2 = partial[(size_t)(b + 2 * G) * kAcc + l];
+      const float r3 = partial[(size_t)(b + 3 * G) * kAcc + l];
+      v += (double)r0;
+      v += (double)r1;
+      v += (double)r2;
+      v += (double)r3;
     }
-#pragma unroll
-    for (int l = 0; l < kAcc; l++) v[l] += (double)r[l];
-  }
-#pragma unroll
-  for (int l = 0; l < kAcc; l++) {
-    const double t = m3s_wave_sum_d(v[l]);
-    if ((tid & 63) == 0) tmp[tid >> 6][l] = t;
+    for (; b < nblocks; b += G) v += (double)partial[(size_t)b * kAcc + l];
+    tmp[g][l] = v;
   }
   __syncthreads();
   if (tid < kAcc) {
     double t = 0.0;
-    for (int w = 0; w < kThreads / M3S_WAVE; w++) t += tmp[w][tid];
+#pragma unroll
+    for (int g = 0; g < G; g++) t += tmp[g][tid];
     sacc[tid] = t;
   }
   __syncthreads();
@@ -359,23 +379,38 @@ __device__ void track_solve(TrackState* st, const float* partial, int nblocks, f
 
 // All Gauss-Newton iterations in ONE launch: nb co-resident workgroups (nb <= 256, a few
 // registers' worth of occupancy, so they fit beside whatever else runs) accumulate their
-// points' partial rows, meet at a grid barrier (monotonic agent-scope counter), then EVERY
-// workgroup reduces the same partials in the same order and takes the same step — the
-// pose never needs a broadcast and the next iteration starts straight away.  Partials
-// are double-buffered by iteration parity (a workgroup can be at most one barrier ahead).
-// Exit: convergence, Cholesky failure, max_iters, or a barrier wait beyond `spin_limit`
-// polls (~0.27 s at the default 2^22; co-residency broken) — that workgroup raises
-// st->abort, every other workgroup sees it in its own wait (or at entry, if it only got a
-// CU after the others left) and leaves too.  No workgroup can pass the barrier that timed
-// out, so workgroup 0 still holds the pose after the last completed iteration and writes
-// it back with done = 0; track_finish_kernel then runs the remaining iterations.
+// points' 36 sums (per-wave reduce-scatter), publish them as tagged 8-byte granules
+// (write-through atomic stores: the data is the flag — no fence, no barrier counter), and
+// EVERY workgroup sweeps all granules until each carries this iteration's tag, sums them in
+// the same fixed order and takes the same step — the pose never needs a broadcast and the
+// next iteration starts straight away.  Granule slots alternate with the iteration parity
+// (a workgroup can be at most one iteration ahead) and are zeroed per call (memset node).
+// tools/track_bench.py --stamps: 38 → 11 µs per iteration at 384x512 (the fence-ordered
+// barrier + a shuffle reduction per value were 27 µs of it).
+// Exit: convergence, Cholesky failure, max_iters, or a sweep beyond `spin_limit` polls
+// (co-residency broken) — that workgroup raises st->abort, every other workgroup sees it in
+// its own sweep (or at entry, if it only got a CU after the others left) and leaves too.  No
+// workgroup can complete the iteration that timed out, so workgroup 0 still holds the pose
+// after the last completed iteration and writes it back with done = 0;
+// track_finish_kernel then runs the remaining iterations.
 // `abort_at` >= 0 forces that exit at iteration abort_at (tests of the recovery path).
+#ifdef M3S_TRACK_STAMPS
+// debug build (tools/track_bench.py --stamps): workgroup 0, lane 0, s_memrealtime (100 MHz)
+// at each phase boundary of the first 8 iterations
+__device__ long long g_track_stamps[8 * 8];
+#define M3S_TS(it, ph) \
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (it) < 8) \
+    g_track_stamps[(it) * 8 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime();
+#else
+#define M3S_TS(it, ph)
+#endif
+
 template <int MODE>
 __global__ __launch_bounds__(kThreads) void track_persistent_kernel(
     TrackState* __restrict__ st, TrackParams prm, const float* __restrict__ K,
     const float* __restrict__ Xf, const float* __restrict__ Xk, const float* __restrict__ Qk,
     const uint8_t* __restrict__ valid, const float* __restrict__ meas_k,
-    const uint8_t* __restrict__ valid_meas, int64_t n, float* __restrict__ partial,
+    const uint8_t* __restrict__ valid_meas, int64_t n, unsigned long long* __restrict__ gran,
     int max_iters, float rel_error, float delta_norm, long spin_limit, int abort_at) {
   if (MODE == TRACK_CALIB) {
     prm.fx = K[0];
@@ -383,65 +418,99 @@ __global__ __launch_bounds__(kThreads) void track_persistent_kernel(
     prm.cx = K[2];
     prm.cy = K[5];
   }
+  constexpr int G = kThreads / kAcc;                      // 7 row groups per value
+  constexpr int R = (kPersistentBlocks + G - 1) / G;      // rows per (value, group) thread
   __shared__ float sT[8];
-  __shared__ int s_status;
+  __shared__ float s_row[kAcc];
+  __shared__ double tmp[G][kAcc];
   __shared__ double sacc[kAcc];
+  __shared__ int s_status;
   const int nb = gridDim.x;
-  unsigned* bar = &st->ticket;
+  const int tid = threadIdx.x;
   float T[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) T[i] = st->T[i];
   double old_cost = st->old_cost;
   int it = 0, status = 0;
-  if (threadIdx.x == 0)
+  if (tid == 0)
     s_status = __hip_atomic_load(&st->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 3 : 0;
   __syncthreads();
   if (s_status == 3) return;  // started after the others gave up: nothing to contribute
   for (; it < max_iters; it++) {
+    M3S_TS(it, 0);
     float acc[kAcc];
 #pragma unroll
     for (int l = 0; l < kAcc; l++) acc[l] = 0.f;
     track_points<MODE>(T, prm, Xf, Xk, Qk, valid, meas_k, valid_meas, n, acc,
-                       (int64_t)blockIdx.x * kThreads + threadIdx.x, (int64_t)nb * kThreads);
-    float* slot = partial + (size_t)(it & 1) * nb * kAcc;
-    block_partial<kThreads>(acc, slot + blockIdx.x * kAcc);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                       (int64_t)blockIdx.x * kThreads + tid, (int64_t)nb * kThreads);
+    M3S_TS(it, 1);
+    block_partial<kThreads>(acc, s_row);
     __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      int timeout = it == abort_at;
-      if (!timeout) {
-        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned target = (unsigned)(it + 1) * (unsigned)nb;
-        for (long spins = 0;
-             __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;
-             spins++) {
-          __builtin_amdgcn_s_sleep(2);
-          if (spins > spin_limit ||
-              __hip_atomic_load(&st->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            timeout = 1;
-            break;
-          }
+    M3S_TS(it, 2);
+    // publish the 36 sums as granules {tag = iteration + 1, value}: the data is the flag —
+    // one 8-byte relaxed agent-scope atomic store each (write-through), no fence, no counter
+    // (cdna_hip_programming.md §6 Guideline 16, R2).  Slots alternate with the iteration
+    // parity: a workgroup can be at most one iteration ahead of the slowest reader.
+    unsigned long long* gslot = gran + (size_t)(it & 1) * kPersistentBlocks * kAcc;
+    const unsigned long long tag = (unsigned long long)(it + 1) << 32;
+    const bool forced = it == abort_at;
+    if (tid < kAcc && !forced)
+      __hip_atomic_store(&gslot[(size_t)blockIdx.x * kAcc + tid],
+                         tag | __builtin_bit_cast(unsigned, s_row[tid]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    // sweep: thread (value l, group g) re-reads its rows g, g + 7, ... until every tag is this
+    // iteration's, then sums them in row order (f64) — the same bits in every workgroup
+    int timeout = forced ? 1 : 0;
+    if (tid < G * kAcc && !forced) {
+      const int l = tid % kAcc, g = tid / kAcc;
+      unsigned long long x[R];
+      for (long spins = 0;; spins++) {
+        bool ok = true;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const int b = g + r * G;
+          x[r] = b < nb ? __hip_atomic_load(&gslot[(size_t)b * kAcc + l], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)
+                        : tag;
+          ok = ok && ((x[r] & 0xffffffff00000000ull) == tag);
         }
+        if (ok) break;
+        if (spins >= spin_limit ||
+            __hip_atomic_load(&st->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          timeout = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      if (timeout)
-        __hip_atomic_store(&st->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_status = timeout ? 3 : 0;
+      double v = 0.0;
+#pragma unroll
+      for (int r = 0; r < R; r++)
+        if (g + r * G < nb) v += (double)__builtin_bit_cast(float, (unsigned)x[r]);
+      tmp[g][l] = v;
     }
-    __syncthreads();
-    if (s_status == 3) {
+    if (__syncthreads_or(timeout)) {
+      if (tid == 0) __hip_atomic_store(&st->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       status = 3;
       break;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    reduce_partials(slot, nb, sacc);
-    if (threadIdx.x == 0) {
+    M3S_TS(it, 3);
+    if (tid < kAcc) {
+      double t = 0.0;
+#pragma unroll
+      for (int g = 0; g < G; g++) t += tmp[g][tid];
+      sacc[tid] = t;
+    }
+    __syncthreads();
+    M3S_TS(it, 4);
+    if (tid == 0) {
       const int r = gn_step(sacc, T, &old_cost, rel_error, delta_norm);
+      M3S_TS(it, 5);
       s_status = r;
       if (r != 2)
         for (int i = 0; i < 8; i++) sT[i] = T[i];
     }
     __syncthreads();
+    M3S_TS(it, 6);
     status = s_status;
     if (status == 2) break;
 #pragma unroll
@@ -451,7 +520,7 @@ __global__ __launch_bounds__(kThreads) void track_persistent_kernel(
       break;
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (blockIdx.x == 0 && tid == 0) {
     for (int i = 0; i < 8; i++) st->T[i] = T[i];
     st->old_cost = old_cost;
     st->iters = it;
@@ -548,13 +617,14 @@ __global__ __launch_bounds__(kFinishThreads) void track_finish_kernel(
 }
 
 struct Layout {
-  size_t state, partial, total;
+  size_t gran, state, partial, total;
 };
 Layout layout() {
   Layout L;
-  L.state = 0;
-  L.partial = 512;
-  L.total = 512 + sizeof(float) * kBlocks * kAcc;
+  L.gran = 0;  // zeroed per call (a memset node): 2 parity slots of 256 x 36 granules
+  L.state = sizeof(unsigned long long) * 2 * kPersistentBlocks * kAcc;
+  L.partial = L.state + 512;
+  L.total = L.partial + sizeof(float) * kBlocks * kAcc;
   return L;
 }
 
@@ -573,22 +643,27 @@ int run_track(const float* Twc_k, const float* Twc_f, const float* Xf, const flo
   char* w = reinterpret_cast<char*>(ws);
   TrackState* st = reinterpret_cast<TrackState*>(w + L.state);
   float* partial = reinterpret_cast<float*>(w + L.partial);
+  unsigned long long* gran = reinterpret_cast<unsigned long long*>(w + L.gran);
   hipLaunchKernelGGL(track_init_kernel, dim3(1), dim3(64), 0, s, Twc_k, Twc_f, st);
   M3S_LAUNCH_CHECK();
   const char* e = getenv("M3S_TRACK_PERSISTENT");  // A/B: 0 = one launch per iteration
   if (!e || atoi(e) != 0) {
     int nb = (int)((n + kThreads - 1) / kThreads);
     if (nb > kPersistentBlocks) nb = kPersistentBlocks;
+    if (const char* b = getenv("M3S_TRACK_BLOCKS"))  // tuning knob (tools/track_bench.py)
+      nb = std::max(1, std::min(nb, atoi(b)));
     // debug knobs for the co-residency recovery path (tests): barrier poll limit, forced
     // abort at a given iteration
     const char* sl = getenv("M3S_TRACK_SPIN_LIMIT");
     const long spin_limit = sl ? atol(sl) : (1l << 22);
     const char* ab = getenv("M3S_TRACK_ABORT_AT");
     const int abort_at = ab ? atoi(ab) : -1;
-    if (max_iters > 0)
+    if (max_iters > 0) {
+      M3S_HIP_CHECK(hipMemsetAsync(gran, 0, L.state - L.gran, s));
       hipLaunchKernelGGL(track_persistent_kernel<MODE>, dim3(nb), dim3(kThreads), 0, s, st, prm,
-                         K, Xf, Xk, Qk, valid, meas_k, valid_meas, n, partial, max_iters,
+                         K, Xf, Xk, Qk, valid, meas_k, valid_meas, n, gran, max_iters,
                          rel_error, delta_norm, spin_limit, abort_at);
+    }
     M3S_LAUNCH_CHECK();
   } else {
     int nb = (int)((n + kThreads - 1) / kThreads);
@@ -608,6 +683,13 @@ int run_track(const float* Twc_k, const float* Twc_f, const float* Xf, const flo
 }
 
 }  // namespace
+
+#ifdef M3S_TRACK_STAMPS
+extern "C" int m3s_debug_track_stamps(long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_track_stamps), sizeof(long long) * 64) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif
 
 extern "C" size_t m3s_track_workspace_bytes(int64_t n) {
   (void)n;
