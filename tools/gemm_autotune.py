@@ -24,7 +24,7 @@ import bench  # noqa: E402
 from monst3r_slam_amd import model as Mdl  # noqa: E402
 
 TILES = {1: "128x128", 2: "64x128 2/CU", 7: "128x128 2/CU", 8: "96x128",
-         10: "64x128 6-stage", 11: "128x128 4-stage"}
+         10: "64x128 6-stage", 11: "128x128 4-stage", 12: "128x128 8 waves"}
 SPLITS = (1, 2, 3, 4, 6, 8)
 
 
