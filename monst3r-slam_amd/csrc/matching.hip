@@ -8,6 +8,7 @@
 // Layout: one lane per query pixel, 256-lane workgroups (4 waves), grid.y = batch.
 // Unlike the reference (16-thread blocks, no tail guard, matching_kernels.cu:36,131,
 // 290-293) any n is accepted.
+#include <stdlib.h>
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -158,14 +159,28 @@ __device__ __forceinline__ _Float16 desc_score(const _Float16* __restrict__ q,
   return score;
 }
 
-template <int F>
+// TILE2D: a workgroup takes a 16x16 tile of query pixels (n == h*w) instead of 256
+// consecutive pixels of one row: the candidate windows of a tile's queries overlap far
+// more (the union of the 31x31-pixel level-1 windows is 46x46 pixels instead of 31x286),
+// so their descriptor rows are re-read from L1/L2 instead of fetched again; consecutive
+// workgroups are neighbouring tiles of one direction.  Per-query work and results unchanged.
+template <int F, bool TILE2D>
 __global__ __launch_bounds__(kBlock) void refine_matches_kernel(
     const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
     const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w, int64_t n,
     int fdim, int radius, int dilation_max) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  int64_t i;
+  if constexpr (TILE2D) {
+    const int tiles_w = (w + 15) >> 4;
+    const int tx = blockIdx.x % tiles_w, ty = blockIdx.x / tiles_w;
+    const int px = tx * 16 + (threadIdx.x & 15), py = ty * 16 + (threadIdx.x >> 4);
+    if (px >= w || py >= h) return;
+    i = (int64_t)py * w + px;
+  } else {
+    i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+  }
   const int64_t b = blockIdx.y;
-  if (i >= n) return;
   const int64_t q = b * n + i;
   constexpr int FMAX = F > 0 ? F : 64;
   _Float16 qd[FMAX];
@@ -353,16 +368,27 @@ extern "C" int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21,
   if (b == 0 || n == 0) return M3S_OK;
   if (!d_D11 || !d_D21 || !d_p1 || !d_p1_new) return M3S_ERR_INVALID_ARG;
   if (fdim > 64 || b > 65535) return M3S_ERR_TOO_LARGE;
-  dim3 grid(m3s_div_up(n, kBlock), (unsigned)b);
   const _Float16* D11 = reinterpret_cast<const _Float16*>(d_D11);
   const _Float16* D21 = reinterpret_cast<const _Float16*>(d_D21);
   const bool aligned = ((uintptr_t)d_D11 % 16 == 0) && ((uintptr_t)d_D21 % 16 == 0);
+  static const bool rows = getenv("M3S_REFINE_ROWS") != nullptr;  // A/B: 1-D row blocks
+  if (fdim == 24 && aligned && n == h * w && !rows) {
+    dim3 grid2((unsigned)(m3s_div_up(w, 16) * m3s_div_up(h, 16)), (unsigned)b);
+    hipLaunchKernelGGL((refine_matches_kernel<24, true>), grid2, dim3(kBlock), 0,
+                       m3s_stream(stream), D11, D21, d_p1, d_p1_new, (int)h, (int)w, n, 24,
+                       radius, dilation_max);
+    M3S_LAUNCH_CHECK();
+    return M3S_OK;
+  }
+  dim3 grid(m3s_div_up(n, kBlock), (unsigned)b);
   if (fdim == 24 && aligned) {
-    hipLaunchKernelGGL(refine_matches_kernel<24>, grid, dim3(kBlock), 0, m3s_stream(stream),
-                       D11, D21, d_p1, d_p1_new, (int)h, (int)w, n, 24, radius, dilation_max);
+    hipLaunchKernelGGL((refine_matches_kernel<24, false>), grid, dim3(kBlock), 0,
+                       m3s_stream(stream), D11, D21, d_p1, d_p1_new, (int)h, (int)w, n, 24,
+                       radius, dilation_max);
   } else {
-    hipLaunchKernelGGL(refine_matches_kernel<0>, grid, dim3(kBlock), 0, m3s_stream(stream), D11,
-                       D21, d_p1, d_p1_new, (int)h, (int)w, n, (int)fdim, radius, dilation_max);
+    hipLaunchKernelGGL((refine_matches_kernel<0, false>), grid, dim3(kBlock), 0,
+                       m3s_stream(stream), D11, D21, d_p1, d_p1_new, (int)h, (int)w, n,
+                       (int)fdim, radius, dilation_max);
   }
   M3S_LAUNCH_CHECK();
   return M3S_OK;

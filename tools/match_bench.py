@@ -13,19 +13,20 @@ dev = torch.device("cuda:0")
 lib = _lib.load()
 h, w, F = 384, 512, 24
 n = h * w
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 g = torch.Generator(device=dev).manual_seed(0)
-D11 = torch.nn.functional.normalize(torch.randn(1, h, w, F, device=dev, generator=g), dim=-1).half()
-D21 = torch.nn.functional.normalize(torch.randn(1, n, F, device=dev, generator=g), dim=-1).half()
+D11 = torch.nn.functional.normalize(torch.randn(B, h, w, F, device=dev, generator=g), dim=-1).half()
+D21 = torch.nn.functional.normalize(torch.randn(B, n, F, device=dev, generator=g), dim=-1).half()
 # matches near the identity (as after iter_proj on consecutive frames): local windows overlap
 yy, xx = torch.meshgrid(torch.arange(h, device=dev), torch.arange(w, device=dev), indexing="ij")
-jit = torch.randint(-4, 5, (2, h, w), device=dev, generator=g)
-p1 = torch.stack([(xx + jit[0]).clamp(0, w - 1), (yy + jit[1]).clamp(0, h - 1)], -1)
-p1 = p1.reshape(1, n, 2).contiguous()
+jit = torch.randint(-4, 5, (B, 2, h, w), device=dev, generator=g)
+p1 = torch.stack([(xx + jit[:, 0]).clamp(0, w - 1), (yy + jit[:, 1]).clamp(0, h - 1)], -1)
+p1 = p1.reshape(B, n, 2).contiguous()
 out = torch.empty_like(p1)
 
 
 def refine():
-    _lib.check(lib.m3s_refine_matches(_lib.ptr(D11), _lib.ptr(D21), _lib.ptr(p1), _lib.ptr(out), 1,
+    _lib.check(lib.m3s_refine_matches(_lib.ptr(D11), _lib.ptr(D21), _lib.ptr(p1), _lib.ptr(out), B,
                                       h, w, n, F, 3, 5, _lib.stream(dev)), "refine")
 
 
@@ -50,4 +51,6 @@ def graph_us(fn, rep=20):
     return e0.elapsed_time(e1) * 1e3 / rep
 
 
-print(f"refine_matches 384x512 r3 d5: {graph_us(refine):.1f} us", flush=True)
+tag = "rows" if os.environ.get("M3S_REFINE_ROWS") else "tile2d"
+us = graph_us(refine)
+print(f"refine_matches 384x512 r3 d5 b={B} {tag}: {us:.1f} us ({us / B:.1f} us per pair)", flush=True)
