@@ -9,6 +9,7 @@
 // Unlike the reference (16-thread blocks, no tail guard, matching_kernels.cu:36,131,
 // 290-293) any n is accepted.
 #include <stdlib.h>
+#include <string.h>
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -241,6 +242,79 @@ __global__ __launch_bounds__(kBlock) void refine_matches_kernel(
   p1_new[2 * q + 1] = v_new;
 }
 
+// The reference configuration (F = 24, radius R = 3, n == h*w) as a latency-hiding variant
+// of the TILE2D kernel above, same visiting order and arithmetic:
+//  * the 2R+1 candidates of one window column (fixed u, the inner v loop) are loaded before
+//    any of them is scored — 21 16-B loads in flight per lane instead of 3 — out-of-image
+//    candidates load pixel 0 and are skipped when scoring, as the reference skips them;
+//  * workgroups are dispatched round-robin over the 8 XCDs (linear id % 8): the tile order
+//    is remapped so each XCD takes a contiguous band of tiles and its L2 holds one band's
+//    windows instead of windows from all over the image;
+//  * 32-bit in-image offsets (h*w < 2^31 is checked by the host).
+template <int R>
+__global__ __launch_bounds__(kBlock) void refine_matches_r_kernel(
+    const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
+    const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
+    int dilation_max) {
+  constexpr int S = 2 * R + 1;
+  const int n = h * w;
+  const int tiles_w = (w + 15) >> 4;
+  const int tiles = tiles_w * ((h + 15) >> 4);
+  const int lin = blockIdx.x, xcd = lin & 7, loc = lin >> 3;
+  const int tq = tiles >> 3, tr = tiles & 7;
+  const int t = xcd < tr ? xcd * (tq + 1) + loc : tr * (tq + 1) + (xcd - tr) * tq + loc;
+  const int px = (t % tiles_w) * 16 + (threadIdx.x & 15);
+  const int py = (t / tiles_w) * 16 + (threadIdx.x >> 4);
+  if (px >= w || py >= h) return;
+  const int64_t q = (int64_t)blockIdx.y * n + (int64_t)py * w + px;
+  _Float16 qd[24];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(D21 + q * 24);
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      uint4 v = src[c];
+      __builtin_memcpy(&qd[8 * c], &v, 16);
+    }
+  }
+  const uint4* img = reinterpret_cast<const uint4*>(D11 + (int64_t)blockIdx.y * n * 24);
+  int64_t u0 = p1[2 * q + 0];
+  int64_t v0 = p1[2 * q + 1];
+  _Float16 max_score = (_Float16)0.0f;
+  int64_t u_new = u0, v_new = v0;
+  for (int d = dilation_max; d > 0; d--) {
+    const int rd = R * d;
+    for (int ii = 0; ii < S; ii++) {
+      const int64_t u = u0 - rd + ii * d;
+      const bool uok = u >= 0 && u < w;
+      uint4 buf[S][3];
+      bool ok[S];
+#pragma unroll
+      for (int jj = 0; jj < S; jj++) {
+        const int64_t v = v0 - rd + jj * d;
+        ok[jj] = uok && v >= 0 && v < h;
+        const int off = ok[jj] ? (int)v * w + (int)u : 0;
+#pragma unroll
+        for (int c = 0; c < 3; c++) buf[jj][c] = img[off * 3 + c];
+      }
+#pragma unroll
+      for (int jj = 0; jj < S; jj++) {
+        _Float16 cd[24];
+        __builtin_memcpy(cd, buf[jj], 48);
+        const _Float16 score = desc_score<24>(qd, cd, 24);
+        if (ok[jj] && (float)score > (float)max_score) {
+          max_score = score;
+          u_new = u;
+          v_new = v0 - rd + jj * d;
+        }
+      }
+    }
+    u0 = u_new;
+    v0 = v_new;
+  }
+  p1_new[2 * q + 0] = u_new;
+  p1_new[2 * q + 1] = v_new;
+}
+
 // ---------------------------------------------------------------------------
 // prep_for_iter_proj (matching.py:25-49) + img_gradient (image.py:5-38), fused.
 // ---------------------------------------------------------------------------
@@ -371,7 +445,18 @@ extern "C" int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21,
   const _Float16* D11 = reinterpret_cast<const _Float16*>(d_D11);
   const _Float16* D21 = reinterpret_cast<const _Float16*>(d_D21);
   const bool aligned = ((uintptr_t)d_D11 % 16 == 0) && ((uintptr_t)d_D21 % 16 == 0);
-  static const bool rows = getenv("M3S_REFINE_ROWS") != nullptr;  // A/B: 1-D row blocks
+  // A/B knob: M3S_REFINE_KERNEL = "rows" (1-D row blocks) | "tile" (plain 16x16 tiles)
+  static const char* kind = getenv("M3S_REFINE_KERNEL");
+  static const bool rows = kind && !strcmp(kind, "rows");
+  static const bool tile = kind && !strcmp(kind, "tile");
+  if (fdim == 24 && aligned && n == h * w && radius == 3 && h * w < (1LL << 31) && !rows &&
+      !tile) {
+    dim3 grid2((unsigned)(m3s_div_up(w, 16) * m3s_div_up(h, 16)), (unsigned)b);
+    hipLaunchKernelGGL(refine_matches_r_kernel<3>, grid2, dim3(kBlock), 0, m3s_stream(stream),
+                       D11, D21, d_p1, d_p1_new, (int)h, (int)w, dilation_max);
+    M3S_LAUNCH_CHECK();
+    return M3S_OK;
+  }
   if (fdim == 24 && aligned && n == h * w && !rows) {
     dim3 grid2((unsigned)(m3s_div_up(w, 16) * m3s_div_up(h, 16)), (unsigned)b);
     hipLaunchKernelGGL((refine_matches_kernel<24, true>), grid2, dim3(kBlock), 0,

@@ -56,6 +56,22 @@ def test_refine_matches_bit_exact(oracle, dev, b, h, w):
     np.testing.assert_array_equal(got.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("radius,dmax", [(3, 5), (2, 3), (3, 1)])
+def test_refine_matches_scattered(oracle, dev, radius, dmax):
+    # scattered p1 (windows off every image edge), 24-d descriptors, 3 directions, a tile
+    # count (5 x 6 = 30) that is not a multiple of the 8 XCDs: the radius-3 latency-hiding
+    # kernel and the generic 16x16-tile kernel (radius 2) on the same inputs
+    import mast3r_slam_backends as mb
+    rng = np.random.default_rng(11 + radius)
+    b, h, w = 3, 70, 90
+    d11 = rng.normal(size=(b, h, w, 24)).astype(np.float16)
+    d21 = rng.normal(size=(b, h * w, 24)).astype(np.float16)
+    p1 = rng.integers(0, [w, h], size=(b, h * w, 2)).astype(np.int64)
+    ref = oracle.refine_matches(d11, d21, p1, radius, dmax)
+    (got,) = mb.refine_matches(_t(d11, dev), _t(d21, dev), _t(p1, dev), radius, dmax)
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
 def test_refine_generic_fdim(oracle, dev):
     import mast3r_slam_backends as mb
     rng = np.random.default_rng(4)

@@ -51,6 +51,6 @@ def graph_us(fn, rep=20):
     return e0.elapsed_time(e1) * 1e3 / rep
 
 
-tag = "rows" if os.environ.get("M3S_REFINE_ROWS") else "tile2d"
+tag = os.environ.get("M3S_REFINE_KERNEL", "r3")
 us = graph_us(refine)
 print(f"refine_matches 384x512 r3 d5 b={B} {tag}: {us:.1f} us ({us / B:.1f} us per pair)", flush=True)
