@@ -391,6 +391,10 @@ class PairModel:
         # the critical path and the graph gains dependency edges, 118.5 vs 124.9 frames/s
         # serial, so one stream is the default.
         self.side = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
+        # DPT act_postprocess branches started mid-decoder (pair(split_heads=True))
+        self.side_early = torch.cuda.Stream(device)
+        self.early_heads = os.environ.get("M3S_EARLY_HEADS", "0") == "1"  # measured slower
+        self._early_ev = []
         self.serial = True
         self.fp8 = False
         # bf16 path: the blocks' LayerNorms folded into the following projections (ln_fold;
@@ -534,18 +538,20 @@ class PairModel:
         return feat, pos
 
     # ---- decoders: both models x both sides, batch z = model*2 + side ----
-    def decode(self, feat_i, feat_j, pos, gh, gw):
+    def decode(self, feat_i, feat_j, pos, gh, gw, on_hook=None):
         """feat_i/feat_j bf16 [S,E] (frame i = side 1, keyframe j = side 2).
         Returns hooks dict: h0 bf16 [4,S,E], h6/h9/h12 bf16 [4,S,D] (h12 = dec_norm)."""
         S, E = gh * gw, self.a.enc_dim
-        return self.decode_multi(feat_i.reshape(1, S, E), feat_j.reshape(1, S, E), gh, gw)
+        return self.decode_multi(feat_i.reshape(1, S, E), feat_j.reshape(1, S, E), gh, gw,
+                                 on_hook=on_hook)
 
-    def decode_multi(self, feat1, feat2, gh, gw, models=2):
+    def decode_multi(self, feat1, feat2, gh, gw, models=2, on_hook=None):
         """G directed pairs at once: feat1/feat2 bf16 [G,S,E] are the first / second view of
         each pair (d3r/model.py:171-190 `_decoder(f1, pos1, f2, pos2)`), decoded by BOTH
         models (models=2) or by MonST3R alone (models=1, the dynamic-mask mono decode).
         Problems z = (g*models + model)*2 + side; every launch covers all of them and reads
-        the weight stack of z % (2*models) (weight_mod).  Returns hooks [2*models*G,S,*]."""
+        the weight stack of z % (2*models) (weight_mod).  Returns hooks [2*models*G,S,*].
+        on_hook(name, hooks): called as each hook (h0, h6, h9, h12) has been enqueued."""
         o, a, W = self.ops, self.a, self.w
         S, E, D = gh * gw, a.enc_dim, a.dec_dim
         G = feat1.shape[0]
@@ -564,8 +570,10 @@ class PairModel:
         o.gemm(h0, W.dec_embed_w, x, S, D, E, Z, sA=S * E, sB=D * E, sC=S * D,
                bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32, wmod=wm,
                ln_stats=(xb, st) if fold else None)
+        if on_hook is not None:
+            on_hook("h0", {"h0": h0})
         if fold:
-            return self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm)
+            return self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm, on_hook)
         adt = U8 if self.fp8 else BF16
         xn = self._buf("dec_xn", (Z, S, D), adt)
         yn = self._buf("dec_yn", (Z, S, D), adt)
@@ -636,12 +644,16 @@ class PairModel:
                 hb = self._buf(f"h{i + 1}", (Z, S, D), BF16)
                 hb.copy_(x)
                 hooks[f"h{i + 1}"] = hb
+                if on_hook is not None:
+                    on_hook(f"h{i + 1}", hooks)
         h12 = self._buf("h12", (Z, S, D), BF16)
         o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
         hooks["h12"] = h12
+        if on_hook is not None:
+            on_hook("h12", hooks)
         return hooks
 
-    def _decode_folded(self, x, xb, st, h0, Z, S, E, D, gh, gw, wm):
+    def _decode_folded(self, x, xb, st, h0, Z, S, E, D, gh, gw, wm, on_hook=None):
         """decode_multi's blocks (croco/blocks.py:172-195 DecoderBlock) with every LayerNorm
         folded into the projection that consumes it (ln_fold): the residual GEMMs write x
         (f32), its bf16 copy and row statistics; qkv (norm1), the cross-attention k/v
@@ -691,9 +703,13 @@ class PairModel:
             o.gemm(hid, P["fc2_w"], x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D,
                    bias=P["fc2_b"], sBias=D, wmod=wm,
                    **dict(R32S, ln_stats=(xc, st)))
+            if (i + 1) in hk and on_hook is not None:
+                on_hook(f"h{i + 1}", hooks)
         h12 = self._buf("h12", (Z, S, D), BF16)
         o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
         hooks["h12"] = h12
+        if on_hook is not None:
+            on_hook("h12", hooks)
         return hooks
 
     # ---- DPT heads (batched over z) ----
@@ -772,13 +788,15 @@ class PairModel:
         t = self.w.h[key]
         return t[self._wbase:] if self._wbase else t
 
-    def heads(self, hooks, gh, gw, H, W, models=2, split=False):
+    def heads(self, hooks, gh, gw, H, W, models=2, split=False, R=None):
         """DPT heads of all 2*models*G problems (z = (g*models + model)*2 + side, head weights
         z % (2*models)) + MASt3R local features of the model-1 problems (models=2 only).
         split (one pair, G = 1): the MASt3R DPT heads — whose pts3d/conf the tracking never
         reads (monst3r_utils.py:290) — are issued on side stream 0 as their own 2-problem
         set, concurrent with the MonST3R heads, the local features and the caller's
         matching / pose solve; the caller joins with `join()` before the next frame.
+        R: the layer_rn outputs of all Z problems computed ahead by early_branch (events in
+        self._early_ev); the refinenets then start from them.
         Returns pts3d f32 [Z,H,W,3], conf f32 [Z,H,W], desc16 f16 [2G,H,W,24],
         desc f32 [2G,H,W,24], desc_conf f32 [2G,H,W] (the latter three: (g, side) of model 1;
         None with models=1)."""
@@ -795,6 +813,8 @@ class PairModel:
             main = torch.cuda.current_stream(self.dev)
             side = self.side[0]
             side.wait_stream(main)
+            for ev in self._early_ev:
+                side.wait_event(ev)
             with torch.cuda.stream(side):
                 if self.lf_side:
                     # the local features (needed by the matching) first on the side chain,
@@ -804,18 +824,24 @@ class PairModel:
                     ev_lf = torch.cuda.Event()
                     ev_lf.record(side)
                 sub = {k: v[2:4] for k, v in hooks.items()}
-                self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4])
+                self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4],
+                          R=None if R is None else [r[2:4] for r in R])
                 self._ev_heads = torch.cuda.Event()
                 self._ev_heads.record(side)
         # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle
         if models == 2 and desc is None:
             self._wm = wm
             desc, desc16, dconf, ev_lf = self._local_features(hooks, G, S, E, D, H, W)
+        for ev in self._early_ev:
+            main_s = torch.cuda.current_stream(self.dev)
+            main_s.wait_event(ev)
+        self._early_ev = []
         if split:
             sub = {k: v[0:2] for k, v in hooks.items()}
-            self._dpt(sub, gh, gw, H, W, 2, 0, 2, None, pts[0:2], conf[0:2])
+            self._dpt(sub, gh, gw, H, W, 2, 0, 2, None, pts[0:2], conf[0:2],
+                      R=None if R is None else [r[0:2] for r in R])
         else:
-            self._dpt(hooks, gh, gw, H, W, Z, 0, wm, None, pts, conf)
+            self._dpt(hooks, gh, gw, H, W, Z, 0, wm, None, pts, conf, R=R)
         self._wait(ev_lf)
         return pts, conf, desc16, desc, dconf
 
@@ -825,21 +851,55 @@ class PairModel:
             torch.cuda.current_stream(self.dev).wait_event(self._ev_heads)
             self._ev_heads = None
 
-    def _dpt(self, hooks, gh, gw, H, W, Z, wbase, wm, tag, pts, conf):
-        """act_postprocess + refinenets + head of Z problems whose hooks are given (views),
-        head weights from stack wbase with weight_mod wm, scratch keyed by tag."""
-        o, a = self.ops, self.a
-        self._tag, self._wbase, self._wm = tag, wbase, wm
-        Hw = self._hw
-        S, E, D = gh * gw, a.enc_dim, a.dec_dim
-        Ld = a.layer_dims
-        F = a.feature_dim
-        # act_postprocess + layer_rn (3x3, no bias → F channels): branches 1-3 on side
-        # stream 0, branch 0 (the largest) on the current stream
+    def _rn_bufs_early(self, gh, gw, Z):
+        saved, self._tag = self._tag, "early"
+        try:
+            return self._rn_bufs(gh, gw, Z)
+        finally:
+            self._tag = saved
+
+    def _early_branch(self, name, hooks, gh, gw, R):
+        """Enqueue hook `name`'s act_postprocess + layer_rn branch (all Z problems, weight
+        stacks z % 4) on self.side_early after the work queued so far on the current
+        stream; heads() waits for the recorded events before the refinenets."""
+        k = {"h0": 0, "h6": 1, "h9": 2, "h12": 3}[name]
+        main = torch.cuda.current_stream(self.dev)
+        st = self.side_early
+        st.wait_stream(main)
+        saved = (self._tag, self._wbase, self._wm)
+        self._tag, self._wbase, self._wm = "early", 0, 4
+        try:
+            with torch.cuda.stream(st):
+                self._ap_branch(k, hooks, gh, gw, hooks[name].shape[0], R)
+                ev = torch.cuda.Event()
+                ev.record(st)
+        finally:
+            self._tag, self._wbase, self._wm = saved
+        self._early_ev.append(ev)
+
+    def _rn_bufs(self, gh, gw, Z):
+        F = self.a.feature_dim
         g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
         dims = [(4 * gh, 4 * gw), (2 * gh, 2 * gw), (gh, gw), (g3h, g3w)]
-        R = [self._buf(f"rn{k}", (Z, dims[k][0], dims[k][1], F), BF16) for k in range(4)]
-        with self._on(0):
+        return [self._buf(f"rn{k}", (Z, dims[k][0], dims[k][1], F), BF16) for k in range(4)]
+
+    def _ap_branch(self, k, hooks, gh, gw, Z, R):
+        """DPT act_postprocess[k] + scratch.layer{k+1}_rn (d3r/heads/dpt_head.py:62-88,
+        croco/dpt_block.py:300-338) of Z problems: hook → R[k] (F channels)."""
+        o, a, Hw, wm = self.ops, self.a, self._hw, self._wm
+        S, E, D = gh * gw, a.enc_dim, a.dec_dim
+        Ld, F = a.layer_dims, a.feature_dim
+        g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
+        if k == 0:
+            t0 = self._buf("ap_t0", (Z, S, Ld[0]), BF16)
+            o.gemm(hooks["h0"], Hw("ap0_w"), t0, S, Ld[0], E, Z, sA=S * E, sB=Ld[0] * E,
+                   sC=S * Ld[0], bias=Hw("ap0_b"), sBias=Ld[0], wmod=wm)
+            L0 = self._buf("ap_L0", (Z, 4 * gh, 4 * gw, Ld[0]), BF16)
+            o.gemm(t0, Hw("ap0t_w"), L0, S, 16 * Ld[0], Ld[0], Z, sA=S * Ld[0],
+                   sB=16 * Ld[0] * Ld[0], sC=16 * S * Ld[0], bias=Hw("ap0t_b"), sBias=Ld[0],
+                   convt=(4, Ld[0], gw), wmod=wm)
+            self._conv3(L0, "rn0_w", R[0], Z, 4 * gh, 4 * gw, Ld[0], F)
+        elif k == 1:
             t1 = self._buf("ap_t1", (Z, S, Ld[1]), BF16)
             o.gemm(hooks["h6"], Hw("ap1_w"), t1, S, Ld[1], D, Z, sA=S * D, sB=Ld[1] * D,
                    sC=S * Ld[1], bias=Hw("ap1_b"), sBias=Ld[1], wmod=wm)
@@ -847,27 +907,39 @@ class PairModel:
             o.gemm(t1, Hw("ap1t_w"), L1, S, 4 * Ld[1], Ld[1], Z, sA=S * Ld[1],
                    sB=4 * Ld[1] * Ld[1], sC=4 * S * Ld[1], bias=Hw("ap1t_b"), sBias=Ld[1],
                    convt=(2, Ld[1], gw), wmod=wm)
-            self._conv3(L1, "rn1_w", R[1], Z, dims[1][0], dims[1][1], Ld[1], F)
+            self._conv3(L1, "rn1_w", R[1], Z, 2 * gh, 2 * gw, Ld[1], F)
+        elif k == 2:
             L2 = self._buf("ap_L2", (Z, gh, gw, Ld[2]), BF16)
             o.gemm(hooks["h9"], Hw("ap2_w"), L2, S, Ld[2], D, Z, sA=S * D, sB=Ld[2] * D,
                    sC=S * Ld[2], bias=Hw("ap2_b"), sBias=Ld[2], wmod=wm)
             self._conv3(L2, "rn2_w", R[2], Z, gh, gw, Ld[2], F)
+        else:
             t3 = self._buf("ap_t3", (Z, gh, gw, Ld[3]), BF16)
             o.gemm(hooks["h12"], Hw("ap3_w"), t3, S, Ld[3], D, Z, sA=S * D, sB=Ld[3] * D,
                    sC=S * Ld[3], bias=Hw("ap3_b"), sBias=Ld[3], wmod=wm)
             L3 = self._buf("ap_L3", (Z, g3h, g3w, Ld[3]), BF16)
             self._conv3(t3, "ap3c_w", L3, Z, gh, gw, Ld[3], Ld[3], stride=2, bias_key="ap3c_b")
             self._conv3(L3, "rn3_w", R[3], Z, g3h, g3w, Ld[3], F)
-            ev_ap = self._event()
-        t0 = self._buf("ap_t0", (Z, S, Ld[0]), BF16)
-        o.gemm(hooks["h0"], Hw("ap0_w"), t0, S, Ld[0], E, Z, sA=S * E, sB=Ld[0] * E,
-               sC=S * Ld[0], bias=Hw("ap0_b"), sBias=Ld[0], wmod=wm)
-        L0 = self._buf("ap_L0", (Z, 4 * gh, 4 * gw, Ld[0]), BF16)
-        o.gemm(t0, Hw("ap0t_w"), L0, S, 16 * Ld[0], Ld[0], Z, sA=S * Ld[0],
-               sB=16 * Ld[0] * Ld[0], sC=16 * S * Ld[0], bias=Hw("ap0t_b"), sBias=Ld[0],
-               convt=(4, Ld[0], gw), wmod=wm)
-        self._conv3(L0, "rn0_w", R[0], Z, dims[0][0], dims[0][1], Ld[0], F)
-        self._wait(ev_ap)
+
+    def _dpt(self, hooks, gh, gw, H, W, Z, wbase, wm, tag, pts, conf, R=None):
+        """act_postprocess + refinenets + head of Z problems whose hooks are given (views),
+        head weights from stack wbase with weight_mod wm, scratch keyed by tag.  R: the
+        four layer_rn outputs when already computed (early_branch), else computed here."""
+        o, a = self.ops, self.a
+        self._tag, self._wbase, self._wm = tag, wbase, wm
+        Hw = self._hw
+        F = a.feature_dim
+        g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
+        if R is None:
+            R = self._rn_bufs(gh, gw, Z)
+            # act_postprocess + layer_rn (3x3, no bias → F channels): branches 1-3 on side
+            # stream 0, branch 0 (the largest) on the current stream
+            with self._on(0):
+                for k in (1, 2, 3):
+                    self._ap_branch(k, hooks, gh, gw, Z, R)
+                ev_ap = self._event()
+            self._ap_branch(0, hooks, gh, gw, Z, R)
+            self._wait(ev_ap)
         # refinenets: path_k = up2(out_conv(RCU2(path_{k+1} + RCU1(R_k)))) with the next
         # level's skip pre-added by the upsample (consumed as RCU1's residual addend)
         p4 = self._buf("path4", (Z, gh, gw, F), BF16)
@@ -913,8 +985,17 @@ class PairModel:
             feat_i, pos = self.encode(img_i)
         else:
             pos = self.positions(1, gh, gw)
-        hooks = self.decode(feat_i[0], feat_j.reshape(-1, a.enc_dim), pos, gh, gw)
-        pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W, split=split_heads)
+        R = None
+        on_hook = None
+        if self.early_heads and split_heads:
+            # the DPT act_postprocess / layer_rn branch of each hook starts on its own
+            # stream as soon as the decoder has produced that hook (h0: before the first
+            # decoder layer; h6 / h9: mid-decoder), for all 4 problems at once
+            R = self._rn_bufs_early(gh, gw, 4)
+            on_hook = lambda name, hk: self._early_branch(name, hk, gh, gw, R)  # noqa: E731
+        hooks = self.decode(feat_i[0], feat_j.reshape(-1, a.enc_dim), pos, gh, gw,
+                            on_hook=on_hook)
+        pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W, split=split_heads, R=R)
         return dict(X=pts[0:2], C=conf[0:2], D16=desc16, D=desc, Q=dconf, feat_i=feat_i,
                     mast3r_X=pts[2:4], mast3r_C=conf[2:4])
 

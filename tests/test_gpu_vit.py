@@ -515,6 +515,28 @@ def test_split_heads_match_batched(dev):
     assert torch.equal(b["D16"], a["D16"]) and torch.equal(b["Q"], a["Q"])
 
 
+def test_early_heads_match_split(dev):
+    """M3S_EARLY_HEADS A/B knob (model.early_heads): the DPT act_postprocess / layer_rn
+    branches started mid-decoder on their own stream (4 problems at once) give the split
+    heads' outputs up to the bf16 GEMM tiling; descriptors (no DPT) exact."""
+    from monst3r_slam_amd import model as Mdl
+    m, _ = Mdl.build(dev, small=True)
+    g = torch.Generator(device=dev).manual_seed(43)
+    img_i = torch.rand(1, 3, 96, 128, device=dev, generator=g) * 2 - 1
+    img_j = torch.rand(1, 3, 96, 128, device=dev, generator=g) * 2 - 1
+    outs = []
+    for early in (False, True):
+        m.early_heads = early
+        o = m.pair(img_i, img_j=img_j, split_heads=True)
+        m.join()
+        outs.append({k: v.clone() for k, v in o.items() if torch.is_tensor(v)})
+    m.early_heads = False
+    a, b = outs
+    for k in ("X", "mast3r_X", "C", "mast3r_C"):
+        assert _rel(b[k], a[k]) < 1e-2, k
+    assert torch.equal(b["D16"], a["D16"]) and torch.equal(b["Q"], a["Q"])
+
+
 def _ln_stats_ref(x):
     """(mean, M2) per 128-column group of the rows of x [.., M, N]."""
     g = x.float().reshape(*x.shape[:-1], x.shape[-1] // 128, 128)
