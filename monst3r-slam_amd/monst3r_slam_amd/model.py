@@ -478,7 +478,26 @@ class PairModel:
 
     # ---- encoder: PatchEmbed + 24 blocks + enc_norm (batch of B images as M = B*S) ----
     def encode(self, img, out=None):
-        """img f32 [B,3,H,W] → feat bf16 [B,S,E], pos int64 [B,S,2]."""
+        """img f32 [B,3,H,W] → feat bf16 [B,S,E], pos int64 [B,S,2].
+        M3S_ENC_TILE="cfg:splits" (experiment knob): the encoder's GEMMs take that tile
+        configuration (e.g. fewer, larger tiles while it shares the chip with the tracking
+        chain) instead of the per-shape table."""
+        knob = os.environ.get("M3S_ENC_TILE")
+        if knob:
+            cfg, _, sp = knob.partition(":")
+            saved = {k: os.environ.get(k) for k in ("M3S_GEMM_TILE", "M3S_GEMM_SPLITS")}
+            os.environ["M3S_GEMM_TILE"], os.environ["M3S_GEMM_SPLITS"] = cfg, sp or "1"
+            try:
+                return self._encode(img, out)
+            finally:
+                for k, v in saved.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+        return self._encode(img, out)
+
+    def _encode(self, img, out=None):
         o, a, W = self.ops, self.a, self.w
         B, _, H, Wd = img.shape
         gh, gw = H // a.patch, Wd // a.patch
