@@ -403,7 +403,11 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
   static_assert(C::A_CH >= 1 && C::B_CH >= 1, "tile too small for 256 threads");
   static_assert((C::A_CH * NT) % C::CPR == 0 && 32 % (C::RPB * C::CPR) == 0, "swizzle");
   static_assert(C::L * (STAGES - 2) <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES];
+  // ALL LDS in one array (the split-K last-arriver flag included, at its end): a second
+  // __shared__ object made hipcc wait vmcnt(0) before the LDS reads of every MFMA phase in
+  // the SPLIT instantiations — the DMA ring drained 4x per K-tile (cdna_hip_programming.md
+  // §5 'Projection GEMM at M = 256' item 4(a)); measured as split-K K-tiles 2.4x slower
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES + 16];
 
   // 1-D grid over (batch x split) groups x tiles.  Workgroups are dispatched to the 8
   // XCDs round-robin by linear id; the bijective remap gives each XCD a contiguous range
@@ -852,7 +856,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
 
   if constexpr (SPLIT) {
     // publish this split's partial tile; the tile's last split sums them all
-    __shared__ int s_last;
+    int& s_last = *reinterpret_cast<int*>(lds + C::LDS_BYTES);
     const int64_t per_b = (int64_t)a.M * a.N;
     float* P = a.ws + (int64_t)zz * per_b;
 #pragma unroll 4
@@ -878,6 +882,9 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
     __syncthreads();
     if (tid == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      // the fence's own wait can be dropped by the compiler: wait here, before the ticket
+      // (cdna_hip_programming.md Guideline 16, Pitfall 12)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       int* ctr = a.cnt + (int64_t)g * nwg + wgid;
       const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = old == a.splits - 1;
