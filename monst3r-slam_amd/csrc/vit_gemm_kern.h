@@ -1100,8 +1100,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
 // T128W8: 128x128 with 8 waves (two per SIMD, each 32x64): one wave's LDS-DMA issue
 // (≈60-185 cycles per 1-KB piece, MI355X_MICROARCH.md) overlaps the other's MFMAs, where
 // the 4-wave block leaves the matrix pipe idle during its own issue
+// T256W8: 256x128 with 8 waves (4 x 2, each 64x64): per CU the LDS-DMA path moves
+// (BM + BN)·BK·2 bytes per K-tile at ≈64 B/clk against 2·BM·BN·BK MFMA FLOPs at ≈4k
+// FLOP/clk, i.e. fetch / MFMA cycles ≈ 64·(BM + BN) / (BM·BN): 1.5 for 64x128, 1.0 for
+// 128², 0.75 here — the first tile whose K-loop the matrix pipe can pace.  For the M = 768
+// batched decoder GEMMs it trades 2x fewer blocks for that; T256 is the 4-wave form.
 enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7, T96 = 8, T96O2 = 9,
-               T64D = 10, T128D = 11, T128W8 = 12 };
+               T64D = 10, T128D = 11, T128W8 = 12, T256W8 = 13 };
 
 // Epilogue flag sets compiled as straight-line variants (8-wide vector path), per mode:
 //   GEMM: bf16 out, +RoPE, +GELU, f32 residual → f32, f32 out;  conv: bf16 out, +bf16
@@ -1171,7 +1176,8 @@ void launch_main(Args& a, dim3 grid, hipStream_t s) {
         return;
       // LayerNorm fold (the ViT blocks' norm → projection pairs): consumers qkv / q / kv
       // (+RoPE) and fc1 (+GELU), producers the residual GEMMs and the embeddings
-      if constexpr (BN == 128 && BK == 64 && (BM == 64 || BM == 96 || BM == 128) && OCC <= 2 &&
+      if constexpr (BN == 128 && BK == 64 && (BM == 64 || BM == 96 || BM == 128 || BM == 256) &&
+                    OCC <= 2 && (BM != 256 || OCC == 1) &&
                     (BM != 96 || OCC == 1)) {
         constexpr int LF = M3S_EPI_LN_FOLD, LS = M3S_EPI_LN_STATS;
         if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_ROPE, SP>(a, grid, s,
@@ -1246,7 +1252,8 @@ int launch(Args& a, int batch, hipStream_t s) {
   if (split) {
     // split-K (fused last-split epilogue): 128^2 GEMM tiles, 64x128 GEMM / conv tiles
     constexpr bool CAN = !F8 && ((BM == 128 && BN == 128 && BK == 64) ||
-                                 (BM == 64 && BN == 128 && BK == 64));
+                                 (BM == 64 && BN == 128 && BK == 64) ||
+                                 (BM == 256 && BN == 128 && BK == 64));
     if constexpr (CAN) {
       if (a.mode == 0)
         launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 0, true>(a, grid, s);

@@ -574,7 +574,7 @@ def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k):
                                                   (768, 4096, 1024, 1, 0, "gelu"),
                                                   (200, 384, 256, 2, 1, "none")])
 @pytest.mark.parametrize("split", ["0", "3"])
-@pytest.mark.parametrize("tile", ["0", "12"])
+@pytest.mark.parametrize("tile", ["0", "12", "13"])
 def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi, split, tile):
     """LN_FOLD: LN(x) Wᵀ + b computed as rstd (bf16(x) (W∘γ)ᵀ − mean c1) + c2 from the
     producer's statistics, vs torch fp32 LayerNorm → Linear (→ RoPE / GELU) on x of
@@ -624,7 +624,7 @@ def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi,
     assert _rel(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("epi", ["gelu", "res"])
 def test_gemm_every_tile_config(ops, dev, monkeypatch, tile, epi):
     """Every tile configuration (M3S_GEMM_TILE override) on a 768-row problem, straight-
@@ -668,7 +668,7 @@ def test_cross_attention_kv_batch_xor(ops, dev):
     assert torch.equal(o, o2)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 7, 10, 12])
+@pytest.mark.parametrize("tile", [1, 2, 7, 10, 12, 13])
 @pytest.mark.parametrize("splits", [2, 3, 5])
 @pytest.mark.parametrize("epi", ["gelu", "res_stats", "rope", "f32"])
 @pytest.mark.parametrize("fused", ["1", "0"])

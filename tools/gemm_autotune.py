@@ -24,16 +24,18 @@ import bench  # noqa: E402
 from monst3r_slam_amd import model as Mdl  # noqa: E402
 
 TILES = {1: "128x128", 2: "64x128 2/CU", 7: "128x128 2/CU", 8: "96x128",
-         10: "64x128 6-stage", 11: "128x128 4-stage", 12: "128x128 8 waves"}
+         10: "64x128 6-stage", 11: "128x128 4-stage", 12: "128x128 8 waves", 6: "256x128", 13: "256x128 8 waves"}
 SPLITS = (1, 2, 3, 4, 6, 8)
 
 
-def record(m, dev, graph):
+def record(m, dev, graph, split_heads=False):
     img = torch.rand(1, 3, 384, 512, device=dev) * 2 - 1
     feat, _ = m.encode(img)
     feat = feat.clone()
     m.ops.record = []
     m.pair(img, feat_j=feat)
+    if split_heads:  # the C3 step's head launches (MonST3R / MASt3R heads as two batch-2 sets)
+        m.pair(img, feat_j=feat, split_heads=True)
     if graph:
         m.mono(feat, 384, 512)
         f4 = feat.expand(4, -1, -1).contiguous()
@@ -75,16 +77,20 @@ def main():
     ap.add_argument("--tiles", type=lambda v: [int(t) for t in v.split(",")], default=None,
                     help="restrict the sweep to these tile configs")
     ap.add_argument("--gemm-only-m", type=int, default=0, help="only launch classes with this M")
+    ap.add_argument("--split-heads", action="store_true", help="also the split-heads pair shapes")
+    ap.add_argument("--min-m", type=int, default=0, help="only launch classes with M >= this")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     m, _ = Mdl.build(dev)
     for k in ("M3S_GEMM_TILE", "M3S_GEMM_SPLITS", "M3S_GEMM_FUSED"):
         os.environ.pop(k, None)
-    groups = record(m, dev, args.graph)
+    groups = record(m, dev, args.graph, args.split_heads)
     res = []
     for key, lst in groups.items():
         M, N, K, batch, flags, mode = key
         if args.gemm_only_m and M != args.gemm_only_m:
+            continue
+        if M < args.min_m:
             continue
         base = time_group(m, dev, lst, {})
         best = (base, None)
