@@ -260,6 +260,10 @@ typedef struct {
                                               on entry and left zero (device; the caller
                                               zeroes it once; one per concurrent stream)   */
   int32_t tile_counters_len;               /* entries; split-K needs batch x tiles of them  */
+  int32_t tile_hint;                       /* 0: the per-shape tuned table / heuristic; > 0: this
+                                              tile configuration (vit_gemm_kern.h TileCfg) with
+                                              split_k (0 → 1) — a caller that knows the launch
+                                              shares the chip (the prefetched encoder) */
 } m3s_gemm_desc;
 
 /* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 8 == 0; conv: Cin % 32 == 0.

@@ -219,6 +219,8 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   const int64_t tiles128 = (int64_t)((d->M + 127) / 128) * ((d->N + 127) / 128) * d->batch;
   const int nk = (int)((eK + 63) / 64);     // K-tiles of 128 bytes per row
   int cfg = forced_tile();
+  const bool hinted = cfg == 0 && d->tile_hint > 0;  // the caller's choice (header)
+  if (hinted) cfg = d->tile_hint;
   const TunedShape* tuned = (cfg == 0 && !getenv("M3S_GEMM_SPLITS")) ? tuned_for(d) : nullptr;
   if (tuned) cfg = tuned->cfg;
   if (cfg == 0 && f8) {
@@ -262,11 +264,11 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   if (const char* e = getenv("M3S_GEMM_SPLITS")) splits = atoi(e);  // tuning override
   if (splits <= 0) {
     splits = 1;
-    if (!conv && (cfg == T128 || cfg == T128O2))
+    if (!hinted && !conv && (cfg == T128 || cfg == T128O2))
       while (tiles128 * splits * 2 <= 256 && nk / (splits * 2) >= 8) splits *= 2;
     // the small DPT levels (24x32, 12x16 convs: 24-96 tiles of 64x128 with K = 2304-6912)
     // split K while the grid stays within one round of 2 blocks per CU
-    if (conv && cfg == T64 && !(d->flags & M3S_EPI_DPT_OUT)) {
+    if (!hinted && conv && cfg == T64 && !(d->flags & M3S_EPI_DPT_OUT)) {
       const int64_t tiles64 = (int64_t)((d->M + 63) / 64) * ((d->N + 127) / 128) * d->batch;
       while (tiles64 * splits * 2 <= 512 && nk / (splits * 2) >= 8) splits *= 2;
     }

@@ -98,7 +98,8 @@ class GemmDesc(ctypes.Structure):
                 ("stride_col_scale", _I64), ("C2", _P), ("stats", _P),
                 ("stats_groups", ctypes.c_int32), ("a_batch_xor", ctypes.c_int32),
                 ("ln_c1", _P), ("ln_eps", ctypes.c_float),
-                ("tile_counters", _P), ("tile_counters_len", ctypes.c_int32)]
+                ("tile_counters", _P), ("tile_counters_len", ctypes.c_int32),
+                ("tile_hint", ctypes.c_int32)]
 
 
 (EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT,

@@ -204,7 +204,7 @@ class FramePipeline:
         main = torch.cuda.current_stream(self.tr.model.dev)
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
-            self.tr.model.encode(img_next, out=self.feat[(k + 1) % 2])
+            self.tr.model.encode(img_next, out=self.feat[(k + 1) % 2], concurrent=True)
         res = self.tr.track(img_cur, T_WCf_init, feat_i=self.feat[k % 2])
         main.wait_stream(self.side)
         return res

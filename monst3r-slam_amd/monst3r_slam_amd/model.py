@@ -84,14 +84,16 @@ class Ops:
     def gemm(self, A, B, C, M, N, K, batch=1, *, lda=None, ldb=None, ldc=None, sA=0, sB=0,
              sC=0, bias=None, sBias=0, R=None, ldr=None, sR=0, flags=0, conv=None, convt=None,
              rope=None, split_k=0, wmod=0, dpt=None, fp8=None, out_fp8=False, ln_stats=None,
-             ln_fold=None):
+             ln_fold=None, tile=None):
         """fp8 = (col_scale f32 [.., N], stride): A and B are OCP e4m3 bytes (torch
         float8_e4m3fn / uint8), the f32 accumulator is scaled per column; out_fp8: C is
         stored as e4m3.
         ln_stats = (C2 bf16, stats f32 [batch, M, N/128, 2]): this f32-out GEMM produces a
         LayerNorm input — also store its bf16 copy and per-128-column (mean, M2).
         ln_fold = (stats, c1 f32, a_xor): A is the bf16 copy of a LayerNorm input and B a
-        gamma-folded weight; the epilogue applies the normalisation (bias = c2)."""
+        gamma-folded weight; the epilogue applies the normalisation (bias = c2).
+        tile = (tile configuration, split-K): the descriptor's tile_hint instead of the
+        per-shape table (PairModel.encode(concurrent=True))."""
         d = _lib.GemmDesc()
         d.A, d.lda, d.strideA = _p(A), lda if lda is not None else K, sA
         d.B, d.ldb, d.strideB = _p(B), ldb if ldb is not None else K, sB
@@ -104,6 +106,8 @@ class Ops:
         cnt = self.counters
         d.tile_counters, d.tile_counters_len = _p(cnt), cnt.numel()
         d.weight_mod = wmod
+        if tile is not None:
+            d.tile_hint, d.split_k = int(tile[0]), int(tile[1])
         if fp8 is not None:
             d.flags |= _lib.IN_FP8
             d.col_scale, d.stride_col_scale = _p(fp8[0]), fp8[1]
@@ -400,6 +404,10 @@ class PairModel:
         # bf16 path: the blocks' LayerNorms folded into the following projections (ln_fold;
         # LN_STATS / LN_FOLD epilogues) instead of separate LayerNorm launches
         self.lnfold = os.environ.get("M3S_LNFOLD", "1") != "0"
+        # tile configurations (TileCfg, split-K) of the prefetched encoder's projections,
+        # measured in the pipelined C3 step (encode(concurrent=True)); {} = per-shape table
+        # (T128W8 residual GEMMs: 212.8 → 224.5 frames/s, profiles/r02_enc_tile_sweep.txt)
+        self.enc_tiles_concurrent = {"proj": (12, 1), "fc2": (12, 1)}
         # split heads: the local-feature MLP runs on the side chain ahead of the MASt3R heads
         self.lf_side = os.environ.get("M3S_LF_SIDE", "1") != "0"
         self._tag = None      # buffer-key prefix of the head set being issued (split heads)
@@ -477,27 +485,27 @@ class PairModel:
         return t
 
     # ---- encoder: PatchEmbed + 24 blocks + enc_norm (batch of B images as M = B*S) ----
-    def encode(self, img, out=None):
+    def encode(self, img, out=None, concurrent=False):
         """img f32 [B,3,H,W] → feat bf16 [B,S,E], pos int64 [B,S,2].
-        M3S_ENC_TILE="cfg:splits" (experiment knob): the encoder's GEMMs take that tile
-        configuration (e.g. fewer, larger tiles while it shares the chip with the tracking
-        chain) instead of the per-shape table."""
+        concurrent: this encoder shares the chip with the tracking chain (the next frame's
+        prefetch, frontend.FramePipeline): its GEMMs take the tile configurations of
+        `enc_tiles_concurrent` (measured in the pipelined C3 step) instead of the
+        per-shape table, which is tuned for launches that have the chip to themselves.
+        M3S_ENC_TILE (experiment knob, tools/enc_tile_sweep.sh): "cfg:splits" for all four
+        projections, or "qkv=cfg:splits,proj=...,fc1=...,fc2=..."; "table" = no hints."""
+        tiles = self.enc_tiles_concurrent if concurrent else {}
         knob = os.environ.get("M3S_ENC_TILE")
         if knob:
-            cfg, _, sp = knob.partition(":")
-            saved = {k: os.environ.get(k) for k in ("M3S_GEMM_TILE", "M3S_GEMM_SPLITS")}
-            os.environ["M3S_GEMM_TILE"], os.environ["M3S_GEMM_SPLITS"] = cfg, sp or "1"
-            try:
-                return self._encode(img, out)
-            finally:
-                for k, v in saved.items():
-                    if v is None:
-                        os.environ.pop(k, None)
-                    else:
-                        os.environ[k] = v
-        return self._encode(img, out)
+            tiles = {}
+            if knob != "table":
+                for part in knob.split(","):
+                    name, _, val = part.rpartition("=")
+                    cfg, _, sp = val.partition(":")
+                    for n in ([name] if name else ["qkv", "proj", "fc1", "fc2"]):
+                        tiles[n] = (int(cfg), int(sp or 1))
+        return self._encode(img, out, tiles)
 
-    def _encode(self, img, out=None):
+    def _encode(self, img, out=None, tiles=None):
         o, a, W = self.ops, self.a, self.w
         B, _, H, Wd = img.shape
         gh, gw = H // a.patch, Wd // a.patch
@@ -527,14 +535,15 @@ class PairModel:
         if fold:
             for i in range(a.enc_depth):
                 o.gemm(xb, P["qkv_wf"][i], qkv, M, 3 * E, E, bias=P["qkv_c2"][i],
-                       rope=(rt, 2 * E, S), ln_fold=(st, P["qkv_c1"][i], 0))
+                       rope=(rt, 2 * E, S), ln_fold=(st, P["qkv_c1"][i], 0), tile=tiles.get("qkv"))
                 o.attn(qkv, 3 * E, S * 3 * E, qkv[:, E:], qkv[:, 2 * E:], 3 * E, S * 3 * E, att,
                        E, S * E, B, a.enc_heads, S, S)
-                o.gemm(att, P["proj_w"][i], x, M, E, E, bias=P["proj_b"][i], R=x, **R32S)
+                o.gemm(att, P["proj_w"][i], x, M, E, E, bias=P["proj_b"][i], R=x,
+                       tile=tiles.get("proj"), **R32S)
                 o.gemm(xb, P["fc1_wf"][i], hid, M, a.mlp_ratio * E, E, bias=P["fc1_c2"][i],
-                       flags=_lib.EPI_GELU, ln_fold=(st, P["fc1_c1"][i], 0))
+                       flags=_lib.EPI_GELU, ln_fold=(st, P["fc1_c1"][i], 0), tile=tiles.get("fc1"))
                 o.gemm(hid, P["fc2_w"][i], x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][i], R=x,
-                       **R32S)
+                       tile=tiles.get("fc2"), **R32S)
         for i in range(a.enc_depth if not fold else 0):
             o.ln(x, P["ln1_g"][i], P["ln1_b"][i], xn, M, E)
             # qkv projection with RoPE2D on q and k fused into the epilogue

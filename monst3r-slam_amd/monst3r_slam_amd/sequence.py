@@ -250,7 +250,7 @@ class SequenceLoop:
                 pipe.side.wait_stream(main)
                 with torch.cuda.stream(pipe.side):
                     self.gather(self.img_next, 1)
-                    m.encode(self.img_next, out=pipe.feat[(k + 1) % 2])
+                    m.encode(self.img_next, out=pipe.feat[(k + 1) % 2], concurrent=True)
                 feat_i = pipe.feat[k % 2]
                 out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i, split_heads=split)
             else:

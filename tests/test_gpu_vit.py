@@ -546,9 +546,11 @@ def _ln_stats_ref(x):
 
 @pytest.mark.parametrize("M,N,K,batch,split_k", [(768, 768, 3072, 4, 1), (768, 1024, 1024, 1, 2),
                                                  (768, 1024, 4096, 1, 0), (200, 256, 96, 2, 1)])
-def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k):
+@pytest.mark.parametrize("tile", [None, 12, 13])
+def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k, tile):
     """LN_STATS: the residual GEMM also stores bf16(x) and per-128-column (mean, M2) of the
-    stored f32 rows — in the main epilogue and in the split-K reduce (split_k 2 / auto)."""
+    stored f32 rows — in the main epilogue and in the split-K reduce (split_k 2 / auto);
+    tile: the descriptor's tile hint (the prefetched encoder's residual GEMMs)."""
     from monst3r_slam_amd import _lib
     g = torch.Generator(device=dev).manual_seed(11)
     A = torch.randn(batch, M, K, device=dev, generator=g).bfloat16()
@@ -560,7 +562,7 @@ def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k):
     st = torch.full((batch, M, N // 128, 2), float("nan"), device=dev)
     ops.gemm(A, B, x, M, N, K, batch, sA=M * K, sB=N * K, sC=M * N, bias=bias, sBias=N, R=x,
              sR=M * N, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, ln_stats=(xb, st),
-             split_k=split_k)
+             split_k=split_k, tile=(tile, max(split_k, 1)) if tile else None)
     assert _rel(x, ref) < 1e-3
     assert torch.equal(xb, x.bfloat16())                      # the bf16 copy of what x holds
     sr = _ln_stats_ref(x)
@@ -723,3 +725,18 @@ def test_gemm_fused_splitk(ops, dev, monkeypatch, tile, splits, epi, fused):
     if epi == "res_stats":
         assert torch.equal(out1[1], out1[0].bfloat16())
     assert int(ops.counters.abs().sum()) == 0
+
+
+@pytest.mark.gpu
+def test_concurrent_encoder_tiles_match_table(dev):
+    """encode(concurrent=True) (the prefetched encoder: tile hints for its residual GEMMs)
+    against the per-shape-table encoder at 384x512: same projections, different tiles (and
+    split-K partitions), so equal up to f32 summation order."""
+    from monst3r_slam_amd import model as Mdl
+    m, _ = Mdl.build(dev)
+    assert m.enc_tiles_concurrent, "no concurrent tile hints configured"
+    img = torch.rand(1, 3, 384, 512, device=dev, generator=torch.Generator(device=dev).manual_seed(5)) * 2 - 1
+    fa = m.encode(img)[0].float().clone()
+    fb = m.encode(img, concurrent=True)[0].float().clone()
+    assert torch.isfinite(fb).all()
+    assert float((fa - fb).norm() / fa.norm()) < 5e-3
