@@ -54,6 +54,7 @@ class Ops:
         self.lib = _lib.load()
         self.dev = dev
         self.record = None  # list → (descriptor, flops, fp8) per GEMM launch (bench roofline)
+        self.tile_default = None  # tile hint for launches issued without one (side chains)
         # f32 split-K / attention-split scratch and the split-K tile counters (zeroed once,
         # left zero by the kernels), one set per stream (the M = 768 GEMMs split K when
         # their grid cannot fill 256 CUs; concurrent streams must not share them)
@@ -94,6 +95,8 @@ class Ops:
         gamma-folded weight; the epilogue applies the normalisation (bias = c2).
         tile = (tile configuration, split-K): the descriptor's tile_hint instead of the
         per-shape table (PairModel.encode(concurrent=True))."""
+        if tile is None:
+            tile = self.tile_default
         d = _lib.GemmDesc()
         d.A, d.lda, d.strideA = _p(A), lda if lda is not None else K, sA
         d.B, d.ldb, d.strideB = _p(B), ldb if ldb is not None else K, sB
@@ -378,6 +381,23 @@ class PackedWeights:
 # ---------------------------------------------------------------------------------------
 # model runner
 # ---------------------------------------------------------------------------------------
+def _tile_knob(env, names, default):
+    """GEMM tile hints {projection: (TileCfg, split-K)} from an experiment knob: "cfg:splits"
+    for every projection, "name=cfg:splits,..." for some (the others: per-shape table),
+    "table" for none; unset → default."""
+    knob = os.environ.get(env)
+    if not knob:
+        return default
+    tiles = {}
+    if knob != "table":
+        for part in knob.split(","):
+            name, _, val = part.rpartition("=")
+            cfg, _, sp = val.partition(":")
+            for n in ([name] if name else names):
+                tiles[n] = (int(cfg), int(sp or 1))
+    return tiles
+
+
 class PairModel:
     """Frame/keyframe pair inference.  Buffers are allocated once per image size."""
 
@@ -408,6 +428,8 @@ class PairModel:
         # measured in the pipelined C3 step (encode(concurrent=True)); {} = per-shape table
         # (T128W8 residual GEMMs: 212.8 → 224.5 frames/s, profiles/r02_enc_tile_sweep.txt)
         self.enc_tiles_concurrent = {"proj": (12, 1), "fc2": (12, 1)}
+        self.dec_tiles = {}   # decoder projections' tile hints (M3S_DEC_TILE; {} = table)
+        self.side_tiles = {}  # split-heads side chain (M3S_SIDE_TILE: lf / dpt; {} = table)
         # split heads: the local-feature MLP runs on the side chain ahead of the MASt3R heads
         self.lf_side = os.environ.get("M3S_LF_SIDE", "1") != "0"
         self._tag = None      # buffer-key prefix of the head set being issued (split heads)
@@ -493,16 +515,8 @@ class PairModel:
         per-shape table, which is tuned for launches that have the chip to themselves.
         M3S_ENC_TILE (experiment knob, tools/enc_tile_sweep.sh): "cfg:splits" for all four
         projections, or "qkv=cfg:splits,proj=...,fc1=...,fc2=..."; "table" = no hints."""
-        tiles = self.enc_tiles_concurrent if concurrent else {}
-        knob = os.environ.get("M3S_ENC_TILE")
-        if knob:
-            tiles = {}
-            if knob != "table":
-                for part in knob.split(","):
-                    name, _, val = part.rpartition("=")
-                    cfg, _, sp = val.partition(":")
-                    for n in ([name] if name else ["qkv", "proj", "fc1", "fc2"]):
-                        tiles[n] = (int(cfg), int(sp or 1))
+        tiles = _tile_knob("M3S_ENC_TILE", ("qkv", "proj", "fc1", "fc2"),
+                           self.enc_tiles_concurrent if concurrent else {})
         return self._encode(img, out, tiles)
 
     def _encode(self, img, out=None, tiles=None):
@@ -701,6 +715,9 @@ class PairModel:
         Dm = a.mlp_ratio * D
         xc = xb                                  # the current bf16 copy of x
         zs = dict(sA=S * D, sC=S * D, wmod=wm)   # the per-problem strides of a [Z,S,D] A
+        # tile hints (M3S_DEC_TILE experiment knob, as M3S_ENC_TILE; default: the table)
+        tl = _tile_knob("M3S_DEC_TILE", ("qkv", "proj", "q", "cproj", "fc1", "fc2"),
+                        self.dec_tiles).get
         for i in range(a.dec_depth):
             P = W.dec[i]
             R32S = dict(R=x, sR=S * D, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32,
@@ -709,27 +726,27 @@ class PairModel:
             # x of the layer's start (the reference's y_ = norm_y(y) before x changes)
             o.gemm(xc, P["qkvkv_wf"], qkv, S, F5, D, Z, sA=S * D, sB=F5 * D, sC=S * F5,
                    bias=P["qkvkv_c2"], sBias=F5, rope=(rt, 3 * D, S), wmod=wm,
-                   ln_fold=(st, P["qkvkv_c1"], 0))
+                   ln_fold=(st, P["qkvkv_c1"], 0), tile=tl("qkv"))
             o.attn(qkv, F5, S * F5, qkv[:, :, D:], qkv[:, :, 3 * D:], F5, S * F5, att,
                    D, S * D, Z, a.dec_heads, S, S)
             o.gemm(att, P["proj_w"], x, S, D, D, Z, sB=D * D, bias=P["proj_b"], sBias=D, **zs,
-                   **R32S)
+                   tile=tl("proj"), **R32S)
             o.gemm(xb, P["q_wf"], q, S, D, D, Z, sB=D * D, bias=P["q_c2"], sBias=D,
-                   rope=(rt, D, S), ln_fold=(st, P["q_c1"], 0), **zs)
+                   rope=(rt, D, S), ln_fold=(st, P["q_c1"], 0), tile=tl("q"), **zs)
             # k' / v' of problem z were computed in problem z ^ 1's rows
             o.attn(q, D, S * D, qkv[:, :, 2 * D:], qkv[:, :, 4 * D:], F5, S * F5, att, D, S * D,
                    Z, a.dec_heads, S, S, kv_xor=1)
             o.gemm(att, P["cproj_w"], x, S, D, D, Z, sB=D * D, bias=P["cproj_b"], sBias=D, **zs,
-                   **R32S)
+                   tile=tl("cproj"), **R32S)
             o.gemm(xb, P["fc1_wf"], hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm,
                    bias=P["fc1_c2"], sBias=Dm, flags=_lib.EPI_GELU, wmod=wm,
-                   ln_fold=(st, P["fc1_c1"], 0))
+                   ln_fold=(st, P["fc1_c1"], 0), tile=tl("fc1"))
             xc = xb
             if (i + 1) in hk:
                 xc = self._buf(f"h{i + 1}", (Z, S, D), BF16)
                 hooks[f"h{i + 1}"] = xc
             o.gemm(hid, P["fc2_w"], x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D,
-                   bias=P["fc2_b"], sBias=D, wmod=wm,
+                   bias=P["fc2_b"], sBias=D, wmod=wm, tile=tl("fc2"),
                    **dict(R32S, ln_stats=(xc, st)))
             if (i + 1) in hk and on_hook is not None:
                 on_hook(f"h{i + 1}", hooks)
@@ -843,17 +860,24 @@ class PairModel:
             side.wait_stream(main)
             for ev in self._early_ev:
                 side.wait_event(ev)
+            # side-chain tile hints (M3S_SIDE_TILE experiment knob: lf / dpt; default table)
+            st = _tile_knob("M3S_SIDE_TILE", ("lf", "dpt"), self.side_tiles)
             with torch.cuda.stream(side):
                 if self.lf_side:
                     # the local features (needed by the matching) first on the side chain,
                     # overlapping the MonST3R heads; then the MASt3R heads (joined later)
                     self._wm = wm
+                    self.ops.tile_default = st.get("lf")
                     desc, desc16, dconf, _ = self._local_features(hooks, G, S, E, D, H, W)
                     ev_lf = torch.cuda.Event()
                     ev_lf.record(side)
                 sub = {k: v[2:4] for k, v in hooks.items()}
-                self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4],
-                          R=None if R is None else [r[2:4] for r in R])
+                self.ops.tile_default = st.get("dpt")
+                try:
+                    self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4],
+                              R=None if R is None else [r[2:4] for r in R])
+                finally:
+                    self.ops.tile_default = None
                 self._ev_heads = torch.cuda.Event()
                 self._ev_heads.record(side)
         # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle
