@@ -28,7 +28,7 @@ TILES = {1: "128x128", 2: "64x128 2/CU", 7: "128x128 2/CU", 8: "96x128",
 SPLITS = (1, 2, 3, 4, 6, 8)
 
 
-def record(m, dev, graph, split_heads=False):
+def record(m, dev, graph, split_heads=False, c5=False):
     img = torch.rand(1, 3, 384, 512, device=dev) * 2 - 1
     feat, _ = m.encode(img)
     feat = feat.clone()
@@ -36,6 +36,15 @@ def record(m, dev, graph, split_heads=False):
     m.pair(img, feat_j=feat)
     if split_heads:  # the C3 step's head launches (MonST3R / MASt3R heads as two batch-2 sets)
         m.pair(img, feat_j=feat, split_heads=True)
+    if c5:  # the configs[4] 512x512 frame's bf16 launches (heads) beside its fp8 ViT
+        m.set_fp8(True)
+        img5 = torch.rand(1, 3, 512, 512, device=dev) * 2 - 1
+        f5 = m.encode(img5)[0].clone()
+        feat_i, pos = m.encode(img5)
+        m.mono(feat_i, 512, 512)
+        hooks = m.decode(feat_i[0], f5[0], pos, 32, 32)
+        m.heads(hooks, 32, 32, 512, 512)
+        m.set_fp8(False)
     if graph:
         m.mono(feat, 384, 512)
         f4 = feat.expand(4, -1, -1).contiguous()
@@ -78,13 +87,14 @@ def main():
                     help="restrict the sweep to these tile configs")
     ap.add_argument("--gemm-only-m", type=int, default=0, help="only launch classes with this M")
     ap.add_argument("--split-heads", action="store_true", help="also the split-heads pair shapes")
+    ap.add_argument("--c5", action="store_true", help="also the 512x512 fp8 frame's bf16 launches")
     ap.add_argument("--min-m", type=int, default=0, help="only launch classes with M >= this")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     m, _ = Mdl.build(dev)
     for k in ("M3S_GEMM_TILE", "M3S_GEMM_SPLITS", "M3S_GEMM_FUSED"):
         os.environ.pop(k, None)
-    groups = record(m, dev, args.graph, args.split_heads)
+    groups = record(m, dev, args.graph, args.split_heads, args.c5)
     res = []
     for key, lst in groups.items():
         M, N, K, batch, flags, mode = key
