@@ -45,6 +45,8 @@ extern template int launch<64, 128, 64, 2, 2, 6, 1>(Args&, int, hipStream_t);
 extern template int launch<128, 128, 64, 2, 2, 4, 1>(Args&, int, hipStream_t);
 extern template int launch<64, 128, 64, 2, 2, 3, 2>(Args&, int, hipStream_t);
 extern template int launch<64, 128, 64, 2, 2, 3, 2, true>(Args&, int, hipStream_t);
+extern template int launch<128, 128, 64, 4, 2, 3, 1, true>(Args&, int, hipStream_t);
+extern template int launch<256, 128, 64, 4, 2, 3, 1, true>(Args&, int, hipStream_t);
 extern template int launch<128, 128, 64, 2, 2, 2, 2, true>(Args&, int, hipStream_t);
 extern template int launch<128, 128, 64, 2, 2, 3, 1, true>(Args&, int, hipStream_t);
 extern template int launch<128, 128, 64, 4, 2, 3, 1>(Args&, int, hipStream_t);
@@ -296,6 +298,8 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     switch (cfg) {
       case T64: return launch<64, 128, 64, 2, 2, 3, 2, true>(a, d->batch, s);
       case T128O2: return launch<128, 128, 64, 2, 2, 2, 2, true>(a, d->batch, s);
+      case T128W8: return launch<128, 128, 64, 4, 2, 3, 1, true>(a, d->batch, s);
+      case T256W8: return launch<256, 128, 64, 4, 2, 3, 1, true>(a, d->batch, s);
       default: return launch<128, 128, 64, 2, 2, 3, 1, true>(a, d->batch, s);
     }
   }

@@ -333,13 +333,17 @@ def _fp8(t):
 @pytest.mark.parametrize("M,N,K,batch,mode", [(768, 3072, 1024, 1, "gelu8"), (768, 768, 768, 4, "res"),
                                               (200, 384, 256, 2, "plain"), (768, 1024, 4096, 1, "res"),
                                               (768, 2304, 768, 4, "rope")])
-def test_gemm_fp8(ops, dev, M, N, K, batch, mode):
+@pytest.mark.parametrize("tile", ["0", "12", "13"])
+def test_gemm_fp8(ops, dev, monkeypatch, M, N, K, batch, mode, tile):
     """OCP e4m3 operands on the scaled 32x32x64 MFMA, per-column dequant scale, the ViT
     epilogue sets (GELU → fp8 out, f32 residual incl. split-K, RoPE), weight_mod batches.
     Reference: the same e4m3 values in fp32 (products exact, f32 sums: tolerance 1e-3;
-    fp8 outputs compared after the same e4m3 rounding of the reference: 1 ulp ≈ 2^-3)."""
+    fp8 outputs compared after the same e4m3 rounding of the reference: 1 ulp ≈ 2^-3).
+    tile: the table / heuristic (0), or the 8-wave 128x128 / 256x128 configurations."""
     from monst3r_slam_amd import _lib
     from oracle import vit_ref as V
+    if tile != "0":
+        monkeypatch.setenv("M3S_GEMM_TILE", tile)
     g = torch.Generator(device=dev).manual_seed(21)
     A = _fp8(torch.randn(batch, M, K, device=dev, generator=g))
     W = torch.randn(2, N, K, device=dev, generator=g) / K ** 0.5

@@ -28,7 +28,7 @@ TILES = {1: "128x128", 2: "64x128 2/CU", 7: "128x128 2/CU", 8: "96x128",
 SPLITS = (1, 2, 3, 4, 6, 8)
 
 
-def record(m, dev, graph, split_heads=False, c5=False):
+def record(m, dev, graph, split_heads=False, c5=False, fp8=False):
     img = torch.rand(1, 3, 384, 512, device=dev) * 2 - 1
     feat, _ = m.encode(img)
     feat = feat.clone()
@@ -53,7 +53,9 @@ def record(m, dev, graph, split_heads=False, c5=False):
     rec, m.ops.record = m.ops.record, None
     groups = collections.OrderedDict()
     for d, fl, f8 in rec:
-        if f8:
+        if f8 and not fp8:
+            continue
+        if fp8 and not f8:
             continue
         key = (d.M, d.N, d.K, d.batch, d.flags, d.mode)
         groups.setdefault(key, []).append((d, fl))
@@ -88,13 +90,14 @@ def main():
     ap.add_argument("--gemm-only-m", type=int, default=0, help="only launch classes with this M")
     ap.add_argument("--split-heads", action="store_true", help="also the split-heads pair shapes")
     ap.add_argument("--c5", action="store_true", help="also the 512x512 fp8 frame's bf16 launches")
+    ap.add_argument("--fp8", action="store_true", help="with --c5: its fp8 launches instead")
     ap.add_argument("--min-m", type=int, default=0, help="only launch classes with M >= this")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     m, _ = Mdl.build(dev)
     for k in ("M3S_GEMM_TILE", "M3S_GEMM_SPLITS", "M3S_GEMM_FUSED"):
         os.environ.pop(k, None)
-    groups = record(m, dev, args.graph, args.split_heads, args.c5)
+    groups = record(m, dev, args.graph, args.split_heads, args.c5, args.fp8)
     res = []
     for key, lst in groups.items():
         M, N, K, batch, flags, mode = key
