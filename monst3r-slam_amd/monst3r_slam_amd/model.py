@@ -429,7 +429,13 @@ class PairModel:
         # (T128W8 residual GEMMs: 212.8 → 224.5 frames/s, profiles/r02_enc_tile_sweep.txt)
         self.enc_tiles_concurrent = {"proj": (12, 1), "fc2": (12, 1)}
         self.dec_tiles = {}   # decoder projections' tile hints (M3S_DEC_TILE; {} = table)
+        # ... of the per-model split decoder (two batch-2 chains beside the prefetched
+        # encoder), measured in the pipelined step: 226.9 → 232.7 frames/s
+        self.dec_tiles_split = {"qkv": (13, 1), "fc2": (12, 1)}
         self.side_tiles = {}  # split-heads side chain (M3S_SIDE_TILE: lf / dpt; {} = table)
+        # the pair decoder split by model onto two streams (decode_multi; M3S_DEC_SPLIT=0
+        # restores the single batch-4 chain): 214.0 → 218.3 frames/s (2 × A/B)
+        self.dec_split = os.environ.get("M3S_DEC_SPLIT", "1") == "1"
         # split heads: the local-feature MLP runs on the side chain ahead of the MASt3R heads
         self.lf_side = os.environ.get("M3S_LF_SIDE", "1") != "0"
         self._tag = None      # buffer-key prefix of the head set being issued (split heads)
@@ -614,6 +620,20 @@ class PairModel:
                ln_stats=(xb, st) if fold else None)
         if on_hook is not None:
             on_hook("h0", {"h0": h0})
+        if fold and self.dec_split and models == 2 and G == 1 and on_hook is None:
+            # the two models' decoders (z 0-1 MonST3R, 2-3 MASt3R: independent chains) as two
+            # batch-2 chains on two streams, so each fills the other's kernel tails / gaps
+            main = torch.cuda.current_stream(self.dev)
+            side = self.side[1]
+            side.wait_stream(main)
+            hooks = self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm, None, part=0)
+            with torch.cuda.stream(side):
+                self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm, None, part=1)
+            main.wait_stream(side)
+            h12 = self._buf("h12", (Z, S, D), BF16)
+            o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
+            hooks["h12"] = h12
+            return hooks
         if fold:
             return self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm, on_hook)
         adt = U8 if self.fp8 else BF16
@@ -695,7 +715,7 @@ class PairModel:
             on_hook("h12", hooks)
         return hooks
 
-    def _decode_folded(self, x, xb, st, h0, Z, S, E, D, gh, gw, wm, on_hook=None):
+    def _decode_folded(self, x, xb, st, h0, Z, S, E, D, gh, gw, wm, on_hook=None, part=None):
         """decode_multi's blocks (croco/blocks.py:172-195 DecoderBlock) with every LayerNorm
         folded into the projection that consumes it (ln_fold): the residual GEMMs write x
         (f32), its bf16 copy and row statistics; qkv (norm1), the cross-attention k/v
@@ -710,6 +730,15 @@ class PairModel:
         att = self._buf("dec_att", (Z, S, D), BF16)
         hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), BF16)
         hooks = {"h0": h0}
+        hook_bufs = {k: self._buf(f"h{k}", (Z, S, D), BF16) for k in a.hooks[1:3]}
+        sl = None
+        if part is not None:
+            # one model's two problems (decode_multi's per-model split): every buffer, the
+            # weight stacks and the statistics sliced to z in [2·part, 2·part + 2), weight_mod 2
+            sl = slice(2 * part, 2 * part + 2)
+            qkv, q, att, hid, x, xb, st = (t[sl] for t in (qkv, q, att, hid, x, xb, st))
+            hook_bufs = {k: v[sl] for k, v in hook_bufs.items()}
+            Z, wm = 2, 2
         rt = self.rope_tab(gh, gw)
         hk = set(a.hooks[1:3])
         Dm = a.mlp_ratio * D
@@ -717,9 +746,11 @@ class PairModel:
         zs = dict(sA=S * D, sC=S * D, wmod=wm)   # the per-problem strides of a [Z,S,D] A
         # tile hints (M3S_DEC_TILE experiment knob, as M3S_ENC_TILE; default: the table)
         tl = _tile_knob("M3S_DEC_TILE", ("qkv", "proj", "q", "cproj", "fc1", "fc2"),
-                        self.dec_tiles).get
+                        self.dec_tiles if part is None else self.dec_tiles_split).get
         for i in range(a.dec_depth):
             P = W.dec[i]
+            if sl is not None:
+                P = {k: v[sl] for k, v in P.items()}
             R32S = dict(R=x, sR=S * D, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32,
                         ln_stats=(xb, st))
             # norm1 → qkv of problem z and norm_y → cross k/v of problem z ^ 1, one GEMM over
@@ -743,13 +774,16 @@ class PairModel:
                    ln_fold=(st, P["fc1_c1"], 0), tile=tl("fc1"))
             xc = xb
             if (i + 1) in hk:
-                xc = self._buf(f"h{i + 1}", (Z, S, D), BF16)
-                hooks[f"h{i + 1}"] = xc
+                xc = hook_bufs[i + 1]
+                hooks[f"h{i + 1}"] = self._buf(f"h{i + 1}", (2 * wm if sl is not None else Z,
+                                                             S, D), BF16)
             o.gemm(hid, P["fc2_w"], x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D,
                    bias=P["fc2_b"], sBias=D, wmod=wm, tile=tl("fc2"),
                    **dict(R32S, ln_stats=(xc, st)))
             if (i + 1) in hk and on_hook is not None:
                 on_hook(f"h{i + 1}", hooks)
+        if sl is not None:
+            return hooks
         h12 = self._buf("h12", (Z, S, D), BF16)
         o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
         hooks["h12"] = h12

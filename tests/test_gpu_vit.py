@@ -744,3 +744,27 @@ def test_concurrent_encoder_tiles_match_table(dev):
     fb = m.encode(img, concurrent=True)[0].float().clone()
     assert torch.isfinite(fb).all()
     assert float((fa - fb).norm() / fa.norm()) < 5e-3
+
+
+@pytest.mark.gpu
+def test_decoder_split_by_model_matches_batched(dev):
+    """dec_split (the two models' decoders as two batch-2 chains on two streams) against the
+    batch-4 decoder: the same math on per-shape tiles that may split K differently, so
+    equal up to f32 summation order."""
+    from monst3r_slam_amd import model as Mdl
+    m, _ = Mdl.build(dev)
+    g = torch.Generator(device=dev).manual_seed(9)
+    img = torch.rand(1, 3, 384, 512, device=dev, generator=g) * 2 - 1
+    feat_k = m.encode(torch.rand(1, 3, 384, 512, device=dev, generator=g) * 2 - 1)[0].clone()
+    outs = []
+    for split in (False, True):
+        m.dec_split = split
+        o = m.pair(img, feat_j=feat_k)
+        torch.cuda.synchronize()
+        outs.append({k: v.float().clone() for k, v in o.items() if v is not None})
+    m.dec_split = False
+    a, b = outs
+    for k in ("X", "C", "D", "Q", "mast3r_X", "mast3r_C"):
+        assert torch.isfinite(b[k]).all(), k
+        rel = float((a[k] - b[k]).norm() / a[k].norm())
+        assert rel < 2e-2, (k, rel)
