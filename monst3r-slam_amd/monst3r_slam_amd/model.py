@@ -426,8 +426,10 @@ class PairModel:
         self.lnfold = os.environ.get("M3S_LNFOLD", "1") != "0"
         # tile configurations (TileCfg, split-K) of the prefetched encoder's projections,
         # measured in the pipelined C3 step (encode(concurrent=True)); {} = per-shape table
-        # (T128W8 residual GEMMs: 212.8 → 224.5 frames/s, profiles/r02_enc_tile_sweep.txt)
-        self.enc_tiles_concurrent = {"proj": (12, 1), "fc2": (12, 1)}
+        # (T128W8 residual GEMMs: 212.8 → 224.5 frames/s; with the split decoder, T256W8
+        # qkv / fc1: 214.9 → 221.3, profiles/r02_enc_tile_sweep.txt)
+        self.enc_tiles_concurrent = {"qkv": (13, 1), "proj": (12, 1), "fc1": (13, 1),
+                                     "fc2": (12, 1)}
         self.dec_tiles = {}   # decoder projections' tile hints (M3S_DEC_TILE; {} = table)
         # ... of the per-model split decoder (two batch-2 chains beside the prefetched
         # encoder), measured in the pipelined step: 226.9 → 232.7 frames/s
