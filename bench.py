@@ -214,10 +214,14 @@ def gemm_replay(model, run, dev, reps=20):
 
 
 def gemm_roofline(model, img, feat_k, dev):
-    """GEMM launches of one pair inference (serial schedule), replayed back-to-back."""
+    """GEMM launches of one pair inference (serial schedule: one batch-4 decoder chain and
+    the per-shape table, no concurrency tile hints), replayed back-to-back.  The C3 step's
+    split decoder / prefetched encoder issue launches tuned to share the chip (DESIGN §4);
+    replayed alone, one after another, they would measure a schedule that never runs."""
     serial, model.serial = model.serial, True
+    split, model.dec_split = model.dec_split, False
     r = gemm_replay(model, lambda: model.pair(img, feat_j=feat_k), dev)["all"]
-    model.serial = serial
+    model.serial, model.dec_split = serial, split
     return r
 
 
@@ -661,7 +665,8 @@ def main():
                          "traffic_per_pair_bytes": pmc["hbm_bytes_per_pair"] if pmc else None,
                          "l2_hit_rate": pmc["l2_hit_rate"] if pmc else None,
                          "kernel": "gemm_kernel (bf16 MFMA GEMM / implicit conv)",
-                         "timing": "the pair's GEMM launches replayed back-to-back in one HIP "
+                         "timing": "the serial pair's GEMM launches (batch-4 decoder, "
+                                   "per-shape table) replayed back-to-back in one HIP "
                                    "graph, HIP events on its stream (bench.gemm_replay)",
                          "gemm_launches_per_pair": roof["launches"],
                          "gemm_ms_per_pair": roof["gemm_ms"],
