@@ -124,10 +124,15 @@ class SlamLoop:
         if idx is None:
             return
         kf, tk = self.keyframes, self.tracker.kf
+        # the tracker's on-device fusion is frame.py's weighted_pointmap mode, the only mode
+        # in which N_updates == N (every other mode resets N to 1 while N_updates grows)
+        mode = self.tracker.cfg["tracking"]["filtering_mode"]
+        if mode != "weighted_pointmap":
+            raise NotImplementedError(f"SlamLoop fuses keyframes as weighted_pointmap, not {mode}")
+        n_upd = kf._h_Nu[idx] + (int(round(float(tk.N.item()))) - kf._h_N[idx])
         kf.X[idx].copy_(tk.X_canon)
         kf.C[idx].copy_(tk.C)
-        kf.set_counts([idx], N=int(round(float(tk.N.item()))),
-                      N_updates=int(round(float(tk.N.item()))))
+        kf.set_counts([idx], N=int(round(float(tk.N.item()))), N_updates=n_upd)
 
     def _refresh_pose(self):
         idx = getattr(self, "_tracked_kf", None)

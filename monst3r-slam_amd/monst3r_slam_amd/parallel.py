@@ -116,8 +116,10 @@ def shard_keyframe_features(frames, idx, encode, group=None):
 
 
 def keyframe_record_bytes(n):
-    """Bytes of one packed keyframe record: X_canon f32 [n,3], C f32 [n], N i32, T_WC f32 [8]."""
-    return (3 * n + n) * 4 + 4 + 32
+    """Bytes of one packed keyframe record: X_canon f32 [n,3], C f32 [n], N i32, N_updates i32,
+    T_WC f32 [8].  N and N_updates are separate counters (frame.py update_pointmap: only
+    the weighted_pointmap mode keeps them equal)."""
+    return (3 * n + n) * 4 + 8 + 32
 
 
 def all_gather_keyframes(frames, idx, owner, group=None):
@@ -159,7 +161,8 @@ def all_gather_keyframes(frames, idx, owner, group=None):
 def _pack_keyframe(frames, k, rec, n):
     rec[:16 * n] = torch.cat((frames.X[k].reshape(-1), frames.C[k].reshape(-1))).view(torch.uint8)
     rec[16 * n:16 * n + 4] = frames.N[k:k + 1].to(torch.int32).view(torch.uint8)
-    rec[16 * n + 4:] = frames.T_WC[k].reshape(8).contiguous().view(torch.uint8)
+    rec[16 * n + 4:16 * n + 8] = frames.N_updates[k:k + 1].to(torch.int32).view(torch.uint8)
+    rec[16 * n + 8:] = frames.T_WC[k].reshape(8).contiguous().view(torch.uint8)
 
 
 def _unpack_keyframes(frames, idx, recs, n):
@@ -168,15 +171,17 @@ def _unpack_keyframes(frames, idx, recs, n):
         xc = rec[:16 * n].view(torch.float32)
         frames.X[k].copy_(xc[:3 * n].reshape(n, 3))
         frames.C[k].copy_(xc[3 * n:].reshape(n, 1))
-        frames.N[k] = rec[16 * n:16 * n + 4].view(torch.int32)[0]
-        frames.T_WC[k].copy_(rec[16 * n + 4:].view(torch.float32).reshape(1, 8))
-        counts[k] = rec[16 * n:16 * n + 4].view(torch.int32)
+        cnt = rec[16 * n:16 * n + 8].view(torch.int32)      # (N, N_updates)
+        frames.N[k] = cnt[0]
+        frames.N_updates[k] = cnt[1]
+        frames.T_WC[k].copy_(rec[16 * n + 8:].view(torch.float32).reshape(1, 8))
+        counts[k] = cnt
     # host mirrors of the counts (one device read for all of them)
     if counts:
         ks = list(counts)
-        vals = torch.cat([counts[k] for k in ks]).tolist()
-        for k, v in zip(ks, vals):
-            frames._h_N[k] = frames._h_Nu[k] = int(v)
+        vals = torch.stack([counts[k] for k in ks]).tolist()
+        for k, (vn, vu) in zip(ks, vals):
+            frames._h_N[k], frames._h_Nu[k] = int(vn), int(vu)
 
 
 class ShardedFactorGraph(FactorGraph):

@@ -170,6 +170,9 @@ class SequenceLoop:
         self.log_T = torch.zeros((seq.n_frames, 8), dtype=torch.float32, device=dev)
         self.img_cur = torch.empty((1, 3, seq.h, seq.w), dtype=torch.float32, device=dev)
         self.img_next = torch.empty_like(self.img_cur)
+        # pipelined: the side stream's gather reads the device frame counter that advance()
+        # rewrites on the main stream; this event orders advance() after the gather
+        self._gathered = torch.cuda.Event() if dev.type == "cuda" else None
 
     # ---- INIT (main_monster_slam.py:279-290) ----
     def reset(self, first=0, parity=0):
@@ -250,6 +253,7 @@ class SequenceLoop:
                 pipe.side.wait_stream(main)
                 with torch.cuda.stream(pipe.side):
                     self.gather(self.img_next, 1)
+                    self._gathered.record(pipe.side)
                     m.encode(self.img_next, out=pipe.feat[(k + 1) % 2], concurrent=True)
                 feat_i = pipe.feat[k % 2]
                 out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i, split_heads=split)
@@ -261,6 +265,8 @@ class SequenceLoop:
             out = self._outputs()
         self.pair_outputs(out)
         res = tr.track_outputs(out, self.T_prev)
+        if pipe is not None and m is not None:
+            main.wait_event(self._gathered)   # the gather read `frame` before advance rewrites it
         self.advance(res, out, feat_i if m is not None else None)
         if m is not None:
             m.join()

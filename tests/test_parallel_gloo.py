@@ -120,10 +120,14 @@ def _kf_worker(rank, world, port, q, single):
             frames.X[k] = v
             frames.C[k] = v + 0.5
             frames.N[k] = rank + 1
+            # N_updates is its own counter (frame.py update_pointmap: equal to N only in
+            # the weighted_pointmap mode) — rank- and keyframe-tagged so a copy of N shows
+            frames.N_updates[k] = 10 * (rank + 1) + k
             frames.T_WC[k] = v + 0.25
         P.all_gather_keyframes(frames, range(6), owner)
         q.put((rank, frames.X[:6].numpy(), frames.C[:6].numpy(), frames.N[:6].numpy(),
-               frames.T_WC[:6].numpy(), list(frames._h_N[:6]), owner))
+               frames.T_WC[:6].numpy(), list(frames._h_N[:6]), owner,
+               frames.N_updates[:6].numpy(), list(frames._h_Nu[:6])))
     finally:
         dist.destroy_process_group()
 
@@ -144,11 +148,13 @@ def test_keyframe_pointmaps_all_gathered(world, single):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, X, C, N, T, hN, owner in res:
+    for rank, X, C, N, T, hN, owner, Nu, hNu in res:
         for k in range(6):
             v = 100.0 * owner[k] + k
             assert (X[k] == v).all() and (C[k] == v + 0.5).all(), (rank, k)
             assert (T[k] == v + 0.25).all() and N[k] == owner[k] + 1 and hN[k] == owner[k] + 1
+            nu = 10 * (owner[k] + 1) + k
+            assert Nu[k] == nu and hNu[k] == nu, (rank, k, Nu[k], hNu[k])
 
 
 def test_pack_roundtrip():
