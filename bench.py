@@ -72,6 +72,10 @@ def parse():
                     help="encode each frame inside its own step (no next-frame encoder overlap)")
     ap.add_argument("--streams", action="store_true",
                     help="overlap independent chains on side streams (measured slower)")
+    ap.add_argument("--timeline-out", default=None,
+                    help="write one replayed step's per-launch GEMM / attention timeline (JSON)")
+    ap.add_argument("--no-timeline", action="store_true",
+                    help="skip the in-step launch timeline (roofline from the isolated replay)")
     return ap.parse_args()
 
 
@@ -188,6 +192,123 @@ def time_replays(g, dev, n):
     return e0.elapsed_time(e1) / n
 
 
+def _union_ticks(iv):
+    """Total length of the union of [s, e) intervals."""
+    tot, cur_s, cur_e = 0, None, None
+    for s, e in sorted(iv):
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        tot += cur_e - cur_s
+    return tot
+
+
+def step_timeline(loop, dev, replays=24, out_path=None):
+    """The captured C3 step timed launch by launch AS IT RUNS (no tracer): the two parity
+    graphs are captured again with the library's step timeline armed (m3s_timeline_set), so
+    every GEMM / attention launch in them carries a slot that its blocks stamp with
+    s_memrealtime (earliest block start, latest wave end; 10 ns ticks), then replayed
+    frame after frame from the INIT keyframe with HIP events around each replay.  Per step:
+    the launches' own durations, the union of the GEMM (attention) intervals — chip time
+    during which at least one GEMM runs, concurrent chains counted once — and the
+    algorithmic FLOPs of the step's own launch set.  The roofline's `achieved` is
+    GEMM FLOPs per step ÷ the GEMM union time per step."""
+    import numpy as np
+    from monst3r_slam_amd import _lib
+    lib, P = _lib.load(), _lib.ptr
+    cap = 8192
+    buf = torch.empty((cap, 2), dtype=torch.int64, device=dev)
+
+    def cap_tl(k):
+        loop.step(k)                      # warm / allocate outside the timeline
+        torch.cuda.synchronize(dev)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        g = torch.cuda.CUDAGraph()
+        n0 = int(lib.m3s_timeline_count())
+        with torch.cuda.graph(g, stream=s):
+            loop.step(k)
+        torch.cuda.synchronize(dev)
+        return g, n0, int(lib.m3s_timeline_count())
+
+    _lib.check(lib.m3s_timeline_set(P(buf), cap), "timeline_set")
+    try:
+        graphs = [cap_tl(0), cap_tl(1)]
+        n = int(lib.m3s_timeline_count())
+        kinds = np.zeros(cap, np.int32)
+        flops = np.zeros(cap, np.float64)
+        dims = np.zeros((cap, 4), np.int64)
+        _lib.check(lib.m3s_timeline_meta(kinds.ctypes.data, flops.ctypes.data, dims.ctypes.data,
+                                         cap), "timeline_meta")
+    finally:
+        lib.m3s_timeline_set(None, 0)
+    if n >= cap:
+        raise RuntimeError("step timeline: slot capacity exceeded")
+    loop.reset(parity=0)
+    torch.cuda.synchronize(dev)
+    rows = []
+    keep = None
+    for i in range(replays):
+        g, a, b = graphs[i % 2]
+        buf[:, 0] = -1                    # UINT64_MAX: atomic-min target
+        buf[:, 1] = 0
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st = torch.cuda.current_stream(dev)
+        e0.record(st)
+        g.replay()
+        e1.record(st)
+        e1.synchronize()
+        step_ms = e0.elapsed_time(e1)
+        t = buf[a:b].cpu().numpy()
+        ok = (t[:, 1] > 0) & (t[:, 0] > 0)
+        if not ok.all():
+            raise RuntimeError(f"step timeline: {int((~ok).sum())} launches left no stamp")
+        k, fl = kinds[a:b], flops[a:b]
+        row = {"step_ms": step_ms, "span_ms": (t[:, 1].max() - t[:, 0].min()) * 1e-5}
+        for name, code in (("gemm", 1), ("attn", 2)):
+            sel = k == code
+            iv = [(int(s), int(e)) for s, e in t[sel]]
+            row[name] = {"launches": int(sel.sum()), "gflop": float(fl[sel].sum()) / 1e9,
+                         "sum_ms": float((t[sel, 1] - t[sel, 0]).sum()) * 1e-5,
+                         "union_ms": _union_ticks(iv) * 1e-5}
+        row["busy_union_ms"] = _union_ticks([(int(s), int(e)) for s, e in t]) * 1e-5
+        rows.append(row)
+        if i == replays - 2:
+            keep = (t.copy(), k.copy(), fl.copy(), dims[a:b].copy(), step_ms)
+    warm = rows[2:]                       # first replays: cold caches after reset
+
+    def med(f):
+        return float(np.median([f(r) for r in warm]))
+
+    res = {"replays": len(warm), "step_ms": med(lambda r: r["step_ms"]),
+           "span_ms": med(lambda r: r["span_ms"]),
+           "gemm_or_attn_union_ms": med(lambda r: r["busy_union_ms"])}
+    for name in ("gemm", "attn"):
+        gf = med(lambda r: r[name]["gflop"])
+        un = med(lambda r: r[name]["union_ms"])
+        sm = med(lambda r: r[name]["sum_ms"])
+        nl = med(lambda r: r[name]["launches"])
+        res[name] = {"launches": nl, "gflop": gf, "union_ms": un, "sum_of_launch_ms": sm,
+                     "avg_launch_us": sm / nl * 1e3 if nl else None,
+                     "tflops_union": gf / un if un else None,
+                     "tflops_per_launch_avg": gf / sm if sm else None}
+    if out_path and keep is not None:
+        t, k, fl, dm, sms = keep
+        t0 = int(t[:, 0].min())
+        js = {"step_ms": sms, "tick_ns": 10, "launches": [
+            {"kind": {1: "gemm", 2: "attn"}[int(kk)], "dims": [int(x) for x in d],
+             "gflop": float(f) / 1e9, "start_us": (int(s) - t0) * 1e-2,
+             "end_us": (int(e) - t0) * 1e-2} for (s, e), kk, f, d in zip(t, k, fl, dm)]}
+        with open(out_path, "w") as fh:
+            json.dump(js, fh)
+    del graphs
+    return res
+
+
 def gemm_replay(model, run, dev, reps=20):
     """Average duration of the GEMM launches of one run(): the launches are recorded
     (descriptors, same buffers, same order) during an eager run, captured back-to-back in
@@ -223,6 +344,57 @@ def gemm_roofline(model, img, feat_k, dev):
     r = gemm_replay(model, lambda: model.pair(img, feat_j=feat_k), dev)["all"]
     model.serial, model.dec_split = serial, split
     return r
+
+
+def step_pmc():
+    """MFMA-busy cycles of the captured C3 step from the committed rocprofv3 PMC pass
+    (tools/step_prof.py under rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU
+    GRBM_GUI_ACTIVE, summarised by tools/step_pmc_report.py; counters cannot be read from
+    inside the timed run).  None if absent."""
+    path = os.path.join(ROOT, "profiles", "r03_step_pmc.json")
+    if not os.path.exists(path):
+        return None
+    d = dict(json.load(open(path)))
+    d["source"] = "profiles/r03_step_pmc.json"
+    return d
+
+
+def roofline_entry(tl, roof, pmc, mfma, step_ms):
+    """The line's roofline for the dominant kernel (the bf16 MFMA GEMM) on the timed step's
+    own launch set: achieved = the step's GEMM FLOPs ÷ the GEMM-active time of the step
+    (union of the launches' in-kernel intervals, step_timeline), peak = dense bf16."""
+    iso = {"launches": roof["launches"], "gemm_ms": roof["gemm_ms"],
+           "gflop": roof["gemm_flops"] / 1e9, "tflops": roof["tflops"],
+           "frac": roof["tflops"] / BF16_DENSE_TFLOPS,
+           "timing": "the serial pair's GEMM launches (batch-4 decoder, per-shape table) "
+                     "replayed back-to-back alone in one HIP graph (bench.gemm_replay)"}
+    e = {"bound": "mfma", "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+         "kernel": "gemm_kernel (bf16 MFMA GEMM / implicit conv)",
+         "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+         "traffic_unit": "HBM bytes per GEMM launch (PMC FETCH_SIZE x2 + WRITE_SIZE, "
+                         + (pmc or {}).get("source", "") + ")",
+         "traffic_per_pair_bytes": pmc["hbm_bytes_per_pair"] if pmc else None,
+         "l2_hit_rate": pmc["l2_hit_rate"] if pmc else None,
+         "isolated_replay": iso}
+    if tl is None:
+        e.update(achieved=iso["tflops"], frac=iso["frac"], timing=iso["timing"])
+        return e
+    g = tl["gemm"]
+    e.update(achieved=g["tflops_union"], frac=g["tflops_union"] / BF16_DENSE_TFLOPS,
+             timing="in-step: the timed C3 graphs re-captured with the step timeline armed "
+                    "(every GEMM / attention launch stamps s_memrealtime at its first block's "
+                    "start and last wave's end), replayed frame by frame; achieved = GEMM "
+                    "FLOPs of the step's own launches / union of their intervals "
+                    "(bench.step_timeline)",
+             gemm_launches_per_step=g["launches"], gemm_gflop_per_step=g["gflop"],
+             gemm_union_ms_per_step=g["union_ms"], gemm_sum_of_launch_ms=g["sum_of_launch_ms"],
+             avg_launch_us=g["avg_launch_us"], tflops_per_launch_avg=g["tflops_per_launch_avg"],
+             attention=tl["attn"], timeline_step_ms=tl["step_ms"],
+             timeline_vs_timed_step=tl["step_ms"] / step_ms,
+             gemm_or_attn_union_ms=tl["gemm_or_attn_union_ms"])
+    if mfma:
+        e["mfma_busy"] = mfma
+    return e
 
 
 class _Bound:
@@ -620,6 +792,8 @@ def main():
             el200 = run_sequence(loop, graphs, SEQ_FRAMES, dev, 1)
             full = dict(sequence_report(loop, seq, SEQ_FRAMES), frames_per_s=SEQ_FRAMES / el200,
                         ms_per_frame=el200 / SEQ_FRAMES * 1e3)
+        tl = None if (args.eager or args.no_timeline) else step_timeline(
+            loop, dev, out_path=args.timeline_out)
         g_pair = None if args.eager else capture(
             lambda: model.pair(loop.img_cur, feat_j=tr.kf.feat), dev)
         pair_ms = time_replays(g_pair, dev, 20) if g_pair else None
@@ -629,6 +803,7 @@ def main():
         kroof = kernel_rooflines(tr, res["pair"], dev)
         roof = gemm_roofline(model, loop.img_cur, tr.kf.feat, dev)
         pmc = pmc_traffic()
+        mfma = step_pmc()
         ms = elapsed / args.steps * 1e3
         line = {
             "metric": METRIC,
@@ -657,21 +832,7 @@ def main():
                        "parallelism": f"replicas{world}"},
             "sequence": seq_rep,
             "pair_inference_ms": pair_ms,
-            "roofline": {"bound": "mfma", "achieved": roof["tflops"], "peak": BF16_DENSE_TFLOPS,
-                         "unit": "TFLOP/s", "frac": roof["tflops"] / BF16_DENSE_TFLOPS,
-                         "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
-                         "traffic_unit": "HBM bytes per GEMM launch (PMC FETCH_SIZE x2 + "
-                                         "WRITE_SIZE, " + (pmc or {}).get("source", "") + ")",
-                         "traffic_per_pair_bytes": pmc["hbm_bytes_per_pair"] if pmc else None,
-                         "l2_hit_rate": pmc["l2_hit_rate"] if pmc else None,
-                         "kernel": "gemm_kernel (bf16 MFMA GEMM / implicit conv)",
-                         "timing": "the serial pair's GEMM launches (batch-4 decoder, "
-                                   "per-shape table) replayed back-to-back in one HIP "
-                                   "graph, HIP events on its stream (bench.gemm_replay)",
-                         "gemm_launches_per_pair": roof["launches"],
-                         "gemm_ms_per_pair": roof["gemm_ms"],
-                         "gemm_gflop_per_pair": roof["gemm_flops"] / 1e9,
-                         "avg_launch_us": roof["avg_launch_us"]},
+            "roofline": roofline_entry(tl, roof, pmc, mfma, ms),
             "kernel_rooflines": kroof,
         }
         if full is not None:

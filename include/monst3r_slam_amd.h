@@ -42,6 +42,19 @@ const char* m3s_status_string(int status);
 int m3s_version(void);                 /* (major<<16)|(minor<<8)|patch */
 int m3s_device_count(void);
 
+/* Step timeline (diagnostic; bench.py step_timeline).  m3s_timeline_set(d_buf, capacity)
+ * arms it: every GEMM (m3s_vit_gemm) and attention (m3s_vit_attention) launch issued
+ * afterwards — eager or captured into a graph — takes the next of `capacity` slots of
+ * d_buf (u64 [capacity][2]: earliest block start, latest wave end, s_memrealtime ticks of
+ * 100 MHz; the caller fills each slot with {UINT64_MAX, 0} before a run).  A null d_buf
+ * disarms it (later launches carry no slot).  m3s_timeline_count() = slots taken since the
+ * last set; m3s_timeline_meta() copies their kinds (1 GEMM, 2 attention), algorithmic
+ * FLOPs (2·M·N·K·batch; 4·Sq·Sk·64·heads·batch) and dims ({M, N, K, batch};
+ * {Sq, Sk, heads, batch}) to host arrays of `capacity` entries (dims: [capacity][4]). */
+int m3s_timeline_set(void* d_buf, int capacity);
+int m3s_timeline_count(void);
+int m3s_timeline_meta(int* kinds, double* flops, int64_t* dims, int capacity);
+
 /* ------------------------------------------------------------------------- *
  * Projective matching.
  * ------------------------------------------------------------------------- */
@@ -127,6 +140,45 @@ int m3s_gauss_newton_points(float* d_Twc, const float* d_Xs, const float* d_Cs,
                             float sigma_point, float C_thresh, float Q_thresh,
                             int max_iter, float delta_thresh, float* d_dx_out,
                             void* d_workspace, int* h_status_out, void* stream);
+
+/* Edge-sharded backend GN (the iteration of gn_kernels.cu:1140-1228 split at
+ * its reduction).  Each rank holds the data rows of ITS two-way edges only (idx / valid /
+ * Q [E_local,...], global edge ids d_edge_ids i32 [E_local]) plus the replicated poses
+ * and pointmaps; per iteration:
+ *   m3s_gn_{rays,calib}_edge_pass  → d_G f64 [E_local][35]: the per-edge sums
+ *                                    (28 of Σ w J'J'ᵀ + 7 of Σ w e J')
+ *   (caller) all-gather the rows into d_G_all [E_total][35] in global edge order
+ *   m3s_gn_solve_step              → assemble + fp64 Cholesky + retract + convergence flag
+ * m3s_gn_sharded_begin once before (ranks of all E_total edges, flags, dx = 0);
+ * m3s_gn_sharded_status after (synchronises; status as h_status_out of the calls above,
+ * iterations taken).  The split count S follows E_total, so every edge's sums — and the
+ * poses — are bit-identical to the unsharded call's.  After convergence the kernels exit
+ * at once (device flag), so a fixed max_iter loop needs no host sync. */
+size_t m3s_gn_sharded_workspace_bytes(int64_t num_poses, int64_t num_edges_total,
+                                      int64_t num_edges_local, int64_t num_points);
+int m3s_gn_sharded_begin(const int64_t* d_ii, const int64_t* d_jj, int64_t num_poses,
+                         int64_t num_points, int64_t num_edges_total, int64_t num_edges_local,
+                         float* d_dx_out, void* d_workspace, void* stream);
+int m3s_gn_rays_edge_pass(const float* d_Twc, const float* d_Xs, const float* d_Cs,
+                          const int32_t* d_edge_ids, const int64_t* d_idx_local,
+                          const uint8_t* d_valid_local, const float* d_Q_local,
+                          int64_t num_poses, int64_t num_points, int64_t num_edges_total,
+                          int64_t num_edges_local, float sigma_ray, float sigma_dist,
+                          float C_thresh, float Q_thresh, double* d_G_local, void* d_workspace,
+                          void* stream);
+int m3s_gn_calib_edge_pass(const float* d_Twc, const float* d_Xs, const float* d_Cs,
+                           const float* d_K, const int32_t* d_edge_ids,
+                           const int64_t* d_idx_local, const uint8_t* d_valid_local,
+                           const float* d_Q_local, int64_t num_poses, int64_t num_points,
+                           int64_t num_edges_total, int64_t num_edges_local, int height,
+                           int width, int pixel_border, float z_eps, float sigma_pixel,
+                           float sigma_depth, float C_thresh, float Q_thresh, double* d_G_local,
+                           void* d_workspace, void* stream);
+int m3s_gn_solve_step(float* d_Twc, const double* d_G_all, int64_t num_poses,
+                      int64_t num_points, int64_t num_edges_total, int64_t num_edges_local,
+                      float delta_thresh, float* d_dx_out, void* d_workspace, void* stream);
+int m3s_gn_sharded_status(const void* d_workspace, int64_t num_poses, int* h_status_out,
+                          int* h_iters_out, void* stream);
 
 /* ------------------------------------------------------------------------- *
  * Frontend tracker: 7-dof Sim3 Gauss-Newton of FrameTracker2.opt_pose_ray_dist_sim3

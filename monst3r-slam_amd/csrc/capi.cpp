@@ -1,4 +1,5 @@
 // Library-level entry points of the C ABI (include/monst3r_slam_amd.h).
+#include <vector>
 #include <hip/hip_runtime.h>
 #include "../../include/monst3r_slam_amd.h"
 
@@ -15,6 +16,49 @@ extern "C" const char* m3s_status_string(int status) {
 }
 
 extern "C" int m3s_version(void) { return (0 << 16) | (1 << 8) | 0; }
+
+// ---- step timeline (common.h) ----
+namespace {
+unsigned long long* g_tl = nullptr;
+int g_tl_cap = 0, g_tl_n = 0;
+std::vector<int> g_tl_kind;
+std::vector<double> g_tl_flops;
+std::vector<int64_t> g_tl_dims;
+}  // namespace
+
+unsigned long long* m3s_timeline_take(int kind, double flops, int64_t d0, int64_t d1, int64_t d2,
+                                      int64_t d3) {
+  if (!g_tl || g_tl_n >= g_tl_cap) return nullptr;
+  g_tl_kind.push_back(kind);
+  g_tl_flops.push_back(flops);
+  g_tl_dims.insert(g_tl_dims.end(), {d0, d1, d2, d3});
+  return g_tl + 2 * (int64_t)g_tl_n++;
+}
+
+extern "C" int m3s_timeline_set(void* d_buf, int capacity) {
+  if (d_buf && capacity <= 0) return M3S_ERR_INVALID_ARG;
+  g_tl = reinterpret_cast<unsigned long long*>(d_buf);
+  g_tl_cap = d_buf ? capacity : 0;
+  if (d_buf) {
+    g_tl_n = 0;
+    g_tl_kind.clear();
+    g_tl_flops.clear();
+    g_tl_dims.clear();
+  }
+  return M3S_OK;
+}
+
+extern "C" int m3s_timeline_count(void) { return g_tl_n; }
+
+extern "C" int m3s_timeline_meta(int* kinds, double* flops, int64_t* dims, int capacity) {
+  if (!kinds || !flops || !dims || capacity < 0) return M3S_ERR_INVALID_ARG;
+  for (int i = 0; i < g_tl_n && i < capacity; i++) {
+    kinds[i] = g_tl_kind[i];
+    flops[i] = g_tl_flops[i];
+    for (int j = 0; j < 4; j++) dims[4 * i + j] = g_tl_dims[4 * i + j];
+  }
+  return M3S_OK;
+}
 
 extern "C" int m3s_device_count(void) {
   int n = 0;

@@ -77,11 +77,12 @@ __global__ __launch_bounds__(kEdgeThreads) void gn_edge_kernel(
     const int* __restrict__ rank_jj, const int64_t* __restrict__ idx_ii2jj,
     const uint8_t* __restrict__ valid_match, const float* __restrict__ Q,
     float* __restrict__ partial, const int* __restrict__ flags, int64_t num_points, int S,
-    GnParams prm) {
+    GnParams prm, const int* __restrict__ edge_ids) {
   if (flags[0]) return;  // converged in an earlier iteration
-  const int e = blockIdx.x;
+  const int e = blockIdx.x;     // row of this rank's edge data (idx / valid / Q / partial)
   const int s = blockIdx.y;
-  const int ix = rank_ii[e], jx = rank_jj[e];
+  const int ge = edge_ids ? edge_ids[e] : e;   // the edge's id in the whole graph
+  const int ix = rank_ii[ge], jx = rank_jj[ge];
   const float* Ti = Twc + 8 * ix;
   const float* Tj = Twc + 8 * jx;
   float tij[3], qij[4], sij;
@@ -304,6 +305,21 @@ __global__ __launch_bounds__(kSolveThreads) void gn_rank_kernel(const int64_t* _
   if (threadIdx.x == 0) flags[2] = s_unique;
 }
 
+// The S partials of each of this rank's E edges → G [E][kAcc] f64, in the solve kernel's
+// fixed order (bit-identical to its step 1).
+__global__ __launch_bounds__(256) void gn_reduce_kernel(const float* __restrict__ partial,
+                                                        double* __restrict__ G,
+                                                        const int* __restrict__ flags, int E,
+                                                        int S) {
+  if (flags[0]) return;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= E * kAcc) return;
+  const int e = idx / kAcc, l = idx % kAcc;
+  double v = 0.0;
+  for (int s = 0; s < S; s++) v += (double)partial[((int64_t)e * S + s) * kAcc + l];
+  G[idx] = v;
+}
+
 __device__ __forceinline__ int tri_idx(int n, int m) {  // n >= m
   return n * (n + 1) / 2 + m;
 }
@@ -312,19 +328,23 @@ __device__ __forceinline__ int tri_idx(int n, int m) {  // n >= m
 __global__ __launch_bounds__(kSolveThreads) void gn_solve_kernel(
     float* __restrict__ Twc, const float* __restrict__ partial, const int* __restrict__ rank_ii,
     const int* __restrict__ rank_jj, double* __restrict__ Ag, double* __restrict__ bg,
-    double* __restrict__ Gs, float* __restrict__ dx_out, int* __restrict__ flags, int E, int S,
-    int P, float delta_thresh) {
+    double* __restrict__ Gs_ws, float* __restrict__ dx_out, int* __restrict__ flags, int E, int S,
+    int P, float delta_thresh, const double* __restrict__ G_in) {
   if (flags[0]) return;
   const int tid = threadIdx.x;
   const int n = 7 * (P - 1);
   const int nt = blockDim.x;
 
-  // 1) reduce the S partials of every edge (fixed order, f64)
-  for (int idx = tid; idx < E * kAcc; idx += nt) {
-    const int e = idx / kAcc, l = idx % kAcc;
-    double v = 0.0;
-    for (int s = 0; s < S; s++) v += (double)partial[((int64_t)e * S + s) * kAcc + l];
-    Gs[idx] = v;
+  // 1) reduce the S partials of every edge (fixed order, f64) — or take them reduced
+  //    (edge-sharded GN: gn_reduce_kernel on each rank, all-gathered in edge order)
+  const double* Gs = G_in ? G_in : Gs_ws;
+  if (!G_in) {
+    for (int idx = tid; idx < E * kAcc; idx += nt) {
+      const int e = idx / kAcc, l = idx % kAcc;
+      double v = 0.0;
+      for (int s = 0; s < S; s++) v += (double)partial[((int64_t)e * S + s) * kAcc + l];
+      Gs_ws[idx] = v;
+    }
   }
   for (int idx = tid; idx < n * n; idx += nt) Ag[idx] = 0.0;
   for (int idx = tid; idx < n; idx += nt) bg[idx] = 0.0;
@@ -541,10 +561,11 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
     for (int it = 0; it < max_iter; it++) {
       hipLaunchKernelGGL(gn_edge_kernel<MODE>, dim3((unsigned)E, (unsigned)S),
                          dim3(kEdgeThreads), 0, st, d_Twc, d_Xs, d_Cs, d_K, rii, rjj, d_idx,
-                         d_valid, d_Q, partial, flags, N, S, prm);
+                         d_valid, d_Q, partial, flags, N, S, prm, nullptr);
       M3S_LAUNCH_CHECK();
       hipLaunchKernelGGL(gn_solve_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_Twc, partial,
-                         rii, rjj, A, b, G, d_dx, flags, (int)E, S, (int)P, delta_thresh);
+                         rii, rjj, A, b, G, d_dx, flags, (int)E, S, (int)P, delta_thresh,
+                         nullptr);
       M3S_LAUNCH_CHECK();
     }
   }
@@ -558,7 +579,165 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
   return M3S_OK;
 }
 
+// ---- edge-sharded GN ----
+// Workspace: flags, ranks of ALL E_total two-way edges, partials of this rank's E_local
+// edges, the dense system.  S comes from E_total, so every edge's partials — hence its G
+// row — are those of the unsharded m3s_gauss_newton_* call, bit for bit.
+struct ShardLayout {
+  size_t flags, rank_ii, rank_jj, partial, A, b, total;
+  int S;
+};
+
+ShardLayout make_shard_layout(int64_t P, int64_t E_total, int64_t E_local, int64_t N) {
+  ShardLayout L;
+  L.S = choose_splits(E_total, N);
+  const int64_t n = 7 * (P > 1 ? P - 1 : 0);
+  size_t off = 0;
+  L.flags = off;
+  off = align_up(off + 64, 256);
+  L.rank_ii = off;
+  off = align_up(off + 4 * E_total, 256);
+  L.rank_jj = off;
+  off = align_up(off + 4 * E_total, 256);
+  L.partial = off;
+  off = align_up(off + 4 * (E_local > 0 ? E_local : 1) * L.S * kAcc, 256);
+  L.A = off;
+  off = align_up(off + 8 * n * n, 256);
+  L.b = off;
+  off = align_up(off + 8 * (n > 0 ? n : 1), 256);
+  L.total = off;
+  return L;
+}
+
+bool shard_sizes_ok(int64_t P, int64_t N, int64_t E_total, int64_t E_local) {
+  return P >= 1 && N >= 1 && E_total >= 1 && E_local >= 0 && E_local <= E_total &&
+         E_total <= 65535 && 7 * P <= 46000;
+}
+
+template <int MODE>
+int shard_edge_pass(const float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
+                    const int32_t* d_edge_ids, const int64_t* d_idx, const uint8_t* d_valid,
+                    const float* d_Q, int64_t P, int64_t N, int64_t E_total, int64_t E_local,
+                    GnParams prm, double* d_G, void* d_ws, void* stream) {
+  if (!shard_sizes_ok(P, N, E_total, E_local) || !d_ws) return M3S_ERR_INVALID_ARG;
+  if (E_local == 0 || P < 2) return M3S_OK;
+  if (!d_Twc || !d_Xs || !d_Cs || !d_edge_ids || !d_idx || !d_valid || !d_Q || !d_G)
+    return M3S_ERR_INVALID_ARG;
+  if (MODE == MODE_CALIB && !d_K) return M3S_ERR_INVALID_ARG;
+  const ShardLayout L = make_shard_layout(P, E_total, E_local, N);
+  char* ws = reinterpret_cast<char*>(d_ws);
+  const int* flags = reinterpret_cast<const int*>(ws + L.flags);
+  float* partial = reinterpret_cast<float*>(ws + L.partial);
+  hipStream_t st = m3s_stream(stream);
+  hipLaunchKernelGGL(gn_edge_kernel<MODE>, dim3((unsigned)E_local, (unsigned)L.S),
+                     dim3(kEdgeThreads), 0, st, d_Twc, d_Xs, d_Cs, d_K,
+                     reinterpret_cast<const int*>(ws + L.rank_ii),
+                     reinterpret_cast<const int*>(ws + L.rank_jj), d_idx, d_valid, d_Q, partial,
+                     flags, N, L.S, prm, reinterpret_cast<const int*>(d_edge_ids));
+  M3S_LAUNCH_CHECK();
+  hipLaunchKernelGGL(gn_reduce_kernel, dim3(m3s_div_up(E_local * kAcc, 256)), dim3(256), 0, st,
+                     partial, d_G, flags, (int)E_local, L.S);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
 }  // namespace
+
+extern "C" size_t m3s_gn_sharded_workspace_bytes(int64_t num_poses, int64_t num_edges_total,
+                                                 int64_t num_edges_local, int64_t num_points) {
+  if (!shard_sizes_ok(num_poses, num_points, num_edges_total, num_edges_local)) return 256;
+  return make_shard_layout(num_poses, num_edges_total, num_edges_local, num_points).total;
+}
+
+extern "C" int m3s_gn_sharded_begin(const int64_t* d_ii, const int64_t* d_jj, int64_t num_poses,
+                                    int64_t num_points, int64_t num_edges_total,
+                                    int64_t num_edges_local, float* d_dx, void* d_ws,
+                                    void* stream) {
+  const int64_t P = num_poses, E = num_edges_total;
+  if (!shard_sizes_ok(P, num_points, E, num_edges_local) || !d_ii || !d_jj || !d_ws ||
+      (P > 1 && !d_dx))
+    return M3S_ERR_INVALID_ARG;
+  const ShardLayout L = make_shard_layout(P, E, num_edges_local, num_points);
+  char* ws = reinterpret_cast<char*>(d_ws);
+  hipStream_t st = m3s_stream(stream);
+  M3S_HIP_CHECK(hipMemsetAsync(ws + L.flags, 0, 64, st));
+  if (P > 1) M3S_HIP_CHECK(hipMemsetAsync(d_dx, 0, sizeof(float) * 7 * (P - 1), st));
+  hipLaunchKernelGGL(gn_rank_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_ii, d_jj, (int)E,
+                     reinterpret_cast<int*>(ws + L.rank_ii), reinterpret_cast<int*>(ws + L.rank_jj),
+                     reinterpret_cast<int*>(ws + L.flags));
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_gn_rays_edge_pass(const float* d_Twc, const float* d_Xs, const float* d_Cs,
+                                     const int32_t* d_edge_ids, const int64_t* d_idx,
+                                     const uint8_t* d_valid, const float* d_Q, int64_t P, int64_t N,
+                                     int64_t E_total, int64_t E_local, float sigma_ray,
+                                     float sigma_dist, float C_thresh, float Q_thresh, double* d_G,
+                                     void* d_ws, void* stream) {
+  GnParams prm{};
+  prm.s0_inv = (float)(1.0 / (double)sigma_ray);
+  prm.s1_inv = (float)(1.0 / (double)sigma_dist);
+  prm.C_thresh = C_thresh;
+  prm.Q_thresh = Q_thresh;
+  return shard_edge_pass<MODE_RAYS>(d_Twc, d_Xs, d_Cs, nullptr, d_edge_ids, d_idx, d_valid, d_Q,
+                                    P, N, E_total, E_local, prm, d_G, d_ws, stream);
+}
+
+extern "C" int m3s_gn_calib_edge_pass(const float* d_Twc, const float* d_Xs, const float* d_Cs,
+                                      const float* d_K, const int32_t* d_edge_ids,
+                                      const int64_t* d_idx, const uint8_t* d_valid,
+                                      const float* d_Q, int64_t P, int64_t N, int64_t E_total,
+                                      int64_t E_local, int height, int width, int pixel_border,
+                                      float z_eps, float sigma_pixel, float sigma_depth,
+                                      float C_thresh, float Q_thresh, double* d_G, void* d_ws,
+                                      void* stream) {
+  GnParams prm{};
+  prm.s0_inv = (float)(1.0 / (double)sigma_pixel);
+  prm.s1_inv = (float)(1.0 / (double)sigma_depth);
+  prm.C_thresh = C_thresh;
+  prm.Q_thresh = Q_thresh;
+  prm.height = height;
+  prm.width = width;
+  prm.pixel_border = pixel_border;
+  prm.z_eps = z_eps;
+  if (width < 1 || height < 1) return M3S_ERR_INVALID_ARG;
+  return shard_edge_pass<MODE_CALIB>(d_Twc, d_Xs, d_Cs, d_K, d_edge_ids, d_idx, d_valid, d_Q, P,
+                                     N, E_total, E_local, prm, d_G, d_ws, stream);
+}
+
+extern "C" int m3s_gn_solve_step(float* d_Twc, const double* d_G, int64_t num_poses,
+                                 int64_t num_points, int64_t num_edges_total,
+                                 int64_t num_edges_local, float delta_thresh, float* d_dx,
+                                 void* d_ws, void* stream) {
+  const int64_t P = num_poses, E = num_edges_total;
+  if (!shard_sizes_ok(P, num_points, E, num_edges_local) || !d_ws) return M3S_ERR_INVALID_ARG;
+  if (P < 2) return M3S_OK;
+  if (!d_Twc || !d_G || !d_dx) return M3S_ERR_INVALID_ARG;
+  const ShardLayout L = make_shard_layout(P, E, num_edges_local, num_points);
+  char* ws = reinterpret_cast<char*>(d_ws);
+  hipLaunchKernelGGL(gn_solve_kernel, dim3(1), dim3(kSolveThreads), 0, m3s_stream(stream), d_Twc,
+                     nullptr, reinterpret_cast<const int*>(ws + L.rank_ii),
+                     reinterpret_cast<const int*>(ws + L.rank_jj),
+                     reinterpret_cast<double*>(ws + L.A), reinterpret_cast<double*>(ws + L.b),
+                     nullptr, d_dx, reinterpret_cast<int*>(ws + L.flags), (int)E, L.S, (int)P,
+                     delta_thresh, d_G);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+extern "C" int m3s_gn_sharded_status(const void* d_ws, int64_t num_poses, int* h_status,
+                                     int* h_iters, void* stream) {
+  if (!d_ws || !h_status) return M3S_ERR_INVALID_ARG;
+  int hflags[4] = {0, 0, 0, 0};
+  hipStream_t st = m3s_stream(stream);
+  M3S_HIP_CHECK(hipMemcpyAsync(hflags, d_ws, sizeof(hflags), hipMemcpyDeviceToHost, st));
+  M3S_HIP_CHECK(hipStreamSynchronize(st));
+  if (hflags[2] != num_poses) *h_status = M3S_ERR_INVALID_ARG;
+  else *h_status = hflags[1] ? M3S_ERR_NOT_PD : M3S_OK;
+  if (h_iters) *h_iters = hflags[3];
+  return M3S_OK;
+}
 
 extern "C" size_t m3s_gn_workspace_bytes(int64_t num_poses, int64_t num_edges) {
   if (num_poses < 1 || num_edges < 1) return 256;

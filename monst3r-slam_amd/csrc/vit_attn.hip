@@ -136,7 +136,9 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, void* __restrict__ o,
     int64_t ldo, int64_t so_b, int o_fp8, int Sq, int Sk, int heads, float c_log2, int splits,
-    int tiles_per_split, float* __restrict__ part, int kv_xor) {
+    int tiles_per_split, float* __restrict__ part, int kv_xor, unsigned long long* tl) {
+  m3s_tl_begin(tl);
+  const M3sTlEnd tl_end{tl};
   constexpr int GT = AW * 64;                        // threads of one key-split group
   constexpr int ACH = TILE_BYTES / 16 / GT;          // DMA chunks per thread per operand
   constexpr int NST = KS == 1 ? ASTAGES : 2;         // ring depth per key split
@@ -534,6 +536,8 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   if ((int64_t)m3s_div_up(sq, 2 * QT) * hb * splits >= (1ll << 31)) return M3S_ERR_TOO_LARGE;
   float* part = splits > 1 ? reinterpret_cast<float*>(d_workspace) : nullptr;
   hipStream_t s = m3s_stream(stream);
+  unsigned long long* tl =
+      m3s_timeline_take(M3S_TL_ATTN, 4.0 * sq * sk * HD * heads * batch, sq, sk, heads, batch);
 #define M3S_ATTN_LAUNCH2(AWV, KSV, TL)                                                       \
   hipLaunchKernelGGL((attn_kernel<AWV, KSV, TL>),                                           \
                      dim3((unsigned)(m3s_div_up(sq, AWV * QT) * heads * batch * splits)),    \
@@ -541,7 +545,7 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
                      reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,                   \
                      reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
                      ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,          \
-                     (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor)
+                     (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl)
 #define M3S_ATTN_LAUNCH(AWV, KSV)                                                            \
   do {                                                                                       \
     if (sk % AKT) M3S_ATTN_LAUNCH2(AWV, KSV, true);                                          \

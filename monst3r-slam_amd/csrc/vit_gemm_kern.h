@@ -82,6 +82,7 @@ struct Args {
   int a_xor;               // LN_FOLD: A and stats of batch g ^ a_xor
   const float* ln_c1;      // LN_FOLD: row sums of the gamma-folded weight (stride sBias)
   float ln_eps;
+  unsigned long long* tl;  // step-timeline slot or null (common.h)
 };
 
 // Row statistics of a LN_FOLD consumer from the producer's per-128-column (mean_t, M2_t)
@@ -394,6 +395,8 @@ template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE,
 __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
   constexpr int NT = WM * WN * 64;            // 4 waves (8: two per SIMD, see T128W8)
   M3S_T(t_start);
+  m3s_tl_begin(a.tl);
+  const M3sTlEnd tl_end{a.tl};
 #ifdef M3S_GEMM_STAMPS
   const long long rt_start = (long long)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -1044,6 +1047,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
 // thread, the whole chip reducing (the fused path reduces a tile on one CU).
 template <int Unused>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
+  const M3sTlEnd tl_end{a.tl};   // the GEMM's slot: the reduce extends its end
   const int vpr = (a.N + 7) / 8;
   const int64_t vid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int g = blockIdx.y;

@@ -26,6 +26,9 @@ SIGNATURES = {
     "m3s_status_string": (ctypes.c_char_p, [_I]),
     "m3s_version": (_I, []),
     "m3s_device_count": (_I, []),
+    "m3s_timeline_set": (_I, [_P, _I]),
+    "m3s_timeline_count": (_I, []),
+    "m3s_timeline_meta": (_I, [_P, _P, _P, _I]),
     "m3s_iter_proj": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _F, _F, _P]),
     "m3s_refine_matches": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
     "m3s_match_prep": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P]),
@@ -38,6 +41,14 @@ SIGNATURES = {
                                     _I, _F, _F, _F, _F, _F, _I, _F, _P, _P, _P, _P]),
     "m3s_gauss_newton_points": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _F,
                                      _F, _I, _F, _P, _P, _P, _P]),
+    "m3s_gn_sharded_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
+    "m3s_gn_sharded_begin": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _P]),
+    "m3s_gn_rays_edge_pass": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _F,
+                                   _F, _F, _P, _P, _P]),
+    "m3s_gn_calib_edge_pass": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I,
+                                    _I, _I, _F, _F, _F, _F, _F, _P, _P, _P]),
+    "m3s_gn_solve_step": (_I, [_P, _P, _I64, _I64, _I64, _I64, _F, _P, _P, _P]),
+    "m3s_gn_sharded_status": (_I, [_P, _I64, _P, _P, _P]),
     "m3s_track_workspace_bytes": (_SZ, [_I64]),
     "m3s_track_rays": (_I, [_P, _P, _P, _P, _P, _P, _I64, _F, _F, _F, _I, _F, _F, _P, _P, _P, _P,
                             _P]),

@@ -184,17 +184,47 @@ def _unpack_keyframes(frames, idx, recs, n):
             frames._h_N[k], frames._h_Nu[k] = int(vn), int(vu)
 
 
+def _is_gloo(group=None):
+    return dist.get_backend(group) == "gloo"
+
+
+def _all_gather_fixed(t, group=None):
+    """all_gather of one equal-shape tensor per rank → [world, *t.shape] on t's device.
+    gloo (the CPU test backend) stages device tensors through the host."""
+    world, _ = _world(group)
+    stage = t.is_cuda and _is_gloo(group)
+    src = t.cpu() if stage else t.contiguous()
+    out = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(out, src, group=group)
+    r = torch.stack(out)
+    return r.to(t.device) if stage else r
+
+
 class ShardedFactorGraph(FactorGraph):
-    """FactorGraph whose per-edge inference + matching is split across the ranks."""
+    """FactorGraph whose per-edge work is split across the ranks.
+
+    Edge e of an add_factors call is matched on rank e % world, and its records (idx,
+    valid, Q of both directions: 18 B/pixel) STAY on that rank: only the two per-edge
+    match fractions (16 B) are all-gathered for the acceptance rule, which then runs
+    identically everywhere.  ii / jj / owner are global on every rank; idx_ii2jj,
+    idx_jj2ii, valid_match_*, Q_* hold this rank's accepted edges only, in global edge
+    order.  solve_GN_* shards the Gauss-Newton edge pass the same way: each rank
+    accumulates its own two-way edges' 35 per-edge sums (m3s_gn_*_edge_pass), one
+    all-gather per iteration of E x 35 f64 (35 KB at E = 128) puts them in edge order on
+    every rank, and every rank runs the same fp64 solve + retraction — the poses equal
+    the unsharded solve's bit for bit (same per-edge sums, same assembly order)."""
 
     def __init__(self, *args, group=None, **kw):
         super().__init__(*args, **kw)
         self.group = group
+        self.owner = torch.as_tensor([], dtype=torch.int32, device=self.device)
 
     def _match_local(self, ii, jj):
         return FactorGraph.match_edges(self, ii, jj)
 
     def match_edges(self, ii, jj):
+        """Every edge's records on every rank (one all-gather of the packed records) — the
+        base-class contract; add_factors below keeps records where they were computed."""
         world, rank = _world(self.group)
         if world == 1:
             return self._match_local(ii, jj)
@@ -208,3 +238,134 @@ class ShardedFactorGraph(FactorGraph):
             r = self._match_local([ii[e] for e in mine], [jj[e] for e in mine])
             loc[:len(mine)] = pack_edges(r, n)
         return unpack_edges(all_gather_rows(loc, E, self.group), n)
+
+    def add_factors(self, ii, jj, min_match_frac, is_reloc=False):
+        """global_opt2.py:35-107 with the records kept on the rank that matched them."""
+        world, rank = _world(self.group)
+        if world == 1:
+            return super().add_factors(ii, jj, min_match_frac, is_reloc)
+        ii, jj = [int(i) for i in ii], [int(j) for j in jj]
+        E = len(ii)
+        mine = list(range(rank, E, world))
+        per = math.ceil(E / world)
+        fr = torch.zeros((per, 2), dtype=torch.float64, device=self.device)
+        r = None
+        if mine:
+            r = self._match_local([ii[e] for e in mine], [jj[e] for e in mine])
+            vj = r["valid_match_j"] & (r["Qj"] > self.cfg["Q_conf"])
+            vi = r["valid_match_i"] & (r["Qi"] > self.cfg["Q_conf"])
+            fr[:len(mine), 0] = vj.sum(dim=(1, 2)).double() / (vj.shape[1] * vj.shape[2])
+            fr[:len(mine), 1] = vi.sum(dim=(1, 2)).double() / (vi.shape[1] * vi.shape[2])
+        frac = all_gather_rows(fr, E, self.group).float()   # edge order (round-robin slots)
+        ii_t = torch.as_tensor(ii, device=self.device)
+        jj_t = torch.as_tensor(jj, device=self.device)
+        invalid = torch.minimum(frac[:, 0], frac[:, 1]) < min_match_frac
+        invalid = (~(ii_t == (jj_t - 1))) & invalid
+        if is_reloc and bool(invalid.any()):
+            return False
+        ok = ~invalid
+        owner = torch.arange(E, device=self.device, dtype=torch.int32) % world
+        self.ii = torch.cat([self.ii, ii_t[ok]])
+        self.jj = torch.cat([self.jj, jj_t[ok]])
+        self.owner = torch.cat([self.owner, owner[ok]])
+        if r is not None:
+            okm = ok[torch.as_tensor(mine, device=self.device)]
+            self.idx_ii2jj = torch.cat([self.idx_ii2jj, r["idx_i2j"][okm]])
+            self.idx_jj2ii = torch.cat([self.idx_jj2ii, r["idx_j2i"][okm]])
+            self.valid_match_j = torch.cat([self.valid_match_j, r["valid_match_j"][okm]])
+            self.valid_match_i = torch.cat([self.valid_match_i, r["valid_match_i"][okm]])
+            self.Q_ii2jj = torch.cat([self.Q_ii2jj, r["Qj"][okm]])
+            self.Q_jj2ii = torch.cat([self.Q_jj2ii, r["Qi"][okm]])
+        return bool(ok.sum() > 0)
+
+    def local_edge_ids(self):
+        """Global two-way edge ids of this rank's rows (prep_two_way_edges order: the E
+        i→j edges, then the same E as j→i)."""
+        _, rank = _world(self.group)
+        E = self.ii.numel()
+        loc = torch.nonzero(self.owner == rank).flatten().to(torch.int32)
+        return torch.cat([loc, loc + E])
+
+    def solve_GN_rays(self):
+        if _world(self.group)[0] == 1:
+            return super().solve_GN_rays()
+        self._solve_sharded("rays")
+
+    def solve_GN_calib(self):
+        if _world(self.group)[0] == 1:
+            return super().solve_GN_calib()
+        self._solve_sharded("calib")
+
+    def _solve_sharded(self, mode):
+        """global_opt2.py:129-221 with the GN edge pass sharded (class doc)."""
+        import ctypes
+        from . import _lib
+        from .global_opt import constrain_points_to_ray
+        world, rank = _world(self.group)
+        c = self.cfg
+        pin = c["pin"]
+        uniq = self.get_unique_kf_idx()
+        if uniq.numel() <= pin:
+            return
+        Xs, T_WCs, Cs = self.get_poses_points(uniq)
+        if mode == "calib":
+            Xs = constrain_points_to_ray((self.frames.h, self.frames.w), Xs, self.K)
+        Xs, Cs = Xs.contiguous(), Cs.contiguous()
+        ii = torch.cat((self.ii, self.jj)).contiguous()
+        jj = torch.cat((self.jj, self.ii)).contiguous()
+        ids = self.local_edge_ids().contiguous()
+        idx = torch.cat((self.idx_ii2jj, self.idx_jj2ii)).contiguous()
+        valid = torch.cat((self.valid_match_j, self.valid_match_i)).contiguous()
+        Q = torch.cat((self.Q_ii2jj, self.Q_jj2ii)).contiguous()
+        pose = T_WCs[:, 0, :].contiguous()
+        P, N = Xs.shape[0], Xs.shape[1]
+        E2, El = ii.numel(), ids.numel()
+        lib, ptr, dev = _lib.load(), _lib.ptr, self.device
+        s = _lib.stream(dev)
+        ws = torch.empty(int(lib.m3s_gn_sharded_workspace_bytes(P, E2, El, N)), dtype=torch.uint8,
+                         device=dev)
+        dx = torch.zeros((max(P - 1, 1), 7), dtype=torch.float32, device=dev)
+        # the per-edge rows all-gather as equal-size padded slabs; where each rank's rows go
+        counts = torch.bincount(self.owner.long(), minlength=world).tolist()
+        pad = max(1, 2 * max(counts))
+        G_loc = torch.zeros((pad, 35), dtype=torch.float64, device=dev)
+        G_all = torch.zeros((E2, 35), dtype=torch.float64, device=dev)
+        E = self.ii.numel()
+        slot = []                                  # gathered row → global two-way edge id
+        for r_ in range(world):
+            loc = torch.nonzero(self.owner == r_).flatten()
+            slot.append(torch.cat([loc, loc + E, torch.full((pad - 2 * loc.numel(),), -1,
+                                                           dtype=loc.dtype, device=dev)]))
+        slot = torch.cat(slot)
+        take = slot >= 0
+        dst = slot[take]
+        _lib.check(lib.m3s_gn_sharded_begin(ptr(ii), ptr(jj), P, N, E2, El, ptr(dx), ptr(ws), s),
+                   "gn_sharded_begin")
+        for _ in range(int(c["max_iters"])):
+            if mode == "rays":
+                st = lib.m3s_gn_rays_edge_pass(
+                    ptr(pose), ptr(Xs), ptr(Cs), ptr(ids), ptr(idx), ptr(valid), ptr(Q), P, N,
+                    E2, El, float(c["sigma_ray"]), float(c["sigma_dist"]), float(c["C_conf"]),
+                    float(c["Q_conf"]), ptr(G_loc), ptr(ws), s)
+            else:
+                h, w = self.frames.h, self.frames.w
+                st = lib.m3s_gn_calib_edge_pass(
+                    ptr(pose), ptr(Xs), ptr(Cs), ptr(self.K.contiguous()), ptr(ids), ptr(idx),
+                    ptr(valid), ptr(Q), P, N, E2, El, h, w, int(c["pixel_border"]),
+                    float(c["depth_eps"]), float(c["sigma_pixel"]), float(c["sigma_depth"]),
+                    float(c["C_conf"]), float(c["Q_conf"]), ptr(G_loc), ptr(ws), s)
+            _lib.check(st, "gn_edge_pass")
+            gathered = _all_gather_fixed(G_loc, self.group).reshape(world * pad, 35)
+            G_all[dst] = gathered[take]
+            _lib.check(lib.m3s_gn_solve_step(ptr(pose), ptr(G_all), P, N, E2, El,
+                                             float(c["delta_norm"]), ptr(dx), ptr(ws), s),
+                       "gn_solve_step")
+        hs, it = ctypes.c_int(0), ctypes.c_int(0)
+        _lib.check(lib.m3s_gn_sharded_status(ptr(ws), P, ctypes.byref(hs), ctypes.byref(it), s),
+                   "gn_sharded_status")
+        if hs.value == -1:
+            raise RuntimeError("gauss_newton (sharded): the number of unique keyframes in ii/jj "
+                               "must equal Xs.size(0)")
+        self.gn_iterations = it.value
+        T_WCs[:, 0, :] = pose
+        self.frames.update_T_WCs(T_WCs[pin:], uniq[pin:])

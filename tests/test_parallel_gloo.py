@@ -61,8 +61,11 @@ def _worker(rank, world, port, q):
         P.shard_keyframe_features(frames, range(6), enc)
         # numpy payloads travel by value: torch tensors would travel as shared-memory handles
         # whose owner may exit before the parent opens them (connection reset)
+        loc = {k: getattr(g, k).numpy() for k in ("idx_ii2jj", "idx_jj2ii", "valid_match_j",
+                                                  "valid_match_i", "Q_ii2jj", "Q_jj2ii")}
         q.put((rank, {k: v.numpy() for k, v in r.items()}, bool(added), g.ii.numpy(),
-               g.jj.numpy(), frames.feat[:6].float().numpy()))
+               g.jj.numpy(), frames.feat[:6].float().numpy(), g.owner.numpy(), loc,
+               g.local_edge_ids().numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -91,13 +94,24 @@ def test_sharded_edges_match_single_process(world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, r, added, ii, jj, feats in res:
+    # accepted edges in order, with the rank that matched each (edge e of the call → e % world)
+    pairs = list(zip(*EDGES))
+    acc = [pairs.index((int(i), int(j))) for i, j in zip(ref_g.ii, ref_g.jj)]
+    for rank, r, added, ii, jj, feats, owner, loc, ids in res:
         r = {k: torch.from_numpy(v) for k, v in r.items()}
         ii, jj, feats = torch.from_numpy(ii), torch.from_numpy(jj), torch.from_numpy(feats)
         for k in ref:
             assert torch.equal(r[k], ref[k].to(r[k].dtype)), (rank, k)
         assert added == ref_added
         assert torch.equal(ii, ref_g.ii) and torch.equal(jj, ref_g.jj)
+        # records stay on the rank that matched them: this rank's rows are the single-process
+        # graph's rows of the accepted edges it owns, in edge order
+        assert list(owner) == [e % world for e in acc]
+        rows = [k for k, e in enumerate(acc) if e % world == rank]
+        for name, v in loc.items():
+            assert torch.equal(torch.from_numpy(v), getattr(ref_g, name)[rows]), (rank, name)
+        E = len(acc)
+        assert list(ids) == rows + [k + E for k in rows]
         # every rank holds every keyframe's features, whoever encoded it
         for k in range(6):
             assert torch.all(feats[k] == float(k)), (rank, k)

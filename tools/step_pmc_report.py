@@ -1,0 +1,120 @@
+"""Per-step summary of rocprofv3 runs of tools/step_prof.py (the bench's captured C3 step).
+
+  python tools/step_pmc_report.py --pmc DIR [--trace DIR] [--flops-json F] --out profiles/X.json
+
+--pmc DIR: a `rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU GRBM_GUI_ACTIVE` run.
+  SQ_VALU_MFMA_BUSY_CYCLES = 32 x the v_mfma_f32_32x32x16_bf16 instructions issued (16 per
+  16x16x32; MI355X_MICROARCH.md 'Per-instruction cycle constants'), summed over the chip;
+  GRBM_GUI_ACTIVE = GPU-busy cycles summed over the 8 XCDs.  Dispatches strictly between
+  the two marker rownorm_kernel dispatches are the profiled steps.
+--trace DIR: a `--kernel-trace --stats` run of the same script: per-kernel-class durations
+  per step (traced: the tracer serialises the step's concurrent chains).
+Derived per step: MFMA-busy SIMD-cycles by kernel class, the MFMA instructions they imply
+(cycles / 32), the effective clock GRBM_GUI_ACTIVE / 8 / Σ dispatch time, and the MFMA
+utilisation of the UNTRACED step = busy SIMD-cycles / (1024 SIMDs x clock x step time),
+with the untraced step time taken from --step-ms (bench's ms_per_step)."""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+
+def _csv(d, suffix):
+    f = sorted(glob.glob(os.path.join(d, "**", "*" + suffix), recursive=True))
+    if not f:
+        raise SystemExit(f"no *{suffix} under {d}")
+    return list(csv.DictReader(open(f[-1])))
+
+
+def klass(name):
+    if "gemm_kernel" in name or "splitk_reduce" in name:
+        return "gemm"
+    if "attn_kernel" in name or "attn_combine" in name:
+        return "attn"
+    return "other"
+
+
+def between_markers(ids, names):
+    m = [d for d in ids if "rownorm_kernel" in names[d]]
+    if len(m) < 2:
+        raise SystemExit("markers not found")
+    return [d for d in ids if m[-2] < d < m[-1]]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pmc", required=True)
+    ap.add_argument("--trace", default=None)
+    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--step-ms", type=float, required=True, help="untraced ms per step")
+    ap.add_argument("--gemm-gflop", type=float, default=None,
+                    help="algorithmic GEMM GFLOP per step (bench step_timeline)")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    rows = _csv(a.pmc, "counter_collection.csv")
+    ctr = collections.defaultdict(dict)
+    names = {}
+    for r in rows:
+        d = int(r["Dispatch_Id"])
+        names[d] = r["Kernel_Name"]
+        ctr[d][r["Counter_Name"]] = ctr[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    ids = between_markers(sorted(names), names)
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    for d in ids:
+        k = klass(names[d])
+        for c, v in ctr[d].items():
+            per[k][c] += v
+        per[k]["dispatches"] += 1
+    S = a.steps
+    out = {"steps": S, "dispatches_per_step": len(ids) / S, "by_class": {}}
+    tot_busy = 0.0
+    for k, v in per.items():
+        busy = v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / S
+        tot_busy += busy
+        out["by_class"][k] = {"dispatches": v["dispatches"] / S,
+                              "mfma_busy_cycles": busy,
+                              "mfma_32x32x16_equiv": busy / 32.0,
+                              "implied_gflop": busy / 32.0 * 32768 / 1e9,
+                              "sq_busy_cu": v.get("SQ_BUSY_CU", 0.0) / S,
+                              "grbm_gui_active": v.get("GRBM_GUI_ACTIVE", 0.0) / S}
+    out["mfma_busy_cycles_per_step"] = tot_busy
+    if a.gemm_gflop:
+        g = out["by_class"].get("gemm", {})
+        out["gemm_counted_vs_algorithmic"] = g.get("implied_gflop", 0.0) / a.gemm_gflop
+    if a.trace:
+        tr = _csv(a.trace, "kernel_trace.csv")
+        tn = {}
+        dur = {}
+        for r in tr:
+            d = int(r["Dispatch_Id"])
+            tn[d] = r["Kernel_Name"]
+            dur[d] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6  # ms
+        tids = between_markers(sorted(tn), tn)
+        t0 = min(int(r["Start_Timestamp"]) for r in tr if int(r["Dispatch_Id"]) in set(tids))
+        t1 = max(int(r["End_Timestamp"]) for r in tr if int(r["Dispatch_Id"]) in set(tids))
+        cls = collections.defaultdict(float)
+        for d in tids:
+            cls[klass(tn[d])] += dur[d]
+        out["traced"] = {"span_ms_per_step": (t1 - t0) * 1e-6 / S,
+                         "kernel_ms_per_step": {k: v / S for k, v in cls.items()},
+                         "dispatches_per_step": len(tids) / S}
+    # effective clock from the PMC run: GRBM_GUI_ACTIVE is summed over the 8 XCDs
+    if a.trace:
+        ksum = sum(out["traced"]["kernel_ms_per_step"].values())
+        grbm = sum(v["grbm_gui_active"] for v in out["by_class"].values())
+        out["clock_ghz_est"] = grbm / 8.0 / (ksum * 1e-3) / 1e9 if ksum else None
+    clk = out.get("clock_ghz_est") or 2.4
+    out["untraced_step_ms"] = a.step_ms
+    out["mfma_util_step"] = tot_busy / (1024.0 * clk * 1e9 * a.step_ms * 1e-3)
+    out["mfma_util_step_at_2.4GHz"] = tot_busy / (1024.0 * 2.4e9 * a.step_ms * 1e-3)
+    out["note"] = ("MFMA utilisation = MFMA-busy SIMD-cycles per step / (1024 SIMDs x clock x "
+                   "untraced step time); the PMC run serialises dispatches, which does not "
+                   "change the cycles the MFMA instructions occupy")
+    json.dump(out, open(a.out, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
