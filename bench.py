@@ -72,6 +72,9 @@ def parse():
                     help="encode each frame inside its own step (no next-frame encoder overlap)")
     ap.add_argument("--streams", action="store_true",
                     help="overlap independent chains on side streams (measured slower)")
+    ap.add_argument("--prefetch-after", type=int, default=None,
+                    help="start the next frame's encoder after this MonST3R decoder layer "
+                         "(default: at the step's start)")
     ap.add_argument("--timeline-out", default=None,
                     help="write one replayed step's per-launch GEMM / attention timeline (JSON)")
     ap.add_argument("--no-timeline", action="store_true",
@@ -220,8 +223,8 @@ def step_timeline(loop, dev, replays=24, out_path=None):
     import numpy as np
     from monst3r_slam_amd import _lib
     lib, P = _lib.load(), _lib.ptr
-    cap = 8192
-    buf = torch.empty((cap, 2), dtype=torch.int64, device=dev)
+    cap = 2048
+    buf = torch.empty((cap, 64, 2), dtype=torch.int64, device=dev)
 
     def cap_tl(k):
         loop.step(k)                      # warm / allocate outside the timeline
@@ -254,8 +257,8 @@ def step_timeline(loop, dev, replays=24, out_path=None):
     keep = None
     for i in range(replays):
         g, a, b = graphs[i % 2]
-        buf[:, 0] = -1                    # UINT64_MAX: atomic-min target
-        buf[:, 1] = 0
+        buf[..., 0] = -1                  # UINT64_MAX: atomic-min target
+        buf[..., 1] = 0
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st = torch.cuda.current_stream(dev)
         e0.record(st)
@@ -263,8 +266,10 @@ def step_timeline(loop, dev, replays=24, out_path=None):
         e1.record(st)
         e1.synchronize()
         step_ms = e0.elapsed_time(e1)
-        t = buf[a:b].cpu().numpy()
-        ok = (t[:, 1] > 0) & (t[:, 0] > 0)
+        tb = buf[a:b].cpu().numpy()       # [launches, 64, 2]; unused pairs stay (-1, 0)
+        st_ = np.where(tb[..., 0] > 0, tb[..., 0], np.iinfo(np.int64).max).min(1)
+        t = np.stack([st_, tb[..., 1].max(1)], 1)
+        ok = (t[:, 1] > 0) & (t[:, 0] < np.iinfo(np.int64).max)
         if not ok.all():
             raise RuntimeError(f"step timeline: {int((~ok).sum())} launches left no stamp")
         k, fl = kinds[a:b], flops[a:b]
@@ -487,7 +492,17 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
         dist.barrier()
     el = time.perf_counter() - t0
     model.symmetric = real_sym
-    valid_frac = float(graph.valid_match_j.float().mean()) if graph.ii.numel() else 0.0
+    # the backend GN alone, from the graph's initial poses, through the edge-sharded path
+    # (per iteration: each rank's edge pass + the E x 35 all-gather + the fp64 solve)
+    frames.T_WC[:n_kf] = T0
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    graph._solve_sharded("rays")
+    gn_ms = (time.perf_counter() - t1) * 1e3
+    gn_it = max(1, int(graph.gn_iterations))
+    valid_frac = float(graph.valid_match_j.float().mean()) if graph.valid_match_j.numel() else 0.0
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -501,8 +516,15 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
             "pointmaps": "scene geometry stand-in over the network outputs (the decode runs)",
             "valid_match_frac": valid_frac,
             "gflop_per_pair": 3603.6, "tflops_achieved": len(ii) * 3603.6e9 * steps / el / 1e12,
-            "allgather_bytes_per_rank": int(-(-len(ii) // world) * P.record_bytes(n)),
-            "sharding": f"edges round-robin over {world} rank(s), RCCL all-gather; newest "
+            "gn": {"ms": gn_ms, "iterations": gn_it, "ms_per_iteration": gn_ms / gn_it,
+                   "edges_two_way": 2 * int(graph.ii.numel()),
+                   "timing": "graph._solve_sharded('rays') from the graph's initial poses, "
+                             "host wall incl. the final status sync"},
+            "records_kept_per_rank_bytes": int(-(-len(ii) // world) * P.record_bytes(n)),
+            "allgather_bytes_per_rank": int(16 * len(ii)),
+            "sharding": f"edges round-robin over {world} rank(s): records stay on the matching "
+                        f"rank, match fractions (16 B/edge) all-gathered, GN edge pass sharded "
+                        f"with one E x 35 f64 all-gather per iteration; newest "
                         f"keyframe pointmap broadcast from the tracking rank "
                         f"({P.keyframe_record_bytes(n) / 1e6:.1f} MB)"}
 
@@ -650,8 +672,33 @@ def pmc_traffic():
     return None
 
 
+def cgroup_cpu_limit():
+    """CPUs the container's cgroup grants (cgroup v2 cpu.max quota / period; v1 cfs files);
+    None when unlimited or unreadable."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / p
+    except (OSError, ValueError):
+        return None
+
+
+def host_threads():
+    """Threads the CPU baseline uses: every CPU this process may run on (affinity mask),
+    capped by the cgroup's CPU quota when one is set."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    lim = cgroup_cpu_limit()
+    n = aff if lim is None else max(1, min(aff, int(lim)))
+    return n, aff, lim
+
+
 def host_cpu():
-    """Host CPU model and thread count (the GPU box's /proc/cpuinfo; lscpu's 'Model name')."""
+    """Host CPU model and thread counts (the GPU box's /proc/cpuinfo; lscpu's 'Model name')."""
     model = None
     try:
         for line in open("/proc/cpuinfo"):
@@ -660,7 +707,9 @@ def host_cpu():
                 break
     except OSError:
         pass
-    return {"model": model, "logical_cpus": os.cpu_count()}
+    n, aff, lim = host_threads()
+    return {"model": model, "logical_cpus": os.cpu_count(), "affinity_cpus": aff,
+            "cgroup_cpu_limit": lim, "threads_used": n}
 
 
 def cpu_baseline(seq):
@@ -678,9 +727,9 @@ def cpu_baseline(seq):
     from oracle import oracle as O
     from oracle import vit_ref as V
     torch.set_flush_denormal(True)
-    nthreads = min(16, os.cpu_count() or 1)
+    nthreads = host_threads()[0]
     torch.set_num_threads(nthreads)
-    os.environ.setdefault("OMP_NUM_THREADS", str(nthreads))
+    os.environ["OMP_NUM_THREADS"] = str(nthreads)   # the C oracle's OpenMP matching
     am, aM = Wt.MONST3R, Wt.MAST3R
     sdm = Wt.make_state_dict(am, 0)
     sdM = Wt.make_state_dict(aM, 1)
@@ -692,6 +741,7 @@ def cpu_baseline(seq):
         V.asymmetric_inference(sdm, am, sdM, aM, img_i, img_j, feat_j=feat_j)
         t_vit = time.perf_counter() - t0
     O.build()
+    O.set_threads(nthreads)
     cfg = default_config()
     Tt, Tj = seq.T_gt_np[1], seq.T_gt_np[0]
     Trel = syn.sim3_mul(syn.sim3_inv(Tt), Tj)
@@ -771,6 +821,8 @@ def main():
     model, tr, seq = setup(dev, rank, n_frames)
     model.serial = not args.streams
     tr.split_heads = not args.no_split_heads
+    if args.prefetch_after is not None:
+        model.layer_event_at = args.prefetch_after
 
     from monst3r_slam_amd import sequence as S
     from monst3r_slam_amd.frontend import FramePipeline

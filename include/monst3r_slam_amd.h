@@ -45,8 +45,10 @@ int m3s_device_count(void);
 /* Step timeline (diagnostic; bench.py step_timeline).  m3s_timeline_set(d_buf, capacity)
  * arms it: every GEMM (m3s_vit_gemm) and attention (m3s_vit_attention) launch issued
  * afterwards — eager or captured into a graph — takes the next of `capacity` slots of
- * d_buf (u64 [capacity][2]: earliest block start, latest wave end, s_memrealtime ticks of
- * 100 MHz; the caller fills each slot with {UINT64_MAX, 0} before a run).  A null d_buf
+ * d_buf (u64 [capacity][64][2]: per slot 64 pairs {earliest block start, latest wave end}
+ * in s_memrealtime ticks of 100 MHz, block b stamping pair b % 64; the launch spans
+ * [min of the starts, max of the ends]; the caller fills every pair with {UINT64_MAX, 0}
+ * before a run).  A null d_buf
  * disarms it (later launches carry no slot).  m3s_timeline_count() = slots taken since the
  * last set; m3s_timeline_meta() copies their kinds (1 GEMM, 2 attention), algorithmic
  * FLOPs (2·M·N·K·batch; 4·Sq·Sk·64·heads·batch) and dims ({M, N, K, batch};
@@ -381,6 +383,15 @@ int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q, const voi
  * with K ordered (c, ky, kx) like the conv weight [1024][3][16][16]. */
 int m3s_vit_patchify(const float* d_img, void* d_out, int64_t batch, int64_t h, int64_t w,
                      void* stream);
+
+/* Strided row copy (decoder input assembly, the local-feature concat): for o < outer,
+ * i < inner, copy `rows` rows of row_bytes from src + o·src_outer + i·src_inner + src_base
+ * (row stride src_row_stride) to dst + o·dst_outer + i·dst_inner + dst_base (row stride
+ * dst_row_stride); every size, stride, base and pointer a multiple of 16 bytes. */
+int m3s_copy_rows(const void* d_src, void* d_dst, int64_t rows, int64_t row_bytes,
+                  int64_t src_row_stride, int64_t dst_row_stride, int64_t outer, int64_t inner,
+                  int64_t src_outer, int64_t src_inner, int64_t src_base, int64_t dst_outer,
+                  int64_t dst_inner, int64_t dst_base, void* stream);
 
 /* Bilinear x2 upsample, align_corners=True (dpt_block.py:215-216), NHWC bf16
  * [B][h][w][C] → [B][oh][ow][C] (oh ≤ 2h, ow ≤ 2w: the DPT crop of dpt_head.py:57);

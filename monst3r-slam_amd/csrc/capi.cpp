@@ -18,6 +18,7 @@ extern "C" const char* m3s_status_string(int status) {
 extern "C" int m3s_version(void) { return (0 << 16) | (1 << 8) | 0; }
 
 // ---- step timeline (common.h) ----
+#define M3S_TL_SUB_HOST 64   // = M3S_TL_SUB: stamp pairs per slot
 namespace {
 unsigned long long* g_tl = nullptr;
 int g_tl_cap = 0, g_tl_n = 0;
@@ -32,7 +33,7 @@ unsigned long long* m3s_timeline_take(int kind, double flops, int64_t d0, int64_
   g_tl_kind.push_back(kind);
   g_tl_flops.push_back(flops);
   g_tl_dims.insert(g_tl_dims.end(), {d0, d1, d2, d3});
-  return g_tl + 2 * (int64_t)g_tl_n++;
+  return g_tl + 2 * M3S_TL_SUB_HOST * (int64_t)g_tl_n++;
 }
 
 extern "C" int m3s_timeline_set(void* d_buf, int capacity) {

@@ -43,21 +43,28 @@ __device__ __forceinline__ double m3s_wave_sum_d(double v) {
 
 // ---- step timeline (diagnostic, include/monst3r_slam_amd.h m3s_timeline_set) ----
 // While a timeline buffer is set, each instrumented launch (GEMM, attention) takes the next
-// slot: two u64 s_memrealtime stamps (100 MHz), [0] = earliest block start (atomic min by
-// one lane per block), [1] = latest wave end (atomic max by one lane per wave).  The slot
-// pointer travels in the kernel arguments, so a captured graph keeps its launches' slots;
-// with no buffer set the pointer is null and the kernels only test it.
+// slot: M3S_TL_SUB pairs of u64 s_memrealtime stamps (100 MHz), [0] = earliest block start
+// (atomic min by one lane per block), [1] = latest wave end (atomic max by one lane per
+// wave), block b updating pair b % M3S_TL_SUB — one address per launch took every block's
+// atomics in series and stretched the step 1.4x.  The slot pointer travels in the kernel
+// arguments, so a captured graph keeps its launches' slots; with no buffer set the pointer
+// is null and the kernels only test it.
 enum { M3S_TL_GEMM = 1, M3S_TL_ATTN = 2 };
+#define M3S_TL_SUB 64
 unsigned long long* m3s_timeline_take(int kind, double flops, int64_t d0, int64_t d1, int64_t d2,
                                         int64_t d3);  // capi.cpp; null when off
 
+__device__ __forceinline__ unsigned long long* m3s_tl_pair(unsigned long long* tl) {
+  return tl + 2 * ((blockIdx.x + blockIdx.y * 7) % M3S_TL_SUB);
+}
 __device__ __forceinline__ void m3s_tl_begin(unsigned long long* tl) {
-  if (tl && threadIdx.x == 0) atomicMin(tl, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (tl && threadIdx.x == 0)
+    atomicMin(m3s_tl_pair(tl), (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 struct M3sTlEnd {  // stamps the wave's end on every return path
   unsigned long long* p;
   __device__ __forceinline__ ~M3sTlEnd() {
     if (p && (threadIdx.x & 63) == 0)
-      atomicMax(p + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+      atomicMax(m3s_tl_pair(p) + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 };

@@ -84,9 +84,14 @@ __device__ __forceinline__ void jac_row(const float* d, const float* P, float* J
   J[6] = -(d[0] * P[0] + d[1] * P[1] + d[2] * P[2]);
 }
 
-__global__ void track_init_kernel(const float* __restrict__ Twc_k, const float* __restrict__ Twc_f,
-                                  TrackState* st) {
-  if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(256) void track_init_kernel(const float* __restrict__ Twc_k,
+                                                         const float* __restrict__ Twc_f,
+                                                         TrackState* st, uint4* gran,
+                                                         int gran_vec) {
+  // the persistent launch's hand-off granules start zeroed (was a memset node)
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < gran_vec; i += gridDim.x * 256)
+    gran[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
   // T_CkCf = T_WCk^-1 * T_WCf
   m3s_rel_sim3<float>(Twc_k, Twc_k + 3, Twc_k[7], Twc_f, Twc_f + 3, Twc_f[7], st->T, st->T + 3,
                       st->T + 7);
@@ -621,7 +626,7 @@ struct Layout {
 };
 Layout layout() {
   Layout L;
-  L.gran = 0;  // zeroed per call (a memset node): 2 parity slots of 256 x 36 granules
+  L.gran = 0;  // zeroed per call by track_init_kernel: 2 parity slots of 256 x 36 granules
   L.state = sizeof(unsigned long long) * 2 * kPersistentBlocks * kAcc;
   L.partial = L.state + 512;
   L.total = L.partial + sizeof(float) * kBlocks * kAcc;
@@ -644,10 +649,13 @@ int run_track(const float* Twc_k, const float* Twc_f, const float* Xf, const flo
   TrackState* st = reinterpret_cast<TrackState*>(w + L.state);
   float* partial = reinterpret_cast<float*>(w + L.partial);
   unsigned long long* gran = reinterpret_cast<unsigned long long*>(w + L.gran);
-  hipLaunchKernelGGL(track_init_kernel, dim3(1), dim3(64), 0, s, Twc_k, Twc_f, st);
-  M3S_LAUNCH_CHECK();
   const char* e = getenv("M3S_TRACK_PERSISTENT");  // A/B: 0 = one launch per iteration
-  if (!e || atoi(e) != 0) {
+  const bool persistent = !e || atoi(e) != 0;
+  const int gran_vec = persistent && max_iters > 0 ? (int)((L.state - L.gran) / 16) : 0;
+  hipLaunchKernelGGL(track_init_kernel, dim3(gran_vec ? 36 : 1), dim3(256), 0, s, Twc_k, Twc_f,
+                     st, reinterpret_cast<uint4*>(w + L.gran), gran_vec);
+  M3S_LAUNCH_CHECK();
+  if (persistent) {
     int nb = (int)((n + kThreads - 1) / kThreads);
     if (nb > kPersistentBlocks) nb = kPersistentBlocks;
     if (const char* b = getenv("M3S_TRACK_BLOCKS"))  // tuning knob (tools/track_bench.py)
@@ -659,7 +667,6 @@ int run_track(const float* Twc_k, const float* Twc_f, const float* Xf, const flo
     const char* ab = getenv("M3S_TRACK_ABORT_AT");
     const int abort_at = ab ? atoi(ab) : -1;
     if (max_iters > 0) {
-      M3S_HIP_CHECK(hipMemsetAsync(gran, 0, L.state - L.gran, s));
       hipLaunchKernelGGL(track_persistent_kernel<MODE>, dim3(nb), dim3(kThreads), 0, s, st, prm,
                          K, Xf, Xk, Qk, valid, meas_k, valid_meas, n, gran, max_iters,
                          rel_error, delta_norm, spin_limit, abort_at);

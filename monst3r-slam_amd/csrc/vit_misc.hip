@@ -338,6 +338,49 @@ extern "C" int m3s_vit_patchify(const float* d_img, void* d_out, int64_t batch, 
   return M3S_OK;
 }
 
+namespace {
+// Strided row copy of `outer x inner` items (decoder input assembly, local-feature concat):
+// item (o, i) copies `rows` rows of row_bytes from src + o·src_outer + i·src_inner + src_base
+// (row stride src_row) to dst + o·dst_outer + i·dst_inner + dst_base (row stride dst_row),
+// 16 B per thread (all sizes, strides and bases 16-B multiples: checked on the host).
+__global__ __launch_bounds__(256) void copy_rows_kernel(
+    const char* __restrict__ src, char* __restrict__ dst, int64_t rows, int64_t vpr,
+    int64_t src_row, int64_t dst_row, int64_t inner, int64_t src_outer, int64_t src_inner,
+    int64_t dst_outer, int64_t dst_inner, int64_t total) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int64_t v = t % vpr;
+  const int64_t r = (t / vpr) % rows;
+  const int64_t item = t / (vpr * rows);
+  const int64_t o = item / inner, i = item - o * inner;
+  const uint4 x = *reinterpret_cast<const uint4*>(src + o * src_outer + i * src_inner +
+                                                  r * src_row + v * 16);
+  *reinterpret_cast<uint4*>(dst + o * dst_outer + i * dst_inner + r * dst_row + v * 16) = x;
+}
+}  // namespace
+
+extern "C" int m3s_copy_rows(const void* d_src, void* d_dst, int64_t rows, int64_t row_bytes,
+                             int64_t src_row_stride, int64_t dst_row_stride, int64_t outer,
+                             int64_t inner, int64_t src_outer, int64_t src_inner,
+                             int64_t src_base, int64_t dst_outer, int64_t dst_inner,
+                             int64_t dst_base, void* stream) {
+  if (!d_src || !d_dst || rows < 0 || row_bytes < 0 || outer < 0 || inner <= 0)
+    return M3S_ERR_INVALID_ARG;
+  const int64_t total = outer * inner * rows * (row_bytes / 16);
+  if (total == 0) return M3S_OK;
+  const int64_t al = row_bytes | src_row_stride | dst_row_stride | src_outer | src_inner |
+                     src_base | dst_outer | dst_inner | dst_base |
+                     (int64_t)(uintptr_t)d_src | (int64_t)(uintptr_t)d_dst;
+  if (al % 16) return M3S_ERR_INVALID_ARG;
+  hipLaunchKernelGGL(copy_rows_kernel, dim3(m3s_div_up(total, 256)), dim3(256), 0,
+                     m3s_stream(stream), reinterpret_cast<const char*>(d_src) + src_base,
+                     reinterpret_cast<char*>(d_dst) + dst_base, rows, row_bytes / 16,
+                     src_row_stride, dst_row_stride, inner, src_outer, src_inner, dst_outer,
+                     dst_inner, total);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
 extern "C" int m3s_vit_upsample2x(const void* d_in, void* d_out, const void* d_add,
                                   int64_t batch, int64_t h, int64_t w, int64_t c, int64_t oh,
                                   int64_t ow, void* stream) {

@@ -68,6 +68,8 @@ SIGNATURES = {
                                _I, _I64, _I64, _I64, _I64, _F, _P, _I64, _I, _P]),
     "m3s_vit_rope_table": (_I, [_P, _I64, _F, _P, _P]),
     "m3s_vit_patchify": (_I, [_P, _P, _I64, _I64, _I64, _P]),
+    "m3s_copy_rows": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64,
+                           _I64, _I64, _P]),
     "m3s_vit_upsample2x": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
     "m3s_vit_dpt_out": (_I, [_P, _P, _P, _P, _P, _I64, _F, _I64, _I64, _I64, _I64, _P]),
     "m3s_vit_local_features": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P]),

@@ -96,9 +96,9 @@ class Tracker:
         H, W = Xii.shape[1:3]
         n = H * W
         # matching.match(Xii, Xji, Dii, Dji, idx_init)  (monst3r_utils.py:498-499)
+        # tracker2.py:127: the matches become the next frame's seed — written in place
         idx, valid_match = M.match(Xii, Xji, out["D16"][0:1], out["D16"][1:2], self.idx_f2k,
-                                   self.cfg["matching"])
-        self.idx_f2k.copy_(idx)                            # tracker2.py:127
+                                   self.cfg["matching"], idx_out=self.idx_f2k)
         idx = idx[0]
         valid_match = valid_match[0]                       # [N,1]
         if self.fused_glue and out["X"].is_contiguous() and out["C"].is_contiguous():

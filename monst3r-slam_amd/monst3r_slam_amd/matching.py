@@ -40,8 +40,10 @@ def prep_for_iter_proj(X11, X21, idx_1_to_2_init=None):
     return rwg, pts, p_init
 
 
-def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None):
-    """matching.py:52-90.  Returns (idx_1_to_2 [b,hw] int64, valid [b,hw,1] bool)."""
+def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None, idx_out=None):
+    """matching.py:52-90.  Returns (idx_1_to_2 [b,hw] int64, valid [b,hw,1] bool).
+    idx_out: int64 [b,hw] to write the indices into (may be idx_1_to_2_init itself: the
+    kernels read the seed before the last one writes the result, in stream order)."""
     cfg = cfg or _config["matching"]
     _lib.require_cuda(X11, X21, D11, D21, names=("X11", "X21", "D11", "D21"))
     lib = _lib.load()
@@ -72,11 +74,17 @@ def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None):
                                           int(cfg["radius"]), int(cfg["dilation_max"]), s),
                    "refine_matches")
         p1 = p1n
-    idx = torch.empty((b, n), dtype=torch.int64, device=dev)
+    if idx_out is not None:
+        if idx_out.shape != (b, n) or idx_out.dtype != torch.int64 or not idx_out.is_contiguous():
+            raise RuntimeError("match: idx_out must be contiguous int64 [b, h*w]")
+        idx = idx_out
+    else:
+        idx = torch.empty((b, n), dtype=torch.int64, device=dev)
     _lib.check(lib.m3s_pixel_to_lin(_lib.ptr(p1), _lib.ptr(idx), b, n, w, s), "pixel_to_lin")
-    return idx, valid.bool().unsqueeze(-1)
+    # the kernels store 0 / 1 bytes: reinterpret as bool (no conversion pass)
+    return idx, valid.view(torch.bool).unsqueeze(-1)
 
 
-def match(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None):
+def match(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None, idx_out=None):
     """matching.py:8-10."""
-    return match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init, cfg)
+    return match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init, cfg, idx_out)

@@ -182,6 +182,13 @@ class Ops:
                                               _p(ws), ws.numel(), kv_xor, self._s()),
                    "vit_attention")
 
+    def copy_rows(self, src, dst, rows, row_bytes, src_row, dst_row, outer, inner, src_outer,
+                  src_inner, src_base, dst_outer, dst_inner, dst_base):
+        """m3s_copy_rows (byte strides): item (o, i) of outer x inner copies `rows` rows."""
+        _lib.check(self.lib.m3s_copy_rows(_p(src), _p(dst), rows, row_bytes, src_row, dst_row,
+                                          outer, inner, src_outer, src_inner, src_base,
+                                          dst_outer, dst_inner, dst_base, self._s()), "copy_rows")
+
     def patchify(self, img, out, b, h, w):
         _lib.check(self.lib.m3s_vit_patchify(_p(img), _p(out), b, h, w, self._s()), "patchify")
 
@@ -438,6 +445,12 @@ class PairModel:
         # the pair decoder split by model onto two streams (decode_multi; M3S_DEC_SPLIT=0
         # restores the single batch-4 chain): 214.0 → 218.3 frames/s (2 × A/B)
         self.dec_split = os.environ.get("M3S_DEC_SPLIT", "1") == "1"
+        # schedule knob: an event recorded on the MonST3R decoder chain after layer
+        # `layer_event_at` (None: no event) — the pipelined loop starts the next frame's
+        # encoder behind it instead of at the step's start (M3S_PREFETCH_AFTER)
+        e = os.environ.get("M3S_PREFETCH_AFTER")
+        self.layer_event_at = int(e) if e not in (None, "") else None
+        self.layer_event = None
         # split heads: the local-feature MLP runs on the side chain ahead of the MASt3R heads
         self.lf_side = os.environ.get("M3S_LF_SIDE", "1") != "0"
         self._tag = None      # buffer-key prefix of the head set being issued (split heads)
@@ -609,9 +622,15 @@ class PairModel:
         self._wm = wm
         Z = wm * G
         h0 = self._buf("h0", (Z, S, E), BF16)
-        hv = h0.view(G, models, 2, S, E)
-        hv[:, :, 0].copy_(feat1.reshape(G, 1, S, E).expand(G, models, S, E))
-        hv[:, :, 1].copy_(feat2.reshape(G, 1, S, E).expand(G, models, S, E))
+        # h0[(g·models + m)·2 + side] = (feat1 | feat2)[g] for every model m: one row copy
+        # per side (in-tree kernel), feat_* [G,S,E] contiguous
+        fb = S * E * 2
+        for side, f in ((0, feat1), (1, feat2)):
+            f = f.reshape(G, S, E)
+            if not f.is_contiguous():
+                raise RuntimeError("decode_multi: features must be contiguous [G,S,E]")
+            o.copy_rows(f, h0, 1, fb, fb, fb, G, models, fb, 0, 0, 2 * models * fb, 2 * fb,
+                        side * fb)
         x = self._buf("dec_x", (Z, S, D), F32)
         fold = self.lnfold and not self.fp8 and self.serial and D % 128 == 0
         if fold:
@@ -774,6 +793,10 @@ class PairModel:
             o.gemm(xb, P["fc1_wf"], hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm,
                    bias=P["fc1_c2"], sBias=Dm, flags=_lib.EPI_GELU, wmod=wm,
                    ln_fold=(st, P["fc1_c1"], 0), tile=tl("fc1"))
+            if part in (None, 0) and self.layer_event_at is not None and \
+                    i + 1 == self.layer_event_at:
+                self.layer_event = torch.cuda.Event()
+                self.layer_event.record(torch.cuda.current_stream(self.dev))
             xc = xb
             if (i + 1) in hk:
                 xc = hook_bufs[i + 1]
@@ -849,9 +872,14 @@ class PairModel:
         dconf = self._buf("desc_conf", (2 * G, H, W), F32)
         with self._on(1):
             cat = self._buf("lf_cat", (2 * G, S, idim), BF16)
-            cv = cat.view(G, 2, S, idim)
-            cv[..., :E].copy_(hooks["h0"].view(G, 2, 2, S, E)[:, 1])
-            cv[..., E:].copy_(hooks["h12"].view(G, 2, 2, S, D)[:, 1])
+            # cat[g·2 + side] = [h0 | h12] of problem z = g·4 + 2 + side (MASt3R's two views)
+            h0, h12 = hooks["h0"], hooks["h12"]
+            if not (h0.is_contiguous() and h12.is_contiguous()):
+                raise RuntimeError("local features: hooks must be contiguous")
+            for src, width, off in ((h0, E, 0), (h12, D, 2 * E)):
+                rb = width * 2
+                o.copy_rows(src, cat, S, rb, rb, idim * 2, G, 2, 4 * S * rb, S * rb, 2 * S * rb,
+                            2 * S * idim * 2, S * idim * 2, off)
             lh = self._buf("lf_hid", (2 * G, S, hidd), BF16)
             o.gemm(cat, self.w.lf_fc1_w, lh, S, hidd, idim, 2 * G, sA=S * idim,
                    sB=hidd * idim, sC=S * hidd, bias=self.w.lf_fc1_b, sBias=hidd,
@@ -910,8 +938,11 @@ class PairModel:
                 sub = {k: v[2:4] for k, v in hooks.items()}
                 self.ops.tile_default = st.get("dpt")
                 try:
-                    self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4],
-                              R=None if R is None else [r[2:4] for r in R])
+                    # M3S_ABLATE_MAST3R_DPT=1: diagnostic ablation only (tools/step_ablation):
+                    # the discarded MASt3R pts3d / conf heads are not issued
+                    if os.environ.get("M3S_ABLATE_MAST3R_DPT") != "1":
+                        self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4],
+                                  R=None if R is None else [r[2:4] for r in R])
                 finally:
                     self.ops.tile_default = None
                 self._ev_heads = torch.cuda.Event()

@@ -243,7 +243,11 @@ class ShardedFactorGraph(FactorGraph):
         """global_opt2.py:35-107 with the records kept on the rank that matched them."""
         world, rank = _world(self.group)
         if world == 1:
-            return super().add_factors(ii, jj, min_match_frac, is_reloc)
+            n0 = self.ii.numel()
+            added = super().add_factors(ii, jj, min_match_frac, is_reloc)
+            self.owner = torch.cat([self.owner, torch.zeros(self.ii.numel() - n0,
+                                                            dtype=torch.int32, device=self.device)])
+            return added
         ii, jj = [int(i) for i in ii], [int(j) for j in jj]
         E = len(ii)
         mine = list(range(rank, E, world))
@@ -355,7 +359,8 @@ class ShardedFactorGraph(FactorGraph):
                     float(c["depth_eps"]), float(c["sigma_pixel"]), float(c["sigma_depth"]),
                     float(c["C_conf"]), float(c["Q_conf"]), ptr(G_loc), ptr(ws), s)
             _lib.check(st, "gn_edge_pass")
-            gathered = _all_gather_fixed(G_loc, self.group).reshape(world * pad, 35)
+            gathered = (_all_gather_fixed(G_loc, self.group) if world > 1 else G_loc).reshape(
+                world * pad, 35)
             G_all[dst] = gathered[take]
             _lib.check(lib.m3s_gn_solve_step(ptr(pose), ptr(G_all), P, N, E2, El,
                                              float(c["delta_norm"]), ptr(dx), ptr(ws), s),

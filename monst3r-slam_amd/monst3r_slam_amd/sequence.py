@@ -250,13 +250,22 @@ class SequenceLoop:
         feat_i = None
         if m is not None:
             if pipe is not None:
+                feat_i = pipe.feat[k % 2]
+                delay = m.layer_event_at is not None
+                if delay:   # the pair first: the encoder waits for its decoder layer event
+                    m.layer_event = None
+                    out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i,
+                                 split_heads=split)
                 pipe.side.wait_stream(main)
+                if delay and m.layer_event is not None:
+                    pipe.side.wait_event(m.layer_event)
                 with torch.cuda.stream(pipe.side):
                     self.gather(self.img_next, 1)
                     self._gathered.record(pipe.side)
                     m.encode(self.img_next, out=pipe.feat[(k + 1) % 2], concurrent=True)
-                feat_i = pipe.feat[k % 2]
-                out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i, split_heads=split)
+                if not delay:
+                    out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i,
+                                 split_heads=split)
             else:
                 self.gather(self.img_cur, 0)
                 out = m.pair(self.img_cur, feat_j=tr.kf.feat, split_heads=split)

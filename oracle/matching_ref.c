@@ -383,3 +383,8 @@ void ref_match_occlusion(const float* X11, const float* X21, const float* p,
     valid[q] = (conv[q] && d < dist_thresh) ? 1 : 0;
   }
 }
+
+/* OpenMP thread count of the restatement (the CPU baseline uses every host core). */
+void ref_set_threads(int n) {
+  if (n > 0) omp_set_num_threads(n);
+}

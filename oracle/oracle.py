@@ -50,8 +50,15 @@ def lib():
         L.ref_match_occlusion.restype = None
         L.ref_float_to_half.argtypes = [ctypes.c_float]
         L.ref_float_to_half.restype = ctypes.c_uint16
+        L.ref_set_threads.argtypes = [ctypes.c_int]
+        L.ref_set_threads.restype = None
         _lib = L
     return _lib
+
+
+def set_threads(n):
+    """OpenMP threads of the C restatement (bench.py cpu_baseline: the host's cores)."""
+    lib().ref_set_threads(int(n))
 
 
 def _p(a):

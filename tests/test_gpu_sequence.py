@@ -154,3 +154,78 @@ def test_c3_sequence_384x512_vs_oracle(dev, parity_log):
     parity_log("test_c3_sequence_384x512_vs_oracle", frames=F - 1, new_keyframes=n_new,
                lost=1, idx_valid="bit-exact", max_abs_dT=dT_max, tol_dT=1e-4, ate_m=ate,
                gn_iterations_hist=summ["gn_iterations_hist"])
+
+
+def test_c3_sequence_200_pipelined_vs_oracle(dev, parity_log):
+    """The headline workload end to end (BASELINE configs[2] as bench.py runs it): all 200
+    frames of the synthetic 384x512 room sequence through SequenceLoop with the full-size
+    models and the prefetching FramePipeline (the next frame's encoder on a side stream,
+    feature double buffer), the stand-in pair outputs, matching, pose solve, keyframe fusion
+    and every keyframe replacement — each frame checked against the numpy/C oracle of the
+    same main loop: match indices / validity bit-exact, lost / new-keyframe decisions equal,
+    |dT_WCf| <= 1e-4, keyframe state within the 32-frame test's tolerances.  The oracle is
+    re-seeded each frame with the GPU's incoming state (pose seed, keyframe pose, pointmap,
+    confidence, count, match seed): the pose solve stops at |dcost/cost| < 1e-3 or
+    |tau| < 1e-3 (tracker2.py:299-357), so a 1e-5 difference in the seed moves the converged
+    pose by up to ~1e-4 and 200 chained frames drift apart by more than any per-frame error
+    (the chained, unseeded comparison is test_c3_sequence_384x512_vs_oracle, 32 frames).  Every 20th
+    frame, the prefetched features must be bit-identical to an encode of the NEXT frame's
+    image (the side stream's gather of the frame counter is ordered before the main
+    stream's advance rewrites it)."""
+    import bench
+    from monst3r_slam_amd import sequence as S
+    from monst3r_slam_amd.config import default_config
+    from monst3r_slam_amd.frontend import FramePipeline
+    from oracle import frontend_ref as FR
+    cfg = default_config()
+    model, tr, seq = bench.setup(dev, 0, bench.SEQ_FRAMES + 1)
+    pipe = FramePipeline(tr, (seq.h, seq.w))
+    loop = S.SequenceLoop(tr, seq, pipe)
+    loop.reset(parity=0)
+    T0 = np.array([0, 0, 0, 0, 0, 0, 1, 1], np.float32)
+    o = FR.SequenceOracle(seq.Xcam[0].cpu().numpy(), seq.C_own[0].reshape(-1, 1).cpu().numpy(),
+                          T0, cfg)
+    n_new, dT_max, n_feat = 0, 0.0, 0
+    for i in range(bench.SEQ_FRAMES):
+        f = i + 1
+        # the GPU's incoming state → the oracle (see docstring)
+        o.T_prev = loop.T_prev.cpu().numpy().copy()
+        o.kf.T_WC = tr.kf.T_WC.cpu().numpy().reshape(8).copy()
+        o.kf.X_canon = tr.kf.X_canon.cpu().numpy().copy()
+        o.kf.C = tr.kf.C.cpu().numpy().copy()
+        o.kf.N = float(tr.kf.N)
+        o.idx = tr.idx_f2k.cpu().numpy().copy()
+        res = loop.step(i)
+        out = res["pair"]
+        X, C = out["X"].cpu().numpy(), out["C"].cpu().numpy()
+        D16, Q = out["D16"].cpu().numpy(), out["Q"].cpu().numpy()
+        ref = o.step(X, C, D16, Q)
+        assert np.array_equal(res["idx_f2k"].cpu().numpy(), ref["idx"]), f
+        assert np.array_equal(res["valid_match"].cpu().numpy(), ref["valid"]), f
+        lost, new_kf = bool(res["lost"]), bool(res["new_kf"])
+        assert lost == ref["lost"] and new_kf == ref["new_kf"], f
+        n_new += new_kf
+        if not lost:
+            dT = float(np.abs(res["T_WCf"].cpu().numpy() - ref["T_WCf"]).max())
+            dT_max = max(dT_max, dT)
+            assert dT <= 1e-4, (f, dT)
+        np.testing.assert_allclose(tr.kf.X_canon.cpu().numpy(), o.kf.X_canon, rtol=1e-4,
+                                   atol=1e-5)
+        np.testing.assert_allclose(tr.kf.C.cpu().numpy(), o.kf.C, rtol=1e-6)
+        assert float(tr.kf.N) == o.kf.N, f
+        if i % 20 == 0 and f + 1 < seq.n_frames:
+            # the same launches as the prefetch (concurrent tile hints): bit-identical
+            torch.cuda.synchronize()
+            got = pipe.feat[(i + 1) % 2]
+            assert torch.equal(got, model.encode(seq.img[f + 1], concurrent=True)[0]), f
+            assert not torch.equal(got, model.encode(seq.img[f], concurrent=True)[0]), f
+            n_feat += 1
+    summ = loop.summary()
+    assert summ["keyframes_added"] == n_new >= 2
+    ate = S.ate_vs_gt(summ["T_WC"][summ["log"][:, 2] == 0],
+                      seq.T_gt_np[1:][summ["log"][:, 2] == 0])
+    assert ate < 5e-2, ate
+    parity_log("test_c3_sequence_200_pipelined_vs_oracle", frames=bench.SEQ_FRAMES,
+               new_keyframes=n_new, idx_valid="bit-exact", max_abs_dT=dT_max, tol_dT=1e-4,
+               ate_m=ate, prefetched_features_checked=n_feat,
+               gn_iterations_hist=summ["gn_iterations_hist"])
