@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--prefetch-after", type=int, default=None,
                     help="start the next frame's encoder after this MonST3R decoder layer "
                          "(default: at the step's start)")
+    ap.add_argument("--defer-mast3r", type=int, default=None,
+                    help="1: run each frame's MASt3R DPT heads (outputs unread by the "
+                         "tracking) during the next frame's decoder; 0: at the frame's end")
     ap.add_argument("--timeline-out", default=None,
                     help="write one replayed step's per-launch GEMM / attention timeline (JSON)")
     ap.add_argument("--no-timeline", action="store_true",
@@ -210,20 +213,21 @@ def _union_ticks(iv):
     return tot
 
 
-def step_timeline(loop, dev, replays=24, out_path=None):
-    """The captured C3 step timed launch by launch AS IT RUNS (no tracer): the two parity
-    graphs are captured again with the library's step timeline armed (m3s_timeline_set), so
-    every GEMM / attention launch in them carries a slot that its blocks stamp with
-    s_memrealtime (earliest block start, latest wave end; 10 ns ticks), then replayed
-    frame after frame from the INIT keyframe with HIP events around each replay.  Per step:
-    the launches' own durations, the union of the GEMM (attention) intervals — chip time
-    during which at least one GEMM runs, concurrent chains counted once — and the
-    algorithmic FLOPs of the step's own launch set.  The roofline's `achieved` is
-    GEMM FLOPs per step ÷ the GEMM union time per step."""
+def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
+    """The captured C3 step timed launch by launch AS IT RUNS (no tracer): `pairs` pairs of
+    the two parity graphs are captured again with the library's step timeline armed
+    (m3s_timeline_set), so every GEMM / attention launch in them carries its own slot that
+    its blocks stamp with s_memrealtime (earliest block start, latest wave end; 10 ns
+    ticks).  Each round replays the 2·pairs graphs back to back — as the timed loop replays
+    its two — frame after frame, with HIP events between replays; the first replay of a
+    round (cold start) is dropped.  Per step: the launches' own durations, the union of the
+    GEMM (attention) intervals — chip time during which at least one GEMM runs, concurrent
+    chains counted once — and the algorithmic FLOPs of the step's own launch set.  The
+    roofline's `achieved` is GEMM FLOPs per step ÷ the GEMM union time per step."""
     import numpy as np
     from monst3r_slam_amd import _lib
     lib, P = _lib.load(), _lib.ptr
-    cap = 2048
+    cap = 4096
     buf = torch.empty((cap, 64, 2), dtype=torch.int64, device=dev)
 
     def cap_tl(k):
@@ -240,7 +244,7 @@ def step_timeline(loop, dev, replays=24, out_path=None):
 
     _lib.check(lib.m3s_timeline_set(P(buf), cap), "timeline_set")
     try:
-        graphs = [cap_tl(0), cap_tl(1)]
+        graphs = [cap_tl(i % 2) for i in range(2 * pairs)]
         n = int(lib.m3s_timeline_count())
         kinds = np.zeros(cap, np.int32)
         flops = np.zeros(cap, np.float64)
@@ -255,41 +259,44 @@ def step_timeline(loop, dev, replays=24, out_path=None):
     torch.cuda.synchronize(dev)
     rows = []
     keep = None
-    for i in range(replays):
-        g, a, b = graphs[i % 2]
+    st = torch.cuda.current_stream(dev)
+    for rd in range(rounds):
         buf[..., 0] = -1                  # UINT64_MAX: atomic-min target
         buf[..., 1] = 0
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        st = torch.cuda.current_stream(dev)
-        e0.record(st)
-        g.replay()
-        e1.record(st)
-        e1.synchronize()
-        step_ms = e0.elapsed_time(e1)
-        tb = buf[a:b].cpu().numpy()       # [launches, 64, 2]; unused pairs stay (-1, 0)
-        st_ = np.where(tb[..., 0] > 0, tb[..., 0], np.iinfo(np.int64).max).min(1)
-        t = np.stack([st_, tb[..., 1].max(1)], 1)
-        ok = (t[:, 1] > 0) & (t[:, 0] < np.iinfo(np.int64).max)
-        if not ok.all():
-            raise RuntimeError(f"step timeline: {int((~ok).sum())} launches left no stamp")
-        k, fl = kinds[a:b], flops[a:b]
-        row = {"step_ms": step_ms, "span_ms": (t[:, 1].max() - t[:, 0].min()) * 1e-5}
-        for name, code in (("gemm", 1), ("attn", 2)):
-            sel = k == code
-            iv = [(int(s), int(e)) for s, e in t[sel]]
-            row[name] = {"launches": int(sel.sum()), "gflop": float(fl[sel].sum()) / 1e9,
-                         "sum_ms": float((t[sel, 1] - t[sel, 0]).sum()) * 1e-5,
-                         "union_ms": _union_ticks(iv) * 1e-5}
-        row["busy_union_ms"] = _union_ticks([(int(s), int(e)) for s, e in t]) * 1e-5
-        rows.append(row)
-        if i == replays - 2:
-            keep = (t.copy(), k.copy(), fl.copy(), dims[a:b].copy(), step_ms)
-    warm = rows[2:]                       # first replays: cold caches after reset
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(graphs) + 1)]
+        evs[0].record(st)
+        for i, (g, _, _) in enumerate(graphs):
+            g.replay()
+            evs[i + 1].record(st)
+        evs[-1].synchronize()
+        tball = buf.cpu().numpy()
+        for i, (g, a, b) in enumerate(graphs):
+            if i == 0:
+                continue                  # cold start after the reset / host sync
+            step_ms = evs[i].elapsed_time(evs[i + 1])
+            tb = tball[a:b]               # [launches, 64, 2]; unused pairs stay (-1, 0)
+            st_ = np.where(tb[..., 0] > 0, tb[..., 0], np.iinfo(np.int64).max).min(1)
+            t = np.stack([st_, tb[..., 1].max(1)], 1)
+            ok = (t[:, 1] > 0) & (t[:, 0] < np.iinfo(np.int64).max)
+            if not ok.all():
+                raise RuntimeError(f"step timeline: {int((~ok).sum())} launches left no stamp")
+            k, fl = kinds[a:b], flops[a:b]
+            row = {"step_ms": step_ms, "span_ms": (t[:, 1].max() - t[:, 0].min()) * 1e-5}
+            for name, code in (("gemm", 1), ("attn", 2)):
+                sel = k == code
+                iv = [(int(s_), int(e)) for s_, e in t[sel]]
+                row[name] = {"launches": int(sel.sum()), "gflop": float(fl[sel].sum()) / 1e9,
+                             "sum_ms": float((t[sel, 1] - t[sel, 0]).sum()) * 1e-5,
+                             "union_ms": _union_ticks(iv) * 1e-5}
+            row["busy_union_ms"] = _union_ticks([(int(s_), int(e)) for s_, e in t]) * 1e-5
+            rows.append(row)
+            if rd == rounds - 1 and i == len(graphs) - 2:
+                keep = (t.copy(), k.copy(), fl.copy(), dims[a:b].copy(), step_ms)
 
     def med(f):
-        return float(np.median([f(r) for r in warm]))
+        return float(np.median([f(r) for r in rows]))
 
-    res = {"replays": len(warm), "step_ms": med(lambda r: r["step_ms"]),
+    res = {"replays": len(rows), "step_ms": med(lambda r: r["step_ms"]),
            "span_ms": med(lambda r: r["span_ms"]),
            "gemm_or_attn_union_ms": med(lambda r: r["busy_union_ms"])}
     for name in ("gemm", "attn"):
@@ -306,8 +313,8 @@ def step_timeline(loop, dev, replays=24, out_path=None):
         t0 = int(t[:, 0].min())
         js = {"step_ms": sms, "tick_ns": 10, "launches": [
             {"kind": {1: "gemm", 2: "attn"}[int(kk)], "dims": [int(x) for x in d],
-             "gflop": float(f) / 1e9, "start_us": (int(s) - t0) * 1e-2,
-             "end_us": (int(e) - t0) * 1e-2} for (s, e), kk, f, d in zip(t, k, fl, dm)]}
+             "gflop": float(f) / 1e9, "start_us": (int(s_) - t0) * 1e-2,
+             "end_us": (int(e) - t0) * 1e-2} for (s_, e), kk, f, d in zip(t, k, fl, dm)]}
         with open(out_path, "w") as fh:
             json.dump(js, fh)
     del graphs
@@ -823,6 +830,8 @@ def main():
     tr.split_heads = not args.no_split_heads
     if args.prefetch_after is not None:
         model.layer_event_at = args.prefetch_after
+    if args.defer_mast3r is not None:
+        model.defer_mast3r = bool(args.defer_mast3r)
 
     from monst3r_slam_amd import sequence as S
     from monst3r_slam_amd.frontend import FramePipeline

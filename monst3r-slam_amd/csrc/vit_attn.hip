@@ -420,6 +420,301 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
     }
 }
 
+// Ping-pong variant of attn_kernel for 8-wave blocks (AW x KS = 8, KS = 2 or 4): the same
+// per-wave arithmetic in the same order (bit-identical results), scheduled so that each
+// SIMD's two waves — w and w + 4, i.e. the early and the late half of the key splits —
+// alternate between a matrix block and a vector block instead of running both in lockstep
+// behind one barrier per tile:
+//   M(j) = P·V of tile j-1 + S = K·Qᵀ of tile j   (16 MFMAs)
+//   V(j) = online softmax of tile j                (exp / max / sum / rescale: VALU)
+// Half-period h (one block barrier each): the early groups run M(h/2) / V((h-1)/2) for even /
+// odd h, the late groups the same one half-period later, so while one wave of a SIMD
+// keeps the matrix pipe busy its partner issues the softmax (cdna_hip_programming.md
+// 'Two waves per SIMD'; the lockstep loop serialised MFMA and softmax on every SIMD).
+// Ring: NST slots per key split; tile j+1 is issued at M(j) (3 slots) or V(j) (2 slots:
+// its slot held tile j-1, read by M(j)'s P·V), and retired (vmcnt 0) before M(j+1).
+template <int AW, int KS, bool TAILS>
+__global__ __launch_bounds__(AW * KS * 64, 1) void attn_pp_kernel(
+    const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
+    const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, void* __restrict__ o,
+    int64_t ldo, int64_t so_b, int o_fp8, int Sq, int Sk, int heads, float c_log2, int splits,
+    int tiles_per_split, float* __restrict__ part, int kv_xor, unsigned long long* tl) {
+  static_assert(AW * KS == 8 && (KS == 2 || KS == 4), "8 waves: w and w + 4 share a SIMD");
+  m3s_tl_begin(tl);
+  const M3sTlEnd tl_end{tl};
+  constexpr int GT = AW * 64;
+  constexpr int ACH = TILE_BYTES / 16 / GT;
+  constexpr int NST = KS == 2 ? 3 : 2;
+  static_assert((KS - 1) * AW * RED_FLOATS * 4 <= KS * NST * STAGE_BYTES, "merge space");
+  __shared__ __attribute__((aligned(16))) char lds[KS * NST * STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wall = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wid = wall % AW;
+  const int ksp = wall / AW;
+  const bool late = ksp >= KS / 2;    // waves 4..7
+  const int gtid = tid - ksp * GT;
+  char* const ring = lds + ksp * NST * STAGE_BYTES;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqt = (Sq + AW * QT - 1) / (AW * QT);
+  const int total = gridDim.x, orig = blockIdx.x;
+  int lin = orig;
+  if (total >= 16) {
+    const int qq = total / 8, rr = total % 8, xcd = orig % 8;
+    lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  }
+  const int qt = lin % nqt;
+  const int hz = lin / nqt;
+  const int h = hz % heads;
+  const int bz = hz / heads;
+  const int q0 = qt * (AW * QT) + wid * QT;
+  const int64_t b = bz / splits;
+  const int sp = bz - (int)b * splits;
+  const bf16_t* Q = q + b * sq_b + h * HD;
+  const int qrow = q0 + r;
+  bf16x8 qf[4];
+  const bf16x8 zero8 = {};
+#pragma unroll
+  for (int ks = 0; ks < 4; ks++)
+    qf[ks] = qrow < Sq ? load8(Q + (int64_t)qrow * ldq + ks * 16 + 8 * hh) : zero8;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int ks = 0; ks < 4; ks++) asm volatile("" : "+v"(qf[ks]));
+
+  const __amdgpu_buffer_rsrc_t rK = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(k + (b ^ kv_xor) * skv_b + h * HD), (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rV = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(v + (b ^ kv_xor) * skv_b + h * HD), (short)0, 0x7ffffff0, 0x00020000);
+  int k_row[ACH];
+  uint32_t k_off[ACH], v_off[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; i++) {
+    const int c = i * GT + gtid;
+    const int row = c >> 3, slot = c & 7;
+    k_row[i] = row;
+    k_off[i] = (uint32_t)(((int64_t)row * ldkv + (slot ^ k_swz(row)) * 8) * 2);
+    v_off[i] = (uint32_t)(((int64_t)row * ldkv + (slot ^ v_swz(row)) * 8) * 2);
+  }
+  const int nkt_all = (Sk + AKT - 1) / AKT;
+  const int kt0 = sp * tiles_per_split;
+  const int nkt = max(0, min(nkt_all - kt0, tiles_per_split));
+  const int nkt_g = nkt > ksp ? (nkt - ksp + KS - 1) / KS : 0;
+  const int nj = (nkt + KS - 1) / KS;
+  auto issue = [&](int j) {
+    const int kt = kt0 + ksp + KS * j;
+    char* sb = ring + (j % NST) * STAGE_BYTES;
+    const uint32_t t0 = (uint32_t)((int64_t)kt * AKT * ldkv * 2);
+#pragma unroll
+    for (int i = 0; i < ACH; i++) {
+      const bool ok = kt * AKT + k_row[i] < Sk;
+      glds16(rK, sb + (i * GT + wid * 64) * 16, ok ? t0 + k_off[i] : OOB);
+      glds16(rV, sb + TILE_BYTES + (i * GT + wid * 64) * 16, ok ? t0 + v_off[i] : OOB);
+    }
+  };
+
+  f32x16 oacc[2];
+#pragma unroll
+  for (int d = 0; d < 2; d++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) oacc[d][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gsel = (lane >> 4) & 1;
+  f32x16 s[2];                 // S^T of the tile between its M and V blocks
+  bf16x8 pf[4];                // P^T of the tile between its V block and the next M block
+
+  auto qk = [&](int j) {
+    const char* sK = ring + (j % NST) * STAGE_BYTES;
+#pragma unroll
+    for (int hs = 0; hs < 2; hs++) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) s[hs][i] = 0.f;
+      const int row = hs * 32 + r;
+#pragma unroll
+      for (int ks = 0; ks < 4; ks++) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(
+            sK + row * 128 + (((2 * ks + hh) ^ k_swz(row)) * 16));
+        s[hs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[hs], 0, 0, 0);
+      }
+    }
+  };
+  auto sm = [&](int j, auto tail_tag) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
+    const int kt = kt0 + ksp + KS * j;
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int hs = 0; hs < 2; hs++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        if constexpr (TAIL) {
+          const int key = kt * AKT + hs * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (key >= Sk) s[hs][i] = -INFINITY;
+        }
+        tmax = fmaxf(tmax, s[hs][i]);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m, tmax);
+    const float alpha = __builtin_amdgcn_exp2f((m - m_new) * c_log2);
+    const float mc = m_new * c_log2;
+    float rs = 0.f;
+#pragma unroll
+    for (int hs = 0; hs < 2; hs++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const float p = __builtin_amdgcn_exp2f(s[hs][i] * c_log2 - mc);
+        rs += p;
+        pf[2 * hs + (i >> 3)][i & 7] = f2bf(p);
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = m_new;
+#pragma unroll
+    for (int d = 0; d < 2; d++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) oacc[d][i] *= alpha;
+  };
+  auto pv = [&](int j) {
+    const char* sV = ring + (j % NST) * STAGE_BYTES + TILE_BYTES;
+    s16x4 vt[2][4][2];
+#pragma unroll
+    for (int d = 0; d < 2; d++) {
+      const int d0 = d * 32 + 16 * gsel + 4 * gp;
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+          const int rr = 16 * c + 8 * x + 4 * hh + gq;
+          vt[d][c][x] = tr_read(sV + rr * 128 + (((d0 >> 3) ^ v_swz(rr)) * 16) + (d0 & 7) * 2);
+        }
+    }
+#define M3S_VT(d) "+v"(vt[d][0][0]), "+v"(vt[d][0][1]), "+v"(vt[d][1][0]), "+v"(vt[d][1][1]), \
+                  "+v"(vt[d][2][0]), "+v"(vt[d][2][1]), "+v"(vt[d][3][0]), "+v"(vt[d][3][1])
+    asm volatile("s_waitcnt lgkmcnt(8)" : M3S_VT(0)::"memory");
+#pragma unroll
+    for (int d = 0; d < 2; d++) {
+      if (d == 1) asm volatile("s_waitcnt lgkmcnt(0)" : M3S_VT(1)::"memory");
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const bf16x4 lob = __builtin_bit_cast(bf16x4, vt[d][c][0]);
+        const bf16x4 hib = __builtin_bit_cast(bf16x4, vt[d][c][1]);
+        bf16x8 vf;
+        vf[0] = lob[0];
+        vf[1] = lob[1];
+        vf[2] = lob[2];
+        vf[3] = lob[3];
+        vf[4] = hib[0];
+        vf[5] = hib[1];
+        vf[6] = hib[2];
+        vf[7] = hib[3];
+        oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[c], oacc[d], 0, 0, 0);
+      }
+    }
+#undef M3S_VT
+  };
+  // the tile that may be partial is the globally last one: only its softmax masks
+  auto sm_any = [&](int j) {
+    if constexpr (TAILS) {
+      if ((kt0 + ksp + KS * j + 1) * AKT > Sk) {
+        sm(j, std::true_type{});
+        return;
+      }
+    }
+    sm(j, std::false_type{});
+  };
+
+  // prologue: tile 0 of every key split resident before the first half-period
+  if (nkt_g > 0) issue(0);
+  vm_wait<0>();
+  block_sync_lds();
+  const int HP = 2 * nj + 2;
+  for (int hp = 0; hp < HP; hp++) {
+    const int hl = late ? hp - 1 : hp;      // this group's own half-period index
+    if (hl >= 0) {
+      if ((hl & 1) == 0) {                  // M(j): P·V of j-1, then K·Qᵀ of j
+        const int j = hl >> 1;
+        if (NST == 3 && j + 1 < nkt_g) issue(j + 1);
+        if (j >= 1 && j - 1 < nkt_g) pv(j - 1);
+        if (j < nkt_g) qk(j);
+      } else {                              // V(j): softmax of j
+        const int j = hl >> 1;
+        if (NST == 2 && j + 1 < nkt_g) issue(j + 1);
+        if (j < nkt_g) sm_any(j);
+        vm_wait<0>();                       // tile j+1 resident before M(j+1)
+      }
+    }
+    block_sync_lds();
+  }
+  // merge the key splits (as attn_kernel: every ring read above is complete)
+  {
+    float* red = reinterpret_cast<float*>(lds);
+    if (ksp > 0) {
+      float* P = red + ((ksp - 1) * AW + wid) * RED_FLOATS;
+#pragma unroll
+      for (int i4 = 0; i4 < 8; i4++)
+        reinterpret_cast<float4*>(P)[i4 * 64 + lane] =
+            make_float4(oacc[i4 >> 2][(i4 & 3) * 4], oacc[i4 >> 2][(i4 & 3) * 4 + 1],
+                        oacc[i4 >> 2][(i4 & 3) * 4 + 2], oacc[i4 >> 2][(i4 & 3) * 4 + 3]);
+      reinterpret_cast<float2*>(P + 2048)[lane] = make_float2(m, l);
+    }
+    block_sync_lds();
+    if (ksp > 0) return;
+#pragma unroll
+    for (int s2 = 1; s2 < KS; s2++) {
+      const float* P = red + ((s2 - 1) * AW + wid) * RED_FLOATS;
+      const float2 ml = reinterpret_cast<const float2*>(P + 2048)[lane];
+      const float M = fmaxf(m, ml.x);
+      const float a0 = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - M) * c_log2);
+      const float a1 = ml.x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((ml.x - M) * c_log2);
+#pragma unroll
+      for (int i4 = 0; i4 < 8; i4++) {
+        const float4 w = reinterpret_cast<const float4*>(P)[i4 * 64 + lane];
+        const int d = i4 >> 2, e = (i4 & 3) * 4;
+        oacc[d][e] = oacc[d][e] * a0 + w.x * a1;
+        oacc[d][e + 1] = oacc[d][e + 1] * a0 + w.y * a1;
+        oacc[d][e + 2] = oacc[d][e + 2] * a0 + w.z * a1;
+        oacc[d][e + 3] = oacc[d][e + 3] * a0 + w.w * a1;
+      }
+      l = l * a0 + ml.y * a1;
+      m = M;
+    }
+  }
+  if (qrow >= Sq) return;
+  if (part) {
+    const int64_t nb = (int64_t)total / ((int64_t)nqt * heads * splits);
+    float* P = part + ((((int64_t)sp * nb + b) * heads + h) * Sq + qrow) * PART_LD;
+#pragma unroll
+    for (int d = 0; d < 2; d++)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; g4++)
+        *reinterpret_cast<float4*>(P + d * 32 + 8 * g4 + 4 * hh) =
+            make_float4(oacc[d][4 * g4], oacc[d][4 * g4 + 1], oacc[d][4 * g4 + 2],
+                        oacc[d][4 * g4 + 3]);
+    if (hh == 0) *reinterpret_cast<float2*>(P + HD) = make_float2(m, l);
+    return;
+  }
+  const float inv_l = 1.0f / l;
+  if (o_fp8) {
+    uint8_t* O8 = reinterpret_cast<uint8_t*>(o) + b * so_b + (int64_t)qrow * ldo + h * HD;
+#pragma unroll
+    for (int d = 0; d < 2; d++)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; g4++)
+        *reinterpret_cast<uint32_t*>(O8 + d * 32 + 8 * g4 + 4 * hh) =
+            pack4_fp8(oacc[d][4 * g4] * inv_l, oacc[d][4 * g4 + 1] * inv_l,
+                      oacc[d][4 * g4 + 2] * inv_l, oacc[d][4 * g4 + 3] * inv_l);
+    return;
+  }
+  bf16_t* O = reinterpret_cast<bf16_t*>(o) + b * so_b + (int64_t)qrow * ldo + h * HD;
+#pragma unroll
+  for (int d = 0; d < 2; d++)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; g4++) {
+      bf16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; j++) w[j] = f2bf(oacc[d][4 * g4 + j] * inv_l);
+      *reinterpret_cast<bf16x4*>(O + d * 32 + 8 * g4 + 4 * hh) = w;
+    }
+}
+
 // Merge the key splits: M = max m_s, O = sum_s O_s 2^((m_s - M) c) / sum_s l_s 2^((m_s - M) c).
 // One thread per (b, h, q, 8 head dims).
 __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part,
@@ -538,7 +833,22 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   hipStream_t s = m3s_stream(stream);
   unsigned long long* tl =
       m3s_timeline_take(M3S_TL_ATTN, 4.0 * sq * sk * HD * heads * batch, sq, sk, heads, batch);
+  // ping-pong kernel: opt-in (M3S_ATTN_PP=1) — bit-identical but measured slower (encoder
+  // 10.1 → 11.8 us, decoder 13.4 → 16.1 us replayed; C3 223 → 217 frames/s)
+  const char* pp_env = getenv("M3S_ATTN_PP");
+  const bool pp = pp_env && atoi(pp_env) != 0;
 #define M3S_ATTN_LAUNCH2(AWV, KSV, TL)                                                       \
+  if constexpr (AWV * KSV == 8)                                                              \
+    if (pp) {                                                                                \
+      hipLaunchKernelGGL((attn_pp_kernel<AWV, KSV, TL>),                                     \
+                         dim3((unsigned)(m3s_div_up(sq, AWV * QT) * heads * batch * splits)),\
+                         dim3(AWV * KSV * 64), 0, s,                                         \
+                         reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,               \
+                         reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
+                         ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,      \
+                         (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl);  \
+      break;                                                                                 \
+    }                                                                                        \
   hipLaunchKernelGGL((attn_kernel<AWV, KSV, TL>),                                           \
                      dim3((unsigned)(m3s_div_up(sq, AWV * QT) * heads * batch * splits)),    \
                      dim3(AWV * KSV * 64), 0, s,                                             \
@@ -548,8 +858,11 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
                      (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl)
 #define M3S_ATTN_LAUNCH(AWV, KSV)                                                            \
   do {                                                                                       \
-    if (sk % AKT) M3S_ATTN_LAUNCH2(AWV, KSV, true);                                          \
-    else M3S_ATTN_LAUNCH2(AWV, KSV, false);                                                  \
+    if (sk % AKT) {                                                                          \
+      M3S_ATTN_LAUNCH2(AWV, KSV, true);                                                      \
+    } else {                                                                                 \
+      M3S_ATTN_LAUNCH2(AWV, KSV, false);                                                     \
+    }                                                                                        \
   } while (0)
   if (ks == 4) M3S_ATTN_LAUNCH(2, 4);
   else if (ks == 2 && aw == 2) M3S_ATTN_LAUNCH(2, 2);

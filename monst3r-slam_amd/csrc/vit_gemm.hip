@@ -50,6 +50,7 @@ extern template int launch<256, 128, 64, 4, 2, 3, 1, true>(Args&, int, hipStream
 extern template int launch<128, 128, 64, 2, 2, 2, 2, true>(Args&, int, hipStream_t);
 extern template int launch<128, 128, 64, 2, 2, 3, 1, true>(Args&, int, hipStream_t);
 extern template int launch<128, 128, 64, 4, 2, 3, 1>(Args&, int, hipStream_t);
+extern template int launch<256, 256, 64, 2, 4, 2, 1>(Args&, int, hipStream_t);
 }  // namespace m3s_gemm
 #endif
 
@@ -258,7 +259,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
         ((tiles96 >= 160 && tiles96 <= 256) || tiles96 % 256 == 0))
       cfg = T96;
   }
-  if (cfg < 1 || cfg > 13 || cfg == 4 || cfg == 5) cfg = T128;
+  if (cfg < 1 || cfg > 14 || cfg == 4 || cfg == 5) cfg = T128;
   if (conv && (cfg == T64D || cfg == T128D)) cfg = T64;
   if (conv && d->Cin % 64 != 0) cfg = T128K32;  // tap-uniform K-tiles need Cin % BK == 0
   if (!conv && cfg == T128K32) cfg = T128;
@@ -279,7 +280,8 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   }
   // fused split-K: 128^2 GEMM tiles or 64x128 GEMM / conv tiles, a workspace for the f32
   // partials and one zeroed counter per (batch, tile)
-  const int bm = (cfg == T64 || cfg == T64D) ? 64 : (cfg == T256 || cfg == T256W8) ? 256 : 128;
+  const int bm = (cfg == T64 || cfg == T64D) ? 64
+                 : (cfg == T256 || cfg == T256W8 || cfg == T256SQ) ? 256 : 128;
   const int64_t tiles_cfg = (int64_t)((d->M + bm - 1) / bm) * ((d->N + 127) / 128) * d->batch;
   const bool split_cfg = (!conv && (cfg == T128 || cfg == T128O2 || cfg == T64 || cfg == T64D ||
                                     cfg == T128D || cfg == T128W8 || cfg == T256 ||
@@ -317,6 +319,13 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     case T128D: return launch<128, 128, 64, 2, 2, 4, 1>(a, d->batch, s);
     case T128W8: return launch<128, 128, 64, 4, 2, 3, 1>(a, d->batch, s);
     case T256W8: return launch<256, 128, 64, 4, 2, 3, 1>(a, d->batch, s);
+    // 256x256: unsplit only (two-pass epilogue), no DPT tail (128-channel rows); the RoPE
+    // and the run-time-flag epilogues spill at 256 VGPRs (-Rpass-analysis) → 256x128
+    case T256SQ:
+      if (a.splits > 1 || !a.vec ||
+          (d->flags & (M3S_EPI_DPT_OUT | M3S_EPI_ROPE | M3S_EPI_CONVT | M3S_EPI_OUT_FP8)))
+        return launch<256, 128, 64, 4, 2, 3, 1>(a, d->batch, s);
+      return launch<256, 256, 64, 2, 4, 2, 1>(a, d->batch, s);
     default: return launch<64, 128, 64, 2, 2, 3, 2>(a, d->batch, s);
   }
 }

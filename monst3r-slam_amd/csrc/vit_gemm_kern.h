@@ -303,6 +303,10 @@ __device__ __forceinline__ void epi_one(const Epi& e, float v, float p, int m, i
 // ---------------------------------------------------------------------------------------
 template <int BM, int BN, int BK, int STAGES, int NTH = 256>
 struct Cfg {
+  // the f32 epilogue tile of a 256x256 block (266 KB) exceeds the 160 KB LDS: it is
+  // written and stored in two passes of 128 rows
+  static constexpr int PASSES = (BM * (BN + 4) * 4 > 160 * 1024) ? 2 : 1;
+  static constexpr int EROWS = BM / PASSES;
   static constexpr int CPR = BK / 8;                 // 16-B chunks per row
   static constexpr int RPB = 256 / (BK * 2);         // rows per 256-B LDS bank row
   static constexpr int A_CH = BM * CPR / NTH;        // DMA chunks per thread per K-tile
@@ -311,7 +315,7 @@ struct Cfg {
   static constexpr int A_BYTES = BM * BK * 2;
   static constexpr int ST_BYTES = (BM + BN) * BK * 2;
   static constexpr int CST = BN + 4;                 // epilogue f32 row stride
-  static constexpr int EPI_BYTES = BM * CST * 4;
+  static constexpr int EPI_BYTES = EROWS * CST * 4;
   static constexpr int LDS_BYTES = STAGES * ST_BYTES > EPI_BYTES ? STAGES * ST_BYTES : EPI_BYTES;
 };
 
@@ -712,7 +716,9 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
 
   // ---- epilogue through LDS: f32 tile [BM][CST] ----
   constexpr int VPR = BN / 8;                 // 8-column vectors per row
-  constexpr int NV = BM * VPR / NT;           // vectors per thread
+  constexpr int PASSES = C::PASSES, EROWS = C::EROWS;
+  static_assert(PASSES == 1 || (!SPLIT && WM == PASSES), "two-pass epilogue: unsplit, one wave row per pass");
+  constexpr int NV = EROWS * VPR / NT;        // vectors per thread (per pass)
   constexpr int RSTEP = NT / VPR;             // rows between one thread's vectors
   static_assert(NT % VPR == 0, "epilogue layout");
   // Vector path: a thread owns columns [n, n+8) of rows r0 + v*RSTEP.  Its bias and, per
@@ -732,19 +738,19 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
   // combines the statistics of row v once, the others read it by lane shuffle
   float ln_mu = 0.f, ln_rs = 0.f;
   static_assert(NV <= 16, "one row per lane of the group");
+  int rb = 0;                                 // first tile row of the epilogue pass
   auto ln_setup = [&]() {
     if ((fl & M3S_EPI_LN_FOLD) && (lane & 15) < NV)
-      ln_row_stats(a, g ^ a.a_xor, min(m0 + er0 + (lane & 15) * RSTEP, a.M - 1), a.K >> 7,
+      ln_row_stats(a, g ^ a.a_xor, min(m0 + rb + er0 + (lane & 15) * RSTEP, a.M - 1), a.K >> 7,
                    ln_mu, ln_rs);
   };
-  if (!SPLIT) ln_setup();
   Epi e = make_epi(a, g);
   e.flags = fl;
   const bool e_rope = (fl & M3S_EPI_ROPE) && en < a.rope_cols;
   auto e_prefetch = [&](int v0) {
 #pragma unroll
     for (int u = 0; u < EG; u++) {
-      const int m = min(m0 + er0 + (v0 + u) * RSTEP, a.M - 1);  // rows ≥ M are not stored
+      const int m = min(m0 + rb + er0 + (v0 + u) * RSTEP, a.M - 1);  // rows ≥ M are not stored
       if (fl & M3S_EPI_LN_FOLD) {  // row v0 + u's statistics, held by lane v0 + u of the row group
         const int src = (lane & ~15) | (v0 + u);
         e_mu[u] = __shfl(ln_mu, src, 64);
@@ -771,7 +777,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
       }
     }
   };
-  auto epi_setup = [&]() {
+  auto epi_setup = [&](bool prefetch_rows) {
     if (!vec_path) return;
     int co;
     (void)out_offset(e, m0, en, co);
@@ -796,28 +802,37 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
             *reinterpret_cast<const float4*>(c1 + (en ^ 16) + 4);
       }
     }
-    e_prefetch(0);
+    if (prefetch_rows) e_prefetch(0);
   };
-  if (!SPLIT) epi_setup();   // split-K: only the tile's last split needs the operands
+  if (!SPLIT) epi_setup(false);   // split-K: only the tile's last split needs the operands
+  float* cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int pass = 0; pass < PASSES; pass++) {
+  rb = pass * EROWS;
+  if (!SPLIT) {
+    ln_setup();
+    if (vec_path) e_prefetch(0);
+  }
   M3S_T(t_e0);
   block_sync_lds();
   M3S_T(t_e1);
-  float* cs = reinterpret_cast<float*>(lds);
 #pragma unroll
   for (int i = 0; i < TM; i++)
 #pragma unroll
     for (int j = 0; j < TN; j++)
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        cs[row * C::CST + wn * (BN / WN) + j * 32 + fr] = acc[i][j][r];
+        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh - rb;
+        if (PASSES == 1 || wm == pass)
+          cs[row * C::CST + wn * (BN / WN) + j * 32 + fr] = acc[i][j][r];
       }
   block_sync_lds();
   M3S_T(t_e2);
 
   if constexpr (EPI >= 0 && (EPI & M3S_EPI_DPT_OUT) != 0) {
     // fused DPT tail: one pixel (row) per thread, all BN = 128 channels in the LDS tile
-    static_assert(BN == 128 && !SPLIT, "DPT_OUT needs the full 128-channel row in one tile");
+    static_assert(BN == 128 && !SPLIT && PASSES == 1,
+                  "DPT_OUT needs the full 128-channel row in one tile");
     const int gw = a.wmod > 0 ? g % a.wmod : g;
     const float* w4 = a.dpt_w4 + (int64_t)gw * 512;
     const float* b4 = a.dpt_b4 + (int64_t)gw * 4;
@@ -900,7 +915,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     ln_setup();
-    epi_setup();
+    epi_setup(true);
     const float* P0 = a.ws + (int64_t)g * a.splits * per_b;
     // slab by slab, all of this thread's vectors of a slab in flight at once (one L2
     // round trip per slab instead of one per vector); the sum stays in split order
@@ -971,7 +986,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
       }
 #pragma unroll
       for (int u = 0; u < EG; u++) {
-        const int m = m0 + er0 + (v0 + u) * RSTEP;
+        const int m = m0 + rb + er0 + (v0 + u) * RSTEP;
         if (m >= a.M) continue;
         float* x = xv[u];
         if (fl & M3S_EPI_LN_FOLD) {  // LN(x) W^T + b = rstd (acc - mean c1) + c2
@@ -1033,14 +1048,17 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
     for (int v = 0; v < NV; v++) {
       const int idx = v * NT + tid;
       const int row = idx / VPR, c = (idx % VPR) * 8;
-      const int m = m0 + row, n = n0 + c;
+      const int m = m0 + rb + row, n = n0 + c;
       if (m >= a.M || n >= a.N) continue;
       const float* src = cs + row * C::CST + c;
       const float* psrc = cs + row * C::CST + (c ^ 16);
       for (int t = 0; t < 8 && n + t < a.N; t++) epi_one(e, src[t], rope ? psrc[t] : 0.f, m, n + t);
     }
   }
-  M3S_STAMP_OUT();
+  if (pass + 1 == PASSES) {
+    M3S_STAMP_OUT();
+  }
+  }  // pass (the next pass's first barrier orders these LDS reads before its writes)
 }
 
 // Unfused split-K: sum the partials (fixed order) and apply the epilogue; 8 columns per
@@ -1109,8 +1127,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
 // FLOP/clk, i.e. fetch / MFMA cycles ≈ 64·(BM + BN) / (BM·BN): 1.5 for 64x128, 1.0 for
 // 128², 0.75 here — the first tile whose K-loop the matrix pipe can pace.  For the M = 768
 // batched decoder GEMMs it trades 2x fewer blocks for that; T256 is the 4-wave form.
+// T256SQ: 256x256 with 8 waves (2 x 4, each 128x64), a 2-stage ring of 64 KB K-tiles and
+// the epilogue in two 128-row passes (the f32 tile would need 266 KB of LDS): fetch / MFMA
+// cycles ≈ 0.5, the shape of cdna_hip_programming.md §5's 256² template — the most MFMA
+// work per staged byte, for launches that can spend fewer CUs (large-M convs, the local-
+// feature MLP, GEMMs sharing the chip with other chains)
 enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7, T96 = 8, T96O2 = 9,
-               T64D = 10, T128D = 11, T128W8 = 12, T256W8 = 13 };
+               T64D = 10, T128D = 11, T128W8 = 12, T256W8 = 13, T256SQ = 14 };
 
 // Epilogue flag sets compiled as straight-line variants (8-wide vector path), per mode:
 //   GEMM: bf16 out, +RoPE, +GELU, f32 residual → f32, f32 out;  conv: bf16 out, +bf16
@@ -1180,9 +1203,10 @@ void launch_main(Args& a, dim3 grid, hipStream_t s) {
         return;
       // LayerNorm fold (the ViT blocks' norm → projection pairs): consumers qkv / q / kv
       // (+RoPE) and fc1 (+GELU), producers the residual GEMMs and the embeddings
-      if constexpr (BN == 128 && BK == 64 && (BM == 64 || BM == 96 || BM == 128 || BM == 256) &&
-                    OCC <= 2 && (BM != 256 || OCC == 1) &&
-                    (BM != 96 || OCC == 1)) {
+      if constexpr (BK == 64 && OCC <= 2 && (BM != 96 || OCC == 1) &&
+                    ((BN == 128 && (BM == 64 || BM == 96 || BM == 128 || BM == 256) &&
+                      (BM != 256 || OCC == 1)) ||
+                     (BN == 256 && BM == 256 && OCC == 1))) {
         constexpr int LF = M3S_EPI_LN_FOLD, LS = M3S_EPI_LN_STATS;
         if (try_epi_b<BM, BN, BK, WM, WN, STAGES, OCC, MODE, LF | M3S_EPI_ROPE, SP>(a, grid, s,
                                                                                      key))

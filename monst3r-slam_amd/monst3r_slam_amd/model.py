@@ -448,6 +448,8 @@ class PairModel:
         # schedule knob: an event recorded on the MonST3R decoder chain after layer
         # `layer_event_at` (None: no event) — the pipelined loop starts the next frame's
         # encoder behind it instead of at the step's start (M3S_PREFETCH_AFTER)
+        # the MASt3R DPT heads deferred into the next pair (SequenceLoop; M3S_DEFER_MAST3R)
+        self.defer_mast3r = os.environ.get("M3S_DEFER_MAST3R", "0") == "1"
         e = os.environ.get("M3S_PREFETCH_AFTER")
         self.layer_event_at = int(e) if e not in (None, "") else None
         self.layer_event = None
@@ -457,6 +459,12 @@ class PairModel:
         self._wbase = 0       # first head-weight stack of that set
         self._wm = 4
         self._ev_heads = None
+        # deferred MASt3R DPT heads (pair(defer_parity=k)): their pts3d / conf are never
+        # read by the tracking (monst3r_utils.py:290), so frame t's run during frame t+1's
+        # decoder on their own stream, from hooks kept in a parity double buffer
+        self._hsuf = ""
+        self.side_defer = torch.cuda.Stream(device)
+        self._ev_defer = None
 
     def set_fp8(self, on=True):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
@@ -499,6 +507,11 @@ class PairModel:
             torch.cuda.current_stream(self.dev).wait_event(ev)
 
     # ---- buffers ----
+    def _hk(self, name):
+        """Decoder hook buffer key: parity-suffixed while pair(defer_parity=...) runs, so the
+        previous frame's hooks survive for its deferred MASt3R heads."""
+        return name + self._hsuf
+
     def _buf(self, key, shape, dtype):
         """Persistent scratch per (name, shape, dtype): a buffer is never freed or
         reallocated, so HIP graphs captured over it stay valid when other batch sizes run."""
@@ -621,7 +634,7 @@ class PairModel:
         wm = 2 * models
         self._wm = wm
         Z = wm * G
-        h0 = self._buf("h0", (Z, S, E), BF16)
+        h0 = self._buf(self._hk("h0"), (Z, S, E), BF16)
         # h0[(g·models + m)·2 + side] = (feat1 | feat2)[g] for every model m: one row copy
         # per side (in-tree kernel), feat_* [G,S,E] contiguous
         fb = S * E * 2
@@ -651,7 +664,7 @@ class PairModel:
             with torch.cuda.stream(side):
                 self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm, None, part=1)
             main.wait_stream(side)
-            h12 = self._buf("h12", (Z, S, D), BF16)
+            h12 = self._buf(self._hk("h12"), (Z, S, D), BF16)
             o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
             hooks["h12"] = h12
             return hooks
@@ -724,12 +737,12 @@ class PairModel:
             o.gemm(hid, w, x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D, bias=P["fc2_b"],
                    sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
             if (i + 1) in hk:
-                hb = self._buf(f"h{i + 1}", (Z, S, D), BF16)
+                hb = self._buf(self._hk(f"h{i + 1}"), (Z, S, D), BF16)
                 hb.copy_(x)
                 hooks[f"h{i + 1}"] = hb
                 if on_hook is not None:
                     on_hook(f"h{i + 1}", hooks)
-        h12 = self._buf("h12", (Z, S, D), BF16)
+        h12 = self._buf(self._hk("h12"), (Z, S, D), BF16)
         o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
         hooks["h12"] = h12
         if on_hook is not None:
@@ -751,7 +764,7 @@ class PairModel:
         att = self._buf("dec_att", (Z, S, D), BF16)
         hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), BF16)
         hooks = {"h0": h0}
-        hook_bufs = {k: self._buf(f"h{k}", (Z, S, D), BF16) for k in a.hooks[1:3]}
+        hook_bufs = {k: self._buf(self._hk(f"h{k}"), (Z, S, D), BF16) for k in a.hooks[1:3]}
         sl = None
         if part is not None:
             # one model's two problems (decode_multi's per-model split): every buffer, the
@@ -800,7 +813,7 @@ class PairModel:
             xc = xb
             if (i + 1) in hk:
                 xc = hook_bufs[i + 1]
-                hooks[f"h{i + 1}"] = self._buf(f"h{i + 1}", (2 * wm if sl is not None else Z,
+                hooks[f"h{i + 1}"] = self._buf(self._hk(f"h{i + 1}"), (2 * wm if sl is not None else Z,
                                                              S, D), BF16)
             o.gemm(hid, P["fc2_w"], x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D,
                    bias=P["fc2_b"], sBias=D, wmod=wm, tile=tl("fc2"),
@@ -809,7 +822,7 @@ class PairModel:
                 on_hook(f"h{i + 1}", hooks)
         if sl is not None:
             return hooks
-        h12 = self._buf("h12", (Z, S, D), BF16)
+        h12 = self._buf(self._hk("h12"), (Z, S, D), BF16)
         o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
         hooks["h12"] = h12
         if on_hook is not None:
@@ -897,7 +910,7 @@ class PairModel:
         t = self.w.h[key]
         return t[self._wbase:] if self._wbase else t
 
-    def heads(self, hooks, gh, gw, H, W, models=2, split=False, R=None):
+    def heads(self, hooks, gh, gw, H, W, models=2, split=False, R=None, mast3r_dpt=True):
         """DPT heads of all 2*models*G problems (z = (g*models + model)*2 + side, head weights
         z % (2*models)) + MASt3R local features of the model-1 problems (models=2 only).
         split (one pair, G = 1): the MASt3R DPT heads — whose pts3d/conf the tracking never
@@ -940,7 +953,7 @@ class PairModel:
                 try:
                     # M3S_ABLATE_MAST3R_DPT=1: diagnostic ablation only (tools/step_ablation):
                     # the discarded MASt3R pts3d / conf heads are not issued
-                    if os.environ.get("M3S_ABLATE_MAST3R_DPT") != "1":
+                    if mast3r_dpt and os.environ.get("M3S_ABLATE_MAST3R_DPT") != "1":
                         self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4],
                                   R=None if R is None else [r[2:4] for r in R])
                 finally:
@@ -969,6 +982,9 @@ class PairModel:
         if self._ev_heads is not None:
             torch.cuda.current_stream(self.dev).wait_event(self._ev_heads)
             self._ev_heads = None
+        if self._ev_defer is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self._ev_defer)
+            self._ev_defer = None
 
     def _rn_bufs_early(self, gh, gw, Z):
         saved, self._tag = self._tag, "early"
@@ -1086,7 +1102,35 @@ class PairModel:
 
 
     # ---- monst3r_asymmetric_inference ----
-    def pair(self, img_i, feat_j=None, img_j=None, feat_i=None, split_heads=False):
+    def _deferred_mast3r_heads(self, parity, gh, gw, H, W):
+        """The MASt3R DPT heads of the PREVIOUS pair (hooks of parity (parity + 1) % 2) on
+        side_defer, ordered only after the work enqueued before this pair: they overlap
+        this pair's decoder (the tracking chain does not read them)."""
+        a = self.a
+        S, E, D = gh * gw, a.enc_dim, a.dec_dim
+        prev = f"#{(parity + 1) % 2}"
+        hk = {}
+        for name, dim in (("h0", E), ("h6", D), ("h9", D), ("h12", D)):
+            key = (None, name + prev, (4, S, dim), BF16)
+            if key not in self._bufs:      # first use: defined contents, not stale memory
+                self._bufs[key] = torch.zeros((4, S, dim), dtype=BF16, device=self.dev)
+            hk[name] = self._bufs[key][2:4]
+        pts = self._buf("pts3d", (4, H, W, 3), F32)
+        conf = self._buf("conf", (4, H, W), F32)
+        sd = self.side_defer
+        sd.wait_stream(torch.cuda.current_stream(self.dev))
+        st = _tile_knob("M3S_SIDE_TILE", ("lf", "dpt"), self.side_tiles)
+        with torch.cuda.stream(sd):
+            self.ops.tile_default = st.get("dpt")
+            try:
+                self._dpt(hk, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4])
+            finally:
+                self.ops.tile_default = None
+            self._ev_defer = torch.cuda.Event()
+            self._ev_defer.record(sd)
+
+    def pair(self, img_i, feat_j=None, img_j=None, feat_i=None, split_heads=False,
+             defer_parity=None):
         """Frame i vs keyframe j (keyframe features cached as in monst3r_utils.py:262-269).
         feat_i: frame i's encoder features when already computed (the prefetched encode of
         frontend.FramePipeline); img_i then only gives the size.
@@ -1112,9 +1156,17 @@ class PairModel:
             # decoder layer; h6 / h9: mid-decoder), for all 4 problems at once
             R = self._rn_bufs_early(gh, gw, 4)
             on_hook = lambda name, hk: self._early_branch(name, hk, gh, gw, R)  # noqa: E731
-        hooks = self.decode(feat_i[0], feat_j.reshape(-1, a.enc_dim), pos, gh, gw,
-                            on_hook=on_hook)
-        pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W, split=split_heads, R=R)
+        defer = defer_parity is not None and split_heads and on_hook is None
+        if defer:
+            self._deferred_mast3r_heads(defer_parity, gh, gw, H, W)
+            self._hsuf = f"#{defer_parity % 2}"
+        try:
+            hooks = self.decode(feat_i[0], feat_j.reshape(-1, a.enc_dim), pos, gh, gw,
+                                on_hook=on_hook)
+        finally:
+            self._hsuf = ""
+        pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W, split=split_heads, R=R,
+                                                    mast3r_dpt=not defer)
         return dict(X=pts[0:2], C=conf[0:2], D16=desc16, D=desc, Q=dconf, feat_i=feat_i,
                     mast3r_X=pts[2:4], mast3r_C=conf[2:4])
 

@@ -243,7 +243,10 @@ class SequenceLoop:
             "seq_advance")
 
     def step(self, k=0, split_heads=None):
-        """One frame; k = the feature-buffer parity (pipelined)."""
+        """One frame; k = the feature-buffer parity (pipelined).  res["idx_f2k"] is the
+        tracker's persistent match buffer (the next frame's seed, written in place by the
+        matcher): after a keyframe replacement advance() has already reset it to the
+        identity, as tracker2.py:255-257 does before the next frame."""
         tr, m, pipe = self.tr, self.tr.model, self.pipe
         split = tr.split_heads if split_heads is None else split_heads
         main = torch.cuda.current_stream(self.dev)
@@ -251,21 +254,26 @@ class SequenceLoop:
         if m is not None:
             if pipe is not None:
                 feat_i = pipe.feat[k % 2]
+                dp = k % 2 if m.defer_mast3r else None
                 delay = m.layer_event_at is not None
                 if delay:   # the pair first: the encoder waits for its decoder layer event
                     m.layer_event = None
+                    ev_start = torch.cuda.Event()
+                    ev_start.record(main)          # main's work before this frame's pair
                     out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i,
-                                 split_heads=split)
-                pipe.side.wait_stream(main)
-                if delay and m.layer_event is not None:
-                    pipe.side.wait_event(m.layer_event)
+                                 split_heads=split, defer_parity=dp)
+                    pipe.side.wait_event(ev_start)
+                    if m.layer_event is not None:
+                        pipe.side.wait_event(m.layer_event)
+                else:
+                    pipe.side.wait_stream(main)
                 with torch.cuda.stream(pipe.side):
                     self.gather(self.img_next, 1)
                     self._gathered.record(pipe.side)
                     m.encode(self.img_next, out=pipe.feat[(k + 1) % 2], concurrent=True)
                 if not delay:
                     out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i,
-                                 split_heads=split)
+                                 split_heads=split, defer_parity=dp)
             else:
                 self.gather(self.img_cur, 0)
                 out = m.pair(self.img_cur, feat_j=tr.kf.feat, split_heads=split)

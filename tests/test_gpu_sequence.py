@@ -29,6 +29,18 @@ def _frames(T=6, seed=0):
     return out
 
 
+def _snapshot_matches(loop):
+    """SequenceLoop writes a frame's matches into the tracker's idx_f2k buffer in place (the
+    next frame's seed) and its advance resets that buffer to the identity on a keyframe
+    replacement: keep a copy of the frame's matches, taken on the stream before advance."""
+    adv = loop.advance
+
+    def advance(res, out, feat_i):
+        res["idx_match"] = loop.tr.idx_f2k.clone()
+        adv(res, out, feat_i)
+    loop.advance = advance
+
+
 def test_tracking_sequence_vs_oracle(dev):
     from monst3r_slam_amd import synthetic as syn
     from monst3r_slam_amd.config import default_config
@@ -116,6 +128,7 @@ def test_c3_sequence_384x512_vs_oracle(dev, parity_log):
     seq = S.SyntheticSequence(F, 384, 512, device=dev, period=100, lost_frames=(lost_at,))
     tr = Tracker(model=None, cfg=cfg)
     loop = S.SequenceLoop(tr, seq)
+    _snapshot_matches(loop)
     loop.reset()
     T0 = np.array([0, 0, 0, 0, 0, 0, 1, 1], np.float32)
     o = FR.SequenceOracle(seq.Xcam[0].cpu().numpy(), seq.C_own[0].reshape(-1, 1).cpu().numpy(),
@@ -127,7 +140,7 @@ def test_c3_sequence_384x512_vs_oracle(dev, parity_log):
         X, C = out["X"].cpu().numpy(), out["C"].cpu().numpy()
         D16, Q = out["D16"].cpu().numpy(), out["Q"].cpu().numpy()
         ref = o.step(X, C, D16, Q)
-        assert np.array_equal(res["idx_f2k"].cpu().numpy(), ref["idx"]), f
+        assert np.array_equal(res["idx_match"].cpu().numpy(), ref["idx"]), f
         assert np.array_equal(res["valid_match"].cpu().numpy(), ref["valid"]), f
         lost, new_kf = bool(res["lost"]), bool(res["new_kf"])
         assert lost == ref["lost"] and new_kf == ref["new_kf"], f
@@ -181,6 +194,7 @@ def test_c3_sequence_200_pipelined_vs_oracle(dev, parity_log):
     model, tr, seq = bench.setup(dev, 0, bench.SEQ_FRAMES + 1)
     pipe = FramePipeline(tr, (seq.h, seq.w))
     loop = S.SequenceLoop(tr, seq, pipe)
+    _snapshot_matches(loop)
     loop.reset(parity=0)
     T0 = np.array([0, 0, 0, 0, 0, 0, 1, 1], np.float32)
     o = FR.SequenceOracle(seq.Xcam[0].cpu().numpy(), seq.C_own[0].reshape(-1, 1).cpu().numpy(),
@@ -200,7 +214,7 @@ def test_c3_sequence_200_pipelined_vs_oracle(dev, parity_log):
         X, C = out["X"].cpu().numpy(), out["C"].cpu().numpy()
         D16, Q = out["D16"].cpu().numpy(), out["Q"].cpu().numpy()
         ref = o.step(X, C, D16, Q)
-        assert np.array_equal(res["idx_f2k"].cpu().numpy(), ref["idx"]), f
+        assert np.array_equal(res["idx_match"].cpu().numpy(), ref["idx"]), f
         assert np.array_equal(res["valid_match"].cpu().numpy(), ref["valid"]), f
         lost, new_kf = bool(res["lost"]), bool(res["new_kf"])
         assert lost == ref["lost"] and new_kf == ref["new_kf"], f

@@ -76,11 +76,17 @@ def test_gemm_rope_epilogue(ops, dev, split_k):
     assert _rel(out, ref.reshape(B * S, 3 * C)) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [None, 14])
 @pytest.mark.parametrize("H,W,cin,cout,stride,relu_in,res", [
     (24, 32, 256, 256, 1, True, True), (12, 16, 768, 768, 2, False, False),
-    (96, 128, 96, 256, 1, False, False), (7, 9, 64, 32, 1, True, False)])
-def test_conv3x3_implicit_gemm(ops, dev, H, W, cin, cout, stride, relu_in, res):
+    (96, 128, 96, 256, 1, False, False), (7, 9, 64, 32, 1, True, False),
+    (48, 64, 256, 256, 1, False, True)])
+def test_conv3x3_implicit_gemm(ops, dev, monkeypatch, H, W, cin, cout, stride, relu_in, res,
+                               tile):
+    """tile 14: the 256x256 configuration (two-pass epilogue) on the same convs."""
     from monst3r_slam_amd import _lib
+    if tile:
+        monkeypatch.setenv("M3S_GEMM_TILE", str(tile))
     from monst3r_slam_amd.model import _conv_pack
     g = torch.Generator(device=dev).manual_seed(2)
     x = torch.randn(2, H, W, cin, device=dev, generator=g).bfloat16()
@@ -135,6 +141,43 @@ def test_attention(ops, dev, monkeypatch, S, heads, batch, ks):
     ref = torch.softmax(q @ k.transpose(-1, -2) / 8.0, -1) @ v
     ref = ref.transpose(1, 2).reshape(batch, S, C)
     assert _rel(o, ref) < 2e-2
+
+
+@pytest.mark.parametrize("Sq,Sk,heads,batch,ks,kv_xor,fp8,splits", [
+    (768, 768, 16, 1, "4", 0, 0, "1"), (768, 768, 12, 2, "2", 0, 0, "1"),
+    (768, 768, 12, 2, "2", 1, 0, "1"), (1024, 1024, 12, 2, "2", 0, 0, "1"),
+    (1000, 1000, 12, 2, "2", 0, 0, "1"), (1000, 1000, 16, 1, "4", 0, 0, "1"),
+    (196, 196, 12, 4, "2", 0, 0, "1"), (12, 12, 4, 2, "4", 0, 0, "1"),
+    (64, 100, 3, 2, "2", 0, 0, "1"), (768, 768, 12, 2, "2", 0, 1, "1"),
+    (768, 768, 12, 2, "2", 0, 0, "3"), (768, 768, 16, 1, "4", 0, 0, "2")])
+def test_attention_pingpong_bit_identical(ops, dev, monkeypatch, Sq, Sk, heads, batch, ks, kv_xor,
+                                          fp8, splits):
+    """attn_pp_kernel (opt-in M3S_ATTN_PP=1; 8-wave blocks whose two halves of the key
+    splits alternate matrix and softmax blocks) performs each wave's arithmetic in the
+    lockstep kernel's order: its output must equal M3S_ATTN_PP=0's bit for bit — full and partial key tiles, Sq != Sk,
+    the cross-attention batch xor, e4m3 output, grid-level key splits."""
+    monkeypatch.setenv("M3S_ATTN_KS", ks)
+    monkeypatch.setenv("M3S_ATTN_SPLITS", splits)
+    g = torch.Generator(device=dev).manual_seed(40 + Sq + heads)
+    D = heads * 64
+    q = torch.randn(batch, Sq, D, device=dev, generator=g).bfloat16()
+    kv = (torch.randn(batch, Sk, 2 * D, device=dev, generator=g) * 2).bfloat16()
+    outs = []
+    for pp in ("0", "1"):
+        monkeypatch.setenv("M3S_ATTN_PP", pp)
+        o = torch.full((batch, Sq, D), 7, device=dev,
+                       dtype=torch.uint8 if fp8 else torch.bfloat16)
+        ops.attn(q, D, Sq * D, kv, kv[:, :, D:], 2 * D, Sk * 2 * D, o, D, Sq * D, batch, heads,
+                 Sq, Sk, kv_xor=kv_xor)
+        outs.append(o)
+    assert torch.equal(outs[0], outs[1])
+    if not fp8:
+        kk, vv = kv.float().reshape(batch, Sk, 2, heads, 64).permute(2, 0, 3, 1, 4)
+        if kv_xor:
+            kk, vv = kk[[1, 0]], vv[[1, 0]]
+        qq = q.float().reshape(batch, Sq, heads, 64).transpose(1, 2)
+        ref = (torch.softmax(qq @ kk.transpose(-1, -2) / 8.0, -1) @ vv).transpose(1, 2)
+        assert _rel(outs[1], ref.reshape(batch, Sq, D)) < 2e-2
 
 
 def test_cross_attention_lengths(ops, dev):
@@ -550,7 +593,7 @@ def _ln_stats_ref(x):
 
 @pytest.mark.parametrize("M,N,K,batch,split_k", [(768, 768, 3072, 4, 1), (768, 1024, 1024, 1, 2),
                                                  (768, 1024, 4096, 1, 0), (200, 256, 96, 2, 1)])
-@pytest.mark.parametrize("tile", [None, 12, 13])
+@pytest.mark.parametrize("tile", [None, 12, 13, 14])
 def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k, tile):
     """LN_STATS: the residual GEMM also stores bf16(x) and per-128-column (mean, M2) of the
     stored f32 rows — in the main epilogue and in the split-K reduce (split_k 2 / auto);
@@ -580,7 +623,7 @@ def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k, tile):
                                                   (768, 4096, 1024, 1, 0, "gelu"),
                                                   (200, 384, 256, 2, 1, "none")])
 @pytest.mark.parametrize("split", ["0", "3"])
-@pytest.mark.parametrize("tile", ["0", "12", "13"])
+@pytest.mark.parametrize("tile", ["0", "12", "13", "14"])
 def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi, split, tile):
     """LN_FOLD: LN(x) Wᵀ + b computed as rstd (bf16(x) (W∘γ)ᵀ − mean c1) + c2 from the
     producer's statistics, vs torch fp32 LayerNorm → Linear (→ RoPE / GELU) on x of
@@ -630,8 +673,8 @@ def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi,
     assert _rel(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9, 10, 11, 12, 13])
-@pytest.mark.parametrize("epi", ["gelu", "res"])
+@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("epi", ["gelu", "res", "tail"])
 def test_gemm_every_tile_config(ops, dev, monkeypatch, tile, epi):
     """Every tile configuration (M3S_GEMM_TILE override) on a 768-row problem, straight-
     line epilogues: 96-row tiles once ran their vector epilogue past the tile (rows of the
@@ -639,6 +682,8 @@ def test_gemm_every_tile_config(ops, dev, monkeypatch, tile, epi):
     from monst3r_slam_amd import _lib
     monkeypatch.setenv("M3S_GEMM_TILE", str(tile))
     M, N, K, b = 768, 768, 512, 2
+    if epi == "tail":          # partial tiles in M and N (256x256: both passes partial)
+        M, N, K, epi = 200, 392, 256, "res"
     g = torch.Generator(device=dev).manual_seed(21 + tile)
     A = torch.randn(b, M, K, device=dev, generator=g).bfloat16()
     B = (torch.randn(b, N, K, device=dev, generator=g) / K ** 0.5).bfloat16()

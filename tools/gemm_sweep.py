@@ -25,6 +25,8 @@ SHAPES = {
             ("enc_fc1", 768, 4096, 1024, 1, "gelu"), ("enc_fc2", 768, 1024, 4096, 1, "res")],
     "dec": [("dec_qkvkv", 768, 3840, 768, 2, "bias"), ("dec_proj", 768, 768, 768, 2, "res"),
             ("dec_fc1", 768, 3072, 768, 2, "gelu"), ("dec_fc2", 768, 768, 3072, 2, "res")],
+    # the MASt3R local-feature MLP (per pair: the two MASt3R views)
+    "lf": [("lf_fc1", 768, 7168, 1792, 2, "gelu"), ("lf_fc2", 768, 6400, 7168, 2, "f32")],
 }
 
 
@@ -49,14 +51,46 @@ def timed(fn, reps=20, replays=5):
     return e0.elapsed_time(e1) / (replays * reps) * 1e3
 
 
+# DPT head convs (H, W, Cin, Cout, batch): implicit-GEMM 3x3, bias (+ bf16 residual)
+CONVS = [("rn1_rcu", 96, 128, 256, 256, 2), ("rn2_rcu", 48, 64, 256, 256, 2),
+         ("rn3_rcu", 24, 32, 256, 256, 2), ("head0", 192, 256, 256, 128, 2),
+         ("head2", 384, 512, 128, 128, 2)]
+
+
+def sweep_convs(tiles):
+    from monst3r_slam_amd.model import _conv_pack
+    for name, H, W, cin, cout, b in CONVS:
+        g = torch.Generator(device=dev).manual_seed(3)
+        x = torch.randn(b, H, W, cin, device=dev, generator=g).bfloat16()
+        w = _conv_pack(torch.randn(cout, cin, 3, 3, device=dev, generator=g) /
+                       (9 * cin) ** 0.5).bfloat16().contiguous()
+        bias = torch.randn(cout, device=dev, generator=g)
+        out = torch.empty(b, H, W, cout, device=dev, dtype=torch.bfloat16)
+        fl = 2.0 * H * W * cout * 9 * cin * b
+
+        def run(tile=None):
+            ops.gemm(x, w, out, H * W, cout, 9 * cin, b, sA=H * W * cin, sB=0,
+                     sC=H * W * cout, bias=bias, sBias=0, conv=(H, W, cin, H, W, 1), tile=tile)
+        us = timed(run)
+        print(json.dumps({"shape": name, "impl": "default", "us": us, "tflops": fl / us / 1e6}),
+              flush=True)
+        for t in tiles:
+            us = timed(lambda: run((t, 1)))
+            print(json.dumps({"shape": name, "impl": "m3s", "tile": t, "splits": 1, "fused": 0,
+                              "us": us, "tflops": fl / us / 1e6}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="all")
     ap.add_argument("--tiles", default="1,2,7,10,11,12,13")
     ap.add_argument("--splits", default="1,2,3,4,6,8")
     a = ap.parse_args()
-    shapes = SHAPES["enc"] + SHAPES["dec"] if a.shapes == "all" else SHAPES[a.shapes]
     tiles = [int(t) for t in a.tiles.split(",")]
+    if a.shapes == "conv":
+        sweep_convs(tiles)
+        return
+    shapes = SHAPES["enc"] + SHAPES["dec"] if a.shapes == "all" else SHAPES[a.shapes]
     splits = [int(t) for t in a.splits.split(",")]
     for name, M, N, K, b, epi in shapes:
         A = torch.randn(b, M, K, device=dev).bfloat16()
@@ -79,6 +113,8 @@ def main():
                          flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, **kw)
             elif epi == "gelu":
                 ops.gemm(A, B, C2, M, N, K, b, bias=bias, flags=_lib.EPI_GELU, **kw)
+            elif epi == "f32":
+                ops.gemm(A, B, x, M, N, K, b, bias=bias, flags=_lib.EPI_OUT_F32, **kw)
             else:
                 ops.gemm(A, B, C2, M, N, K, b, bias=bias, **kw)
         us = timed(run)
