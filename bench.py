@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--defer-mast3r", type=int, default=None,
                     help="1: run each frame's MASt3R DPT heads (outputs unread by the "
                          "tracking) during the next frame's decoder; 0: at the frame's end")
+    ap.add_argument("--group", type=int, default=2,
+                    help="frames per prefetched encoder batch (1: the next frame's encoder each "
+                         "step; 2: two frames at M = 1536, spread over two steps)")
     ap.add_argument("--timeline-out", default=None,
                     help="write one replayed step's per-launch GEMM / attention timeline (JSON)")
     ap.add_argument("--no-timeline", action="store_true",
@@ -227,7 +230,7 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
     import numpy as np
     from monst3r_slam_amd import _lib
     lib, P = _lib.load(), _lib.ptr
-    cap = 4096
+    cap = 8192
     buf = torch.empty((cap, 64, 2), dtype=torch.int64, device=dev)
 
     def cap_tl(k):
@@ -244,7 +247,8 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
 
     _lib.check(lib.m3s_timeline_set(P(buf), cap), "timeline_set")
     try:
-        graphs = [cap_tl(i % 2) for i in range(2 * pairs)]
+        period = loop.pipe.period if loop.pipe is not None else 2
+        graphs = [cap_tl(i % period) for i in range(period * max(1, 2 * pairs // period))]
         n = int(lib.m3s_timeline_count())
         kinds = np.zeros(cap, np.int32)
         flops = np.zeros(cap, np.float64)
@@ -784,7 +788,7 @@ def run_sequence(loop, graphs, steps, dev, world):
     t0 = time.perf_counter()
     for i in range(steps):
         if graphs is not None:
-            graphs[i % 2].replay()
+            graphs[i % len(graphs)].replay()
         else:
             loop.step(i)
     torch.cuda.synchronize(dev)
@@ -835,15 +839,17 @@ def main():
 
     from monst3r_slam_amd import sequence as S
     from monst3r_slam_amd.frontend import FramePipeline
-    pipe = None if args.no_prefetch else FramePipeline(tr, (H, W), args.side_priority)
+    pipe = None if args.no_prefetch else FramePipeline(tr, (H, W), args.side_priority,
+                                                       group=args.group)
     loop = S.SequenceLoop(tr, seq, pipe)
     loop.reset(parity=0)
     for w in range(args.warmup):
         loop.step(w)
     torch.cuda.synchronize(dev)
-    # two graphs with the feature double-buffer parities swapped, replayed alternately
-    graphs = None if args.eager else [capture(lambda: loop.step(0), dev, args.main_priority),
-                                      capture(lambda: loop.step(1), dev, args.main_priority)]
+    # one graph per step of the prefetch period (feature slots rotated), replayed in turn
+    period = pipe.period if pipe is not None else 2
+    graphs = None if args.eager else [capture(lambda k=k: loop.step(k), dev, args.main_priority)
+                                      for k in range(period)]
     elapsed = run_sequence(loop, graphs, args.steps, dev, world)
 
     if rank == 0:
@@ -886,7 +892,10 @@ def main():
                                    "MASt3R pair inference + projective matching + Sim3 ray GN "
                                    "+ keyframe fusion / replacement)",
                        "schedule": ("serial" if pipe is None else
-                                    "next frame's encoder prefetched on a side stream") +
+                                    "next frame's encoder prefetched on a side stream"
+                                    if pipe.group == 1 else
+                                    "encoder prefetched on a side stream, two frames per "
+                                    "batch (M = 1536) spread over two steps") +
                                    ("" if args.no_split_heads else
                                     "; MASt3R DPT heads on a side stream"),
                        "h": H, "w": W, "models": "MonST3R ViT-L/B dpt + MASt3R ViT-L/B catmlp+dpt",

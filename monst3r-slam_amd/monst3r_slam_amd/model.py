@@ -209,6 +209,36 @@ class Ops:
 # ---------------------------------------------------------------------------------------
 # weight packing
 # ---------------------------------------------------------------------------------------
+def _drain(gen):
+    """Run a launch-issuing generator to its end; its return value."""
+    while True:
+        try:
+            next(gen)
+        except StopIteration as e:
+            return e.value
+
+
+def _round_robin(chains):
+    """Issue [(stream, generator)] chains one step (one block) each in turn, each step on
+    its chain's stream, until all are exhausted; the chains' return values in order.
+    HIP graphs are submitted node by node in capture order, so a chain captured behind
+    another's complete node list starts that many submissions (≈3 µs each) late."""
+    live = list(range(len(chains)))
+    res = [None] * len(chains)
+    while live:
+        nxt = []
+        for c in live:
+            stream, g = chains[c]
+            with torch.cuda.stream(stream):
+                try:
+                    next(g)
+                    nxt.append(c)
+                except StopIteration as e:
+                    res[c] = e.value
+        live = nxt
+    return res
+
+
 def _conv_pack(w):
     """[Cout][Cin][k][k] → [Cout][k][k][Cin] flattened (implicit-GEMM K order ky, kx, ci)."""
     return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
@@ -465,6 +495,13 @@ class PairModel:
         self._hsuf = ""
         self.side_defer = torch.cuda.Stream(device)
         self._ev_defer = None
+        # side chains to issue block by block between the split decoders' blocks:
+        # [(stream, generator)], consumed by the next decode (SequenceLoop sets the
+        # prefetched encoder here).  Off by default (M3S_INTERLEAVE=1): measured in the C3
+        # step, 200.0 vs 223.8 frames/s with the two-frame encoder, 223.4 vs 224.3 with the
+        # one-frame encoder — chain after chain, the encoder gets ahead alone
+        self.interleave = None
+        self.interleave_capture = os.environ.get("M3S_INTERLEAVE", "0") == "1"
 
     def set_fp8(self, on=True):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
@@ -486,6 +523,16 @@ class PairModel:
         return q[i], dict(fp8=(sc[i], 0))
 
     # ---- streams ----
+    def _take_interleave(self):
+        chains, self.interleave = list(self.interleave or []), None
+        return chains
+
+    def _drain_interleave(self):
+        """Issue what is left of the interleaved side chains, each on its own stream."""
+        for stream, g in self._take_interleave():
+            with torch.cuda.stream(stream):
+                _drain(g)
+
     def _on(self, k):
         """Context: launch on side stream k (after everything queued so far on the current
         stream), or on the current stream when serial."""
@@ -551,17 +598,44 @@ class PairModel:
         projections, or "qkv=cfg:splits,proj=...,fc1=...,fc2=..."; "table" = no hints."""
         tiles = _tile_knob("M3S_ENC_TILE", ("qkv", "proj", "fc1", "fc2"),
                            self.enc_tiles_concurrent if concurrent else {})
-        return self._encode(img, out, tiles)
+        return self._encode(img.shape, img, out, tiles)
 
-    def _encode(self, img, out=None, tiles=None):
+    def encode_gen(self, img, out=None, concurrent=False):
+        """encode() as a generator that yields after each block (interleaved capture)."""
+        tiles = _tile_knob("M3S_ENC_TILE", ("qkv", "proj", "fc1", "fc2"),
+                           self.enc_tiles_concurrent if concurrent else {})
+        return self._encode_gen(img.shape, img, out, tiles)
+
+    def encode_part(self, shape, part, parts, img=None, out=None, gen=False):
+        """Part `part` of `parts` of a prefetched encode (concurrent tile hints) of a batch of
+        `shape` = [B,3,H,W] images: part 0 embeds `img` and runs the first depth/parts blocks,
+        the last part runs the remaining blocks and writes enc_norm into `out` [B,S,E].  The
+        residual stream stays in this model's persistent buffers between the parts, so the
+        parts may be issued in different captured graphs (frontend.FramePipeline(group=2)
+        spreads a two-frame encode over two tracking steps).  Launch for launch the same work
+        as encode(img, out, concurrent=True)."""
+        tiles = _tile_knob("M3S_ENC_TILE", ("qkv", "proj", "fc1", "fc2"),
+                           self.enc_tiles_concurrent)
+        d = self.a.enc_depth
+        lo, hi = d * part // parts, d * (part + 1) // parts
+        g = self._encode_gen(shape, img if part == 0 else None,
+                             out if part == parts - 1 else None, tiles, (lo, hi),
+                             begin=part == 0, end=part == parts - 1)
+        return g if gen else _drain(g)
+
+    def _encode(self, *args, **kw):
+        return _drain(self._encode_gen(*args, **kw))
+
+    def _encode_gen(self, shape, img=None, out=None, tiles=None, layers=None, begin=True,
+                    end=True):
+        """(Generator: yields after issuing each block; returns (feat, pos).)"""
         o, a, W = self.ops, self.a, self.w
-        B, _, H, Wd = img.shape
+        B, _, H, Wd = shape
         gh, gw = H // a.patch, Wd // a.patch
         S, E = gh * gw, a.enc_dim
         M = B * S
-        img = img.to(F32).contiguous()
+        lo, hi = layers if layers is not None else (0, a.enc_depth)
         patches = self._buf("enc_patch", (M, 3 * a.patch * a.patch), BF16)
-        o.patchify(img, patches, B, H, Wd)
         x = self._buf("enc_x", (M, E), F32)
         fold = self.lnfold and not self.fp8 and E % 128 == 0
         if fold:
@@ -570,8 +644,11 @@ class PairModel:
             xb = self._buf("enc_xb", (M, E), BF16)
             st = self._buf("enc_stats", (M, E // 128, 2), F32)
             R32S = dict(flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, ln_stats=(xb, st))
-        o.gemm(patches, W.patch_w, x, M, E, 3 * a.patch * a.patch, bias=W.patch_b,
-               flags=_lib.EPI_OUT_F32, ln_stats=(xb, st) if fold else None)
+        if begin:
+            img = img.to(F32).contiguous()
+            o.patchify(img, patches, B, H, Wd)
+            o.gemm(patches, W.patch_w, x, M, E, 3 * a.patch * a.patch, bias=W.patch_b,
+                   flags=_lib.EPI_OUT_F32, ln_stats=(xb, st) if fold else None)
         adt = U8 if self.fp8 else BF16   # GEMM A operands: e4m3 bytes in fp8 mode
         xn = self._buf("enc_xn", (M, E), adt)
         qkv = self._buf("enc_qkv", (M, 3 * E), BF16)
@@ -581,7 +658,7 @@ class PairModel:
         rt = self.rope_tab(gh, gw)
         P, P8 = W.enc, W.enc8
         if fold:
-            for i in range(a.enc_depth):
+            for i in range(lo, hi):
                 o.gemm(xb, P["qkv_wf"][i], qkv, M, 3 * E, E, bias=P["qkv_c2"][i],
                        rope=(rt, 2 * E, S), ln_fold=(st, P["qkv_c1"][i], 0), tile=tiles.get("qkv"))
                 o.attn(qkv, 3 * E, S * 3 * E, qkv[:, E:], qkv[:, 2 * E:], 3 * E, S * 3 * E, att,
@@ -592,7 +669,8 @@ class PairModel:
                        flags=_lib.EPI_GELU, ln_fold=(st, P["fc1_c1"][i], 0), tile=tiles.get("fc1"))
                 o.gemm(hid, P["fc2_w"][i], x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][i], R=x,
                        tile=tiles.get("fc2"), **R32S)
-        for i in range(a.enc_depth if not fold else 0):
+                yield i
+        for i in (range(lo, hi) if not fold else ()):
             o.ln(x, P["ln1_g"][i], P["ln1_b"][i], xn, M, E)
             # qkv projection with RoPE2D on q and k fused into the epilogue
             w, kw = self._wt(P, P8, "qkv_w", i)
@@ -609,6 +687,9 @@ class PairModel:
             w, kw = self._wt(P, P8, "fc2_w", i)
             o.gemm(hid, w, x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][i], R=x,
                    flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, **kw)
+            yield i
+        if not end:
+            return None, pos
         feat = out if out is not None else torch.empty((B, S, E), dtype=BF16, device=self.dev)
         o.ln(x, W.enc_norm_g, W.enc_norm_b, feat, M, E)
         return feat, pos
@@ -660,14 +741,24 @@ class PairModel:
             main = torch.cuda.current_stream(self.dev)
             side = self.side[1]
             side.wait_stream(main)
-            hooks = self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm, None, part=0)
-            with torch.cuda.stream(side):
-                self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm, None, part=1)
+            g0 = self._decode_folded_gen(x, xb, st, h0, Z, S, E, D, gh, gw, wm, None, part=0)
+            g1 = self._decode_folded_gen(x, xb, st, h0, Z, S, E, D, gh, gw, wm, None, part=1)
+            if self.interleave_capture:
+                # capture order = the order the runtime submits the graph's nodes (serially,
+                # ≈3 µs each): the two chains and the caller's side chains (self.interleave)
+                # are issued block by block in turn, so none waits behind another's whole
+                # node list at the step's start
+                hooks = _round_robin([(main, g0), (side, g1)] + self._take_interleave())[0]
+            else:
+                hooks = _drain(g0)
+                with torch.cuda.stream(side):
+                    _drain(g1)
             main.wait_stream(side)
             h12 = self._buf(self._hk("h12"), (Z, S, D), BF16)
             o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
             hooks["h12"] = h12
             return hooks
+        self._drain_interleave()
         if fold:
             return self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm, on_hook)
         adt = U8 if self.fp8 else BF16
@@ -749,8 +840,12 @@ class PairModel:
             on_hook("h12", hooks)
         return hooks
 
-    def _decode_folded(self, x, xb, st, h0, Z, S, E, D, gh, gw, wm, on_hook=None, part=None):
-        """decode_multi's blocks (croco/blocks.py:172-195 DecoderBlock) with every LayerNorm
+    def _decode_folded(self, *args, **kw):
+        return _drain(self._decode_folded_gen(*args, **kw))
+
+    def _decode_folded_gen(self, x, xb, st, h0, Z, S, E, D, gh, gw, wm, on_hook=None, part=None):
+        """(Generator: yields after issuing each block; returns the hooks.)
+        decode_multi's blocks (croco/blocks.py:172-195 DecoderBlock) with every LayerNorm
         folded into the projection that consumes it (ln_fold): the residual GEMMs write x
         (f32), its bf16 copy and row statistics; qkv (norm1), the cross-attention k/v
         (norm_y of the other side), q (norm2) and fc1 (norm3) normalise in the epilogue.
@@ -820,6 +915,7 @@ class PairModel:
                    **dict(R32S, ln_stats=(xc, st)))
             if (i + 1) in hk and on_hook is not None:
                 on_hook(f"h{i + 1}", hooks)
+            yield i
         if sl is not None:
             return hooks
         h12 = self._buf(self._hk("h12"), (Z, S, D), BF16)
@@ -1102,7 +1198,7 @@ class PairModel:
 
 
     # ---- monst3r_asymmetric_inference ----
-    def _deferred_mast3r_heads(self, parity, gh, gw, H, W):
+    def _deferred_mast3r_heads(self, parity, gh, gw, H, W, stream_ready=False):
         """The MASt3R DPT heads of the PREVIOUS pair (hooks of parity (parity + 1) % 2) on
         side_defer, ordered only after the work enqueued before this pair: they overlap
         this pair's decoder (the tracking chain does not read them)."""
@@ -1118,7 +1214,8 @@ class PairModel:
         pts = self._buf("pts3d", (4, H, W, 3), F32)
         conf = self._buf("conf", (4, H, W), F32)
         sd = self.side_defer
-        sd.wait_stream(torch.cuda.current_stream(self.dev))
+        if not stream_ready:
+            sd.wait_stream(torch.cuda.current_stream(self.dev))
         st = _tile_knob("M3S_SIDE_TILE", ("lf", "dpt"), self.side_tiles)
         with torch.cuda.stream(sd):
             self.ops.tile_default = st.get("dpt")
@@ -1158,13 +1255,25 @@ class PairModel:
             on_hook = lambda name, hk: self._early_branch(name, hk, gh, gw, R)  # noqa: E731
         defer = defer_parity is not None and split_heads and on_hook is None
         if defer:
-            self._deferred_mast3r_heads(defer_parity, gh, gw, H, W)
+            if self.interleave_capture:
+                # issued after the decoders' first blocks (an interleaved chain that
+                # starts one round late), not ahead of them
+                sd = self.side_defer
+                sd.wait_stream(torch.cuda.current_stream(self.dev))
+
+                def _deferred():
+                    yield None
+                    self._deferred_mast3r_heads(defer_parity, gh, gw, H, W, stream_ready=True)
+                self.interleave = list(self.interleave or []) + [(sd, _deferred())]
+            else:
+                self._deferred_mast3r_heads(defer_parity, gh, gw, H, W)
             self._hsuf = f"#{defer_parity % 2}"
         try:
             hooks = self.decode(feat_i[0], feat_j.reshape(-1, a.enc_dim), pos, gh, gw,
                                 on_hook=on_hook)
         finally:
             self._hsuf = ""
+            self._drain_interleave()
         pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W, split=split_heads, R=R,
                                                     mast3r_dpt=not defer)
         return dict(X=pts[0:2], C=conf[0:2], D16=desc16, D=desc, Q=dconf, feat_i=feat_i,

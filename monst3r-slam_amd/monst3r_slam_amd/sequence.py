@@ -169,7 +169,8 @@ class SequenceLoop:
         self.log_i = torch.zeros((seq.n_frames, LOG_INTS), dtype=torch.int32, device=dev)
         self.log_T = torch.zeros((seq.n_frames, 8), dtype=torch.float32, device=dev)
         self.img_cur = torch.empty((1, 3, seq.h, seq.w), dtype=torch.float32, device=dev)
-        self.img_next = torch.empty_like(self.img_cur)
+        g = pipe.group if pipe is not None else 1
+        self.img_next = torch.empty((g, 3, seq.h, seq.w), dtype=torch.float32, device=dev)
         # pipelined: the side stream's gather reads the device frame counter that advance()
         # rewrites on the main stream; this event orders advance() after the gather
         self._gathered = torch.cuda.Event() if dev.type == "cuda" else None
@@ -204,7 +205,10 @@ class SequenceLoop:
         self.log_i.zero_()
         self.log_T.zero_()
         if self.pipe is not None:
-            self.pipe.prime(s.img[first + 1], parity)
+            g = self.pipe.group
+            if first + g >= s.n_frames:
+                raise ValueError("sequence too short for the prefetch group")
+            self.pipe.prime(s.img[first + 1:first + 1 + g].reshape(g, 3, s.h, s.w), parity)
 
     def gather(self, dst, offset):
         s = self.seq
@@ -243,7 +247,7 @@ class SequenceLoop:
             "seq_advance")
 
     def step(self, k=0, split_heads=None):
-        """One frame; k = the feature-buffer parity (pipelined).  res["idx_f2k"] is the
+        """One frame; k = the step index modulo the pipeline's period (feature-buffer slot).  res["idx_f2k"] is the
         tracker's persistent match buffer (the next frame's seed, written in place by the
         matcher): after a keyframe replacement advance() has already reset it to the
         identity, as tracker2.py:255-257 does before the next frame."""
@@ -253,7 +257,9 @@ class SequenceLoop:
         feat_i = None
         if m is not None:
             if pipe is not None:
-                feat_i = pipe.feat[k % 2]
+                feat_i = pipe.slot(k)
+                # group 2: the odd step continues the pair encode its even step started
+                gathers = pipe.group == 1 or k % 2 == 0
                 dp = k % 2 if m.defer_mast3r else None
                 delay = m.layer_event_at is not None
                 if delay:   # the pair first: the encoder waits for its decoder layer event
@@ -268,9 +274,16 @@ class SequenceLoop:
                 else:
                     pipe.side.wait_stream(main)
                 with torch.cuda.stream(pipe.side):
-                    self.gather(self.img_next, 1)
-                    self._gathered.record(pipe.side)
-                    m.encode(self.img_next, out=pipe.feat[(k + 1) % 2], concurrent=True)
+                    if gathers:   # group g: the frames g .. 2g-1 after the tracked one
+                        for j in range(pipe.group):
+                            self.gather(self.img_next[j:j + 1], pipe.group + j if
+                                        pipe.group > 1 else 1)
+                        self._gathered.record(pipe.side)
+                    if delay or not m.interleave_capture:
+                        pipe.encode_side(self.img_next, k)
+                if not (delay or not m.interleave_capture):
+                    # the encoder's blocks are captured between the decoders' blocks
+                    m.interleave = [(pipe.side, pipe.encode_side_gen(self.img_next, k))]
                 if not delay:
                     out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i,
                                  split_heads=split, defer_parity=dp)
@@ -282,7 +295,7 @@ class SequenceLoop:
             out = self._outputs()
         self.pair_outputs(out)
         res = tr.track_outputs(out, self.T_prev)
-        if pipe is not None and m is not None:
+        if pipe is not None and m is not None and gathers:
             main.wait_event(self._gathered)   # the gather read `frame` before advance rewrites it
         self.advance(res, out, feat_i if m is not None else None)
         if m is not None:

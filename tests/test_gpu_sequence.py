@@ -36,7 +36,7 @@ def _snapshot_matches(loop):
     adv = loop.advance
 
     def advance(res, out, feat_i):
-        res["idx_match"] = loop.tr.idx_f2k.clone()
+        res["idx_match"] = loop.tr.idx_f2k.reshape(-1).clone()   # [1, n] buffer → [n]
         adv(res, out, feat_i)
     loop.advance = advance
 
@@ -192,7 +192,7 @@ def test_c3_sequence_200_pipelined_vs_oracle(dev, parity_log):
     from oracle import frontend_ref as FR
     cfg = default_config()
     model, tr, seq = bench.setup(dev, 0, bench.SEQ_FRAMES + 1)
-    pipe = FramePipeline(tr, (seq.h, seq.w))
+    pipe = FramePipeline(tr, (seq.h, seq.w), group=2)   # bench.py's default schedule
     loop = S.SequenceLoop(tr, seq, pipe)
     _snapshot_matches(loop)
     loop.reset(parity=0)
@@ -227,12 +227,15 @@ def test_c3_sequence_200_pipelined_vs_oracle(dev, parity_log):
                                    atol=1e-5)
         np.testing.assert_allclose(tr.kf.C.cpu().numpy(), o.kf.C, rtol=1e-6)
         assert float(tr.kf.N) == o.kf.N, f
-        if i % 20 == 0 and f + 1 < seq.n_frames:
-            # the same launches as the prefetch (concurrent tile hints): bit-identical
+        if i % 20 == 19 and f + 2 < seq.n_frames:
+            # the odd step completed the pair that the next two steps track (frames f + 1,
+            # f + 2): bit-identical to one two-frame encode of those images (same launches)
             torch.cuda.synchronize()
-            got = pipe.feat[(i + 1) % 2]
-            assert torch.equal(got, model.encode(seq.img[f + 1], concurrent=True)[0]), f
-            assert not torch.equal(got, model.encode(seq.img[f], concurrent=True)[0]), f
+            got = pipe.pairs[(i // 2 + 1) % 2].clone()
+            imgs = seq.img[f + 1:f + 3].reshape(2, 3, seq.h, seq.w)
+            assert torch.equal(got, model.encode(imgs, concurrent=True)[0]), f
+            imgs = seq.img[f:f + 2].reshape(2, 3, seq.h, seq.w)
+            assert not torch.equal(got, model.encode(imgs, concurrent=True)[0]), f
             n_feat += 1
     summ = loop.summary()
     assert summ["keyframes_added"] == n_new >= 2
