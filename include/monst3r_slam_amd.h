@@ -77,6 +77,16 @@ int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21, const int64
                        int64_t* d_p1_new, int64_t b, int64_t h, int64_t w, int64_t n,
                        int64_t fdim, int radius, int dilation_max, void* stream);
 
+/* refine_matches in the reference configuration (F = 24, radius 3, n == h*w) reading D11 in
+ * chunk-planar layout [b][3][h*w][8] f16 (written by m3s_desc_planar or by
+ * m3s_vit_local_features_planar): results identical to m3s_refine_matches on the same
+ * descriptors; the layout coalesces the candidate loads.  D21 stays [b][h*w][24]. */
+int m3s_refine_matches_planar(const uint16_t* d_D11p, const uint16_t* d_D21, const int64_t* d_p1,
+                              int64_t* d_p1_new, int64_t b, int64_t h, int64_t w, int radius,
+                              int dilation_max, void* stream);
+/* [b][n][24] f16 descriptor rows → chunk-planar [b][3][n][8] (16-B aligned buffers). */
+int m3s_desc_planar(const uint16_t* d_D, uint16_t* d_Dp, int64_t b, int64_t n, void* stream);
+
 /* Fused replacement for matching.prep_for_iter_proj (matching.py:25-49) and
  * image.img_gradient (image.py:5-38): rays = X11/max(|X11|,1e-12);
  * g{x,y} = 3×3 Scharr/32 on reflect-padded rays;  pts = X21/max(|X21|,1e-12);

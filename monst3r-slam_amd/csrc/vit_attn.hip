@@ -131,8 +131,11 @@ constexpr int RED_FLOATS = 8 * 64 * 4 + 64 * 2;  // one wave's partial: O^T 32x6
 // variant instantiated, and only in the peeled last trip: with both variants in the loop
 // the compiler merged them into one block that ran the MFMAs and softmax of BOTH and
 // selected the results (32 MFMAs, 855 instructions per tile instead of 16 / 422).
-template <int AW, int KS, bool TAILS>
-__global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
+// NSTX > 0: DMA ring depth per key split (default 2 when KS > 1, so two 8-wave blocks fit a
+// CU; 3 keeps two key tiles in flight behind the one being computed, for grids that leave
+// one block per CU anyway — the pair decoder's 144 blocks).
+template <int AW, int KS, bool TAILS, int NSTX = 0>
+__global__ __launch_bounds__(AW * KS * 64, NSTX == 3 ? 1 : 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, void* __restrict__ o,
     int64_t ldo, int64_t so_b, int o_fp8, int Sq, int Sk, int heads, float c_log2, int splits,
@@ -141,7 +144,7 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
   const M3sTlEnd tl_end{tl};
   constexpr int GT = AW * 64;                        // threads of one key-split group
   constexpr int ACH = TILE_BYTES / 16 / GT;          // DMA chunks per thread per operand
-  constexpr int NST = KS == 1 ? ASTAGES : 2;         // ring depth per key split
+  constexpr int NST = NSTX > 0 ? NSTX : (KS == 1 ? ASTAGES : 2);  // ring depth per key split
   static_assert(KS == 1 || (KS - 1) * AW * RED_FLOATS * 4 <= KS * NST * STAGE_BYTES,
                 "partials must fit in the ring");
   __shared__ __attribute__((aligned(16))) char lds[KS * NST * STAGE_BYTES];
@@ -837,10 +840,24 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   // 10.1 → 11.8 us, decoder 13.4 → 16.1 us replayed; C3 223 → 217 frames/s)
   const char* pp_env = getenv("M3S_ATTN_PP");
   const bool pp = pp_env && atoi(pp_env) != 0;
+  // 3-stage K/V ring for the 2-key-split blocks (M3S_ATTN_NST3=1: A/B knob)
+  static const char* nst3_env = getenv("M3S_ATTN_NST3");
+  const bool nst3 = nst3_env && atoi(nst3_env) != 0;
 #define M3S_ATTN_LAUNCH2(AWV, KSV, TL)                                                       \
   if constexpr (AWV * KSV == 8)                                                              \
     if (pp) {                                                                                \
       hipLaunchKernelGGL((attn_pp_kernel<AWV, KSV, TL>),                                     \
+                         dim3((unsigned)(m3s_div_up(sq, AWV * QT) * heads * batch * splits)),\
+                         dim3(AWV * KSV * 64), 0, s,                                         \
+                         reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,               \
+                         reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
+                         ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,      \
+                         (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl);  \
+      break;                                                                                 \
+    }                                                                                        \
+  if constexpr (KSV == 2)                                                                    \
+    if (nst3) {                                                                              \
+      hipLaunchKernelGGL((attn_kernel<AWV, KSV, TL, 3>),                                     \
                          dim3((unsigned)(m3s_div_up(sq, AWV * QT) * heads * batch * splits)),\
                          dim3(AWV * KSV * 64), 0, s,                                         \
                          reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,               \

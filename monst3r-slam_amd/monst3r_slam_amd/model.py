@@ -465,8 +465,10 @@ class PairModel:
         # measured in the pipelined C3 step (encode(concurrent=True)); {} = per-shape table
         # (T128W8 residual GEMMs: 212.8 → 224.5 frames/s; with the split decoder, T256W8
         # qkv / fc1: 214.9 → 221.3, profiles/r02_enc_tile_sweep.txt)
-        self.enc_tiles_concurrent = {"qkv": (13, 1), "proj": (12, 1), "fc1": (13, 1),
-                                     "fc2": (12, 1)}
+        # round 3, two-frame encoder (M = 1536) in the step: fc1 on the 256² tile,
+        # proj / fc2 on 256x128: 238.2 → 242.8 frames/s (profiles/r03_sched_sweep_b.txt)
+        self.enc_tiles_concurrent = {"qkv": (13, 1), "proj": (13, 1), "fc1": (14, 1),
+                                     "fc2": (13, 1)}
         self.dec_tiles = {}   # decoder projections' tile hints (M3S_DEC_TILE; {} = table)
         # ... of the per-model split decoder (two batch-2 chains beside the prefetched
         # encoder), measured in the pipelined step: 226.9 → 232.7 frames/s
@@ -502,6 +504,10 @@ class PairModel:
         # one-frame encoder — chain after chain, the encoder gets ahead alone
         self.interleave = None
         self.interleave_capture = os.environ.get("M3S_INTERLEAVE", "0") == "1"
+        # DPT act_postprocess branches 0 / 1 on a stream of the head set's own, beside
+        # branches 3 / 2 and refinenet4 (M3S_AP_SIDE=0: all four in turn on one stream)
+        self.ap_side = os.environ.get("M3S_AP_SIDE", "1") != "0"
+        self._ap_streams = {}
 
     def set_fp8(self, on=True):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
@@ -523,6 +529,12 @@ class PairModel:
         return q[i], dict(fp8=(sc[i], 0))
 
     # ---- streams ----
+    def _ap_stream(self, tag):
+        st = self._ap_streams.get(tag)
+        if st is None:
+            st = self._ap_streams[tag] = torch.cuda.Stream(self.dev)
+        return st
+
     def _take_interleave(self):
         chains, self.interleave = list(self.interleave or []), None
         return chains
@@ -1161,16 +1173,33 @@ class PairModel:
         Hw = self._hw
         F = a.feature_dim
         g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
+        ev_01 = None
         if R is None:
             R = self._rn_bufs(gh, gw, Z)
-            # act_postprocess + layer_rn (3x3, no bias → F channels): branches 1-3 on side
-            # stream 0, branch 0 (the largest) on the current stream
-            with self._on(0):
-                for k in (1, 2, 3):
-                    self._ap_branch(k, hooks, gh, gw, Z, R)
-                ev_ap = self._event()
-            self._ap_branch(0, hooks, gh, gw, Z, R)
-            self._wait(ev_ap)
+            if self.serial and self.ap_side:
+                # act_postprocess + layer_rn (3x3, no bias → F channels) in the order the
+                # refinenets consume them: branches 3, 2 (refinenet4) on this stream, 0 and 1
+                # (needed from refinenet3 / 2 on) on a stream of this head set's own
+                main = torch.cuda.current_stream(self.dev)
+                side = self._ap_stream(tag)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._ap_branch(1, hooks, gh, gw, Z, R)
+                    ev_1 = torch.cuda.Event()
+                    ev_1.record(side)
+                    self._ap_branch(0, hooks, gh, gw, Z, R)
+                    ev_01 = torch.cuda.Event()
+                    ev_01.record(side)
+                self._ap_branch(3, hooks, gh, gw, Z, R)
+                self._ap_branch(2, hooks, gh, gw, Z, R)
+            else:
+                # branches 1-3 on side stream 0, branch 0 (the largest) on the current stream
+                with self._on(0):
+                    for k in (1, 2, 3):
+                        self._ap_branch(k, hooks, gh, gw, Z, R)
+                    ev_ap = self._event()
+                self._ap_branch(0, hooks, gh, gw, Z, R)
+                self._wait(ev_ap)
         # refinenets: path_k = up2(out_conv(RCU2(path_{k+1} + RCU1(R_k)))) with the next
         # level's skip pre-added by the upsample (consumed as RCU1's residual addend)
         p4 = self._buf("path4", (Z, gh, gw, F), BF16)
@@ -1178,7 +1207,11 @@ class PairModel:
         # the `path + skip` that refinenet_{k-1}'s RCU1 residual takes)
         self._fusion(4, R[3], None, Z, g3h, g3w, (gh, gw), R[2], p4)
         p3 = self._buf("path3", (Z, 2 * gh, 2 * gw, F), BF16)
+        if ev_01 is not None:
+            torch.cuda.current_stream(self.dev).wait_event(ev_1)
         self._fusion(3, p4, R[2], Z, gh, gw, (2 * gh, 2 * gw), R[1], p3)
+        if ev_01 is not None:
+            torch.cuda.current_stream(self.dev).wait_event(ev_01)
         p2 = self._buf("path2", (Z, 4 * gh, 4 * gw, F), BF16)
         self._fusion(2, p3, R[1], Z, 2 * gh, 2 * gw, (4 * gh, 4 * gw), R[0], p2)
         p1 = self._buf("path1", (Z, 8 * gh, 8 * gw, F), BF16)

@@ -9,19 +9,22 @@ CPU tests):
 
   shard_keyframe_features  keyframes encoded round-robin across ranks, features
                            all-gathered (1.5 MB bf16 per keyframe at 384x512)
-  ShardedFactorGraph       FactorGraph whose match_edges runs the rank's round-robin share
-                           of the edges and all-gathers one packed record per edge
-                           (idx i32 x2, valid u8 x2, Q f32 x2 = 18 B/pixel, 3.5 MB/edge);
-                           the acceptance rule and the GN solve then run identically on
-                           every rank (the GN system is tiny; replicating it avoids a
-                           broadcast of the poses).
+  ShardedFactorGraph       FactorGraph whose add_factors matches the rank's round-robin
+                           share of the edges and KEEPS their records (idx, valid, Q:
+                           18 B/pixel) on that rank: only the per-edge match fractions are
+                           all-gathered for the acceptance rule.  Its GN shards the edge
+                           pass the same way — each rank reduces its own edges to 35 f64
+                           sums per two-way edge, one E x 35 all-gather per iteration, then
+                           the same fp64 solve + retraction on every rank (bit-identical to
+                           the unsharded poses).  match_edges (the base-class contract:
+                           every record everywhere) all-gathers packed records instead.
   all_gather_keyframes     the keyframe pointmaps (X_canon, C, N, T_WC) each rank is
                            authoritative for — the tracking rank's fused keyframes, new
                            keyframes — all-gathered into every rank's keyframe store before
                            the backend reads them (3.1 MB per keyframe at 384x512), so the
                            replicated GN sees the same pointmaps everywhere
-Each all-gather moves ceil(E/world) records per rank in ONE collective (padded), i.e.
-world-1 of every world records cross xGMI once — no per-edge messages.
+Each all-gather moves ceil(E/world) rows per rank in ONE collective (padded): no per-edge
+messages.
 """
 from __future__ import annotations
 

@@ -51,6 +51,27 @@ def graph_us(fn, rep=20):
     return e0.elapsed_time(e1) * 1e3 / rep
 
 
+D11p = torch.empty((B, 3, n, 8), dtype=torch.float16, device=dev)
+out2 = torch.empty_like(p1)
+
+
+def planar():
+    _lib.check(lib.m3s_desc_planar(_lib.ptr(D11), _lib.ptr(D11p), B, n, _lib.stream(dev)), "pl")
+
+
+def refine_planar():
+    _lib.check(lib.m3s_refine_matches_planar(_lib.ptr(D11p), _lib.ptr(D21), _lib.ptr(p1),
+                                             _lib.ptr(out2), B, h, w, 3, 5, _lib.stream(dev)),
+               "refine_planar")
+
+
 tag = os.environ.get("M3S_REFINE_KERNEL", "r3")
 us = graph_us(refine)
 print(f"refine_matches 384x512 r3 d5 b={B} {tag}: {us:.1f} us ({us / B:.1f} us per pair)", flush=True)
+us = graph_us(planar)
+print(f"desc_planar 384x512 b={B}: {us:.1f} us", flush=True)
+us = graph_us(refine_planar)
+print(f"refine_matches_planar 384x512 r3 d5 b={B}: {us:.1f} us ({us / B:.1f} us per pair)",
+      flush=True)
+torch.cuda.synchronize()
+print("planar == rows:", bool(torch.equal(out, out2)), flush=True)

@@ -1,5 +1,5 @@
 """The bench's timed C3 step alone, for rocprofv3 (kernel trace / PMC passes): the same
-model, sequence, prefetching FramePipeline and the two parity graphs as bench.py, replayed
+model, sequence, prefetching FramePipeline and the period's graphs as bench.py, replayed
 `--steps` frames from the INIT keyframe.  The replays are bracketed by two marker launches
 (m3s_retr_rownorm on one row: a kernel the step never runs), so a profile's dispatches
 strictly between the two rownorm_kernel dispatches are exactly those steps.
@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--out", default=None, help="JSON with the untraced-equivalent wall time")
+    ap.add_argument("--group", type=int, default=2, help="frames per prefetched encoder batch")
     args = ap.parse_args()
     from monst3r_slam_amd import _lib
     from monst3r_slam_amd import sequence as S
@@ -41,13 +42,13 @@ def main():
     model, tr, seq = bench.setup(dev, 0, max(bench.SEQ_FRAMES, args.steps) + 1)
     model.serial = True
     tr.split_heads = True
-    pipe = FramePipeline(tr, (bench.H, bench.W), 0)
+    pipe = FramePipeline(tr, (bench.H, bench.W), 0, group=args.group)
     loop = S.SequenceLoop(tr, seq, pipe)
     loop.reset(parity=0)
     for w in range(args.warmup):
         loop.step(w)
     torch.cuda.synchronize(dev)
-    graphs = [bench.capture(lambda: loop.step(0), dev), bench.capture(lambda: loop.step(1), dev)]
+    graphs = [bench.capture(lambda k=k: loop.step(k), dev) for k in range(pipe.period)]
     lib = _lib.load()
     mbuf = torch.ones(128, dtype=torch.float32, device=dev)
     loop.reset(parity=0)
@@ -56,7 +57,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        graphs[i % 2].replay()
+        graphs[i % len(graphs)].replay()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     marker(lib, mbuf, dev)
