@@ -131,23 +131,59 @@ constexpr int RED_FLOATS = 8 * 64 * 4 + 64 * 2;  // one wave's partial: O^T 32x6
 // variant instantiated, and only in the peeled last trip: with both variants in the loop
 // the compiler merged them into one block that ran the MFMAs and softmax of BOTH and
 // selected the results (32 MFMAs, 855 instructions per tile instead of 16 / 422).
-// NSTX > 0: DMA ring depth per key split (default 2 when KS > 1, so two 8-wave blocks fit a
-// CU; 3 keeps two key tiles in flight behind the one being computed, for grids that leave
-// one block per CU anyway — the pair decoder's 144 blocks).
-template <int AW, int KS, bool TAILS, int NSTX = 0>
-__global__ __launch_bounds__(AW * KS * 64, NSTX == 3 ? 1 : 2) void attn_kernel(
+// Fused cross-attention q projection (QP): the block computes its own Q tile,
+//   q = RoPE(rstd·(x Wq'ᵀ − mean·c1) + c2)  (the LayerNorm-folded q GEMM of the decoder,
+//   croco/blocks.py:180-185 norm2 + projq, with RoPE2D on q),
+// for its AW·32 query rows and head h from the bf16 LN input x and the producer's row
+// statistics, instead of reading q written by a separate GEMM launch.  The K loop, the
+// MFMA shape / operand order and the epilogue arithmetic are the GEMM's (vit_gemm_kern.h
+// ln_row_stats, the LN_FOLD epilogue, rope8), so Q — and the attention output — are
+// bit-identical to the two-launch path with an unsplit q GEMM.
+struct QProj {
+  const bf16_t* x;      // [batch][Sq][K] bf16 rows (ld ldx, batch stride sx)
+  int64_t ldx, sx;
+  const float* stats;   // [batch][Sq][K/128] (mean, M2) of x's producer
+  const bf16_t* w;      // [wmod][heads·64][K] gamma-folded q weight (stride sw)
+  int64_t sw;
+  int wmod;
+  const float* c1;      // [wmod][heads·64] row sums of w, stride sc
+  const float* c2;      // [wmod][heads·64] folded bias, stride sc
+  int64_t sc;
+  const float* rope;    // [rope_tokens][2][32] cos | sin (rope_table_kernel)
+  int rope_tokens;
+  int K;
+  float eps;
+};
+constexpr int QP_A_BYTES = 128 * 128;                // 128 rows x 64 k bf16
+constexpr int QP_B_BYTES = 64 * 128;                 // 64 cols x 64 k bf16
+constexpr int QP_ST = QP_A_BYTES + QP_B_BYTES;       // one k-chunk stage
+constexpr int QP_NST = 5;                            // stages: 4 k-chunks in flight
+constexpr int QP_QROW = 144;                         // Q tile row pitch (64 bf16 + 16 B)
+// the Q tile and row statistics reuse the stage buffers once the k loop is done
+constexpr int QP_LDS = QP_NST * QP_ST;
+static_assert(128 * QP_QROW + 128 * 8 <= QP_LDS, "Q tile fits the stages");
+
+// (A 3-stage K/V ring for the 2-key-split blocks — two key tiles in flight behind the one
+// being computed, one block per CU — measured 228.1 vs 230.5 frames/s in the C3 step:
+// removed)
+template <int AW, int KS, bool TAILS, bool QP = false>
+__global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, void* __restrict__ o,
     int64_t ldo, int64_t so_b, int o_fp8, int Sq, int Sk, int heads, float c_log2, int splits,
-    int tiles_per_split, float* __restrict__ part, int kv_xor, unsigned long long* tl) {
+    int tiles_per_split, float* __restrict__ part, int kv_xor, unsigned long long* tl,
+    QProj qp) {
   m3s_tl_begin(tl);
   const M3sTlEnd tl_end{tl};
   constexpr int GT = AW * 64;                        // threads of one key-split group
   constexpr int ACH = TILE_BYTES / 16 / GT;          // DMA chunks per thread per operand
-  constexpr int NST = NSTX > 0 ? NSTX : (KS == 1 ? ASTAGES : 2);  // ring depth per key split
+  constexpr int NST = KS == 1 ? ASTAGES : 2;         // ring depth per key split
   static_assert(KS == 1 || (KS - 1) * AW * RED_FLOATS * 4 <= KS * NST * STAGE_BYTES,
                 "partials must fit in the ring");
-  __shared__ __attribute__((aligned(16))) char lds[KS * NST * STAGE_BYTES];
+  static_assert(!QP || (AW == 4 && KS == 2), "q projection: 4 query waves x 2 key splits");
+  constexpr int RING_BYTES = KS * NST * STAGE_BYTES;
+  constexpr int LDS_BYTES = QP && QP_LDS > RING_BYTES ? QP_LDS : RING_BYTES;
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wall = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -179,9 +215,119 @@ __global__ __launch_bounds__(AW * KS * 64, NSTX == 3 ? 1 : 2) void attn_kernel(
   const int qrow = q0 + r;
   bf16x8 qf[4];
   const bf16x8 zero8 = {};
+  if constexpr (QP) {
+    // ---- the block's Q tile [128 queries][64 d] = LN-folded x Wq'ᵀ + RoPE ----
+    (void)Q;
+    char* const sQ = lds;
+    float2* const sS = reinterpret_cast<float2*>(sQ + 128 * QP_QROW);
+    const int qb0 = qt * (AW * QT);                  // first query row of the block
+    const int wsel = qp.wmod > 0 ? (int)(b % qp.wmod) : (int)b;
+    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(qp.x + b * qp.sx), (short)0, 0x7ffffff0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(qp.w + (int64_t)wsel * qp.sw + (int64_t)h * HD * qp.K), (short)0,
+        0x7ffffff0, 0x00020000);
+    // DMA chunks (16 B): A = 128 rows x 8 chunks (2 per thread), B = 64 rows x 8 (1 per
+    // thread); chunk c lands at image row c >> 3, slot c & 7 and carries logical k-chunk
+    // slot ^ k_swz(row) (the K-tile image and swizzle of the attention main loop)
+    uint32_t xa_off[2];
 #pragma unroll
-  for (int ks = 0; ks < 4; ks++)
-    qf[ks] = qrow < Sq ? load8(Q + (int64_t)qrow * ldq + ks * 16 + 8 * hh) : zero8;
+    for (int i = 0; i < 2; i++) {
+      const int c = i * 512 + tid, row = c >> 3, slot = c & 7;
+      xa_off[i] = qb0 + row < Sq
+                      ? (uint32_t)(((int64_t)(qb0 + row) * qp.ldx + (slot ^ k_swz(row)) * 8) * 2)
+                      : OOB;
+    }
+    const uint32_t wb_off =
+        (uint32_t)(((int64_t)(tid >> 3) * qp.K + ((tid & 7) ^ k_swz(tid >> 3)) * 8) * 2);
+    // 3 DMA instructions per thread and k-chunk; QP_NST - 1 chunks in flight (the chunks
+    // are short: with one in flight the loop paid an L2 round trip per chunk)
+    auto issue_qp = [&](int kc, int buf) {
+      const uint32_t k0 = (uint32_t)kc * 64 * 2;
+      char* st = lds + buf * QP_ST;
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+        glds16(rX, st + (i * 512 + wall * 64) * 16, xa_off[i] == OOB ? OOB : xa_off[i] + k0);
+      glds16(rW, st + QP_A_BYTES + (wall * 64) * 16, wb_off + k0);
+    };
+    const int rg = wall & 3, cg = wall >> 2;         // this wave's 32 rows / 32 columns
+    f32x16 qacc;
+#pragma unroll
+    for (int i = 0; i < 16; i++) qacc[i] = 0.f;
+    const int nkc = qp.K / 64;
+#pragma unroll
+    for (int t = 0; t < QP_NST - 1; t++)
+      if (t < nkc) issue_qp(t, t);
+    for (int t = 0; t < nkc; t++) {
+      // retire chunk t; min(QP_NST - 2, nkc - 1 - t) younger chunks stay in flight
+      const int ahead = min(QP_NST - 2, nkc - 1 - t);
+      if (ahead >= 3) vm_wait<9>();
+      else if (ahead == 2) vm_wait<6>();
+      else if (ahead == 1) vm_wait<3>();
+      else vm_wait<0>();
+      block_sync_lds();                              // chunk t visible; t - 1 fully read
+      if (t + QP_NST - 1 < nkc) issue_qp(t + QP_NST - 1, (t + QP_NST - 1) % QP_NST);
+      const char* a_img = lds + (t % QP_NST) * QP_ST;
+      const char* b_img = a_img + QP_A_BYTES;
+      const int ar = rg * 32 + r, br = cg * 32 + r;
+#pragma unroll
+      for (int kk = 0; kk < 4; kk++) {
+        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(
+            a_img + ar * 128 + (((2 * kk + hh) ^ k_swz(ar)) * 16));
+        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(
+            b_img + br * 128 + (((2 * kk + hh) ^ k_swz(br)) * 16));
+        qacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, qacc, 0, 0, 0);
+      }
+    }
+    block_sync_lds();                                // stage buffers free for the Q tile
+    // row statistics (vit_gemm_kern.h ln_row_stats, same order) of the block's 128 rows
+    if (tid < 128) {
+      const int m = qb0 + tid;
+      float2 st8[8];
+      const int groups = qp.K >> 7;
+      const float2* st = reinterpret_cast<const float2*>(qp.stats) + (b * Sq + m) * groups;
+#pragma unroll
+      for (int t = 0; t < 8; t++) st8[t] = (t < groups && m < Sq) ? st[t] : make_float2(0.f, 0.f);
+      float sm = 0.f, m2 = 0.f;
+#pragma unroll
+      for (int t = 0; t < 8; t++) sm += st8[t].x;
+      const float mean = sm / (float)groups;
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        const float d = t < groups ? st8[t].x - mean : 0.f;
+        m2 += fmaf(128.f * d, d, st8[t].y);
+      }
+      sS[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (128.f * (float)groups) + qp.eps));
+    }
+    block_sync_lds();
+    // LN_FOLD epilogue + RoPE (rope8: pairs (i, i + 16) of each 32-wide half; the partner
+    // column is lane r ^ 16), bf16 into the Q tile
+    const int nl = cg * 32 + r;                      // column inside the head
+    const int n = h * HD + nl;
+    const float c1v = qp.c1[wsel * qp.sc + n], c2v = qp.c2[wsel * qp.sc + n];
+    const int i0 = r & 15;
+    const float sg = (r & 16) ? 1.f : -1.f;          // lower: u c - v s; upper: v c + u s
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int rl = rg * 32 + 8 * (i >> 2) + 4 * hh + (i & 3);
+      const float2 ms = sS[rl];
+      const float xv = fmaf(ms.y, fmaf(-ms.x, c1v, qacc[i]), c2v);
+      const float pv = __shfl_xor(xv, 16, 64);
+      const int m = qb0 + rl;
+      const float* tt = qp.rope + ((int64_t)(m % qp.rope_tokens) * 2 + cg) * 32;
+      const float val = xv * tt[i0] + sg * pv * tt[16 + i0];
+      *reinterpret_cast<bf16_t*>(sQ + rl * QP_QROW + nl * 2) = m < Sq ? f2bf(val) : f2bf(0.f);
+    }
+    block_sync_lds();
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++)
+      qf[ks] = *reinterpret_cast<const bf16x8*>(sQ + (wid * QT + r) * QP_QROW + (ks * 16 + 8 * hh) * 2);
+    block_sync_lds();                                // Q tile read before the K/V ring reuses it
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++)
+      qf[ks] = qrow < Sq ? load8(Q + (int64_t)qrow * ldq + ks * 16 + 8 * hh) : zero8;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q ready before the DMA queue fills
   // launder: the compiler would otherwise wait vmcnt(0) (draining the DMA ring) at every
   // use of these ordinary-load results inside the loop
@@ -840,9 +986,7 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   // 10.1 → 11.8 us, decoder 13.4 → 16.1 us replayed; C3 223 → 217 frames/s)
   const char* pp_env = getenv("M3S_ATTN_PP");
   const bool pp = pp_env && atoi(pp_env) != 0;
-  // 3-stage K/V ring for the 2-key-split blocks (M3S_ATTN_NST3=1: A/B knob)
-  static const char* nst3_env = getenv("M3S_ATTN_NST3");
-  const bool nst3 = nst3_env && atoi(nst3_env) != 0;
+  const QProj qp0 = {};
 #define M3S_ATTN_LAUNCH2(AWV, KSV, TL)                                                       \
   if constexpr (AWV * KSV == 8)                                                              \
     if (pp) {                                                                                \
@@ -852,18 +996,7 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
                          reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,               \
                          reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
                          ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,      \
-                         (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl);  \
-      break;                                                                                 \
-    }                                                                                        \
-  if constexpr (KSV == 2)                                                                    \
-    if (nst3) {                                                                              \
-      hipLaunchKernelGGL((attn_kernel<AWV, KSV, TL, 3>),                                     \
-                         dim3((unsigned)(m3s_div_up(sq, AWV * QT) * heads * batch * splits)),\
-                         dim3(AWV * KSV * 64), 0, s,                                         \
-                         reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,               \
-                         reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
-                         ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,      \
-                         (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl);  \
+                         (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl);     \
       break;                                                                                 \
     }                                                                                        \
   hipLaunchKernelGGL((attn_kernel<AWV, KSV, TL>),                                           \
@@ -872,7 +1005,7 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
                      reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,                   \
                      reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
                      ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,          \
-                     (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl)
+                     (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl, qp0)
 #define M3S_ATTN_LAUNCH(AWV, KSV)                                                            \
   do {                                                                                       \
     if (sk % AKT) {                                                                          \
@@ -895,6 +1028,65 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   }
 #undef M3S_ATTN_LAUNCH
 #undef M3S_ATTN_LAUNCH2
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
+// Cross-attention with the q projection fused in (QProj above).  Only the pair decoder's
+// configuration: 4 query waves x 2 key splits per block, K % 64 == 0, K ≤ 1024, head dim 64.
+extern "C" int m3s_vit_attention_qproj(const m3s_qproj_desc* d, const void* d_k, const void* d_v,
+                                       int64_t ld_kv, int64_t stride_kv, void* d_o,
+                                       int64_t ld_o, int64_t stride_o, int64_t batch,
+                                       int64_t heads, int64_t sq, int64_t sk,
+                                       int kv_batch_xor, void* stream) {
+  if (!d || !d->x || !d->stats || !d->w || !d->c1 || !d->c2 || !d->rope_table || !d_k || !d_v ||
+      !d_o || batch <= 0 || heads <= 0 || sq <= 0 || sk <= 0)
+    return M3S_ERR_INVALID_ARG;
+  if (kv_batch_xor < 0 || kv_batch_xor > 1 || (kv_batch_xor && batch % 2)) return M3S_ERR_INVALID_ARG;
+  if (d->k % 128 || d->k > 1024 || d->k < 128 || d->rope_tokens <= 0 || d->weight_mod < 0)
+    return M3S_ERR_INVALID_ARG;
+  if ((((uintptr_t)d->x) | ((uintptr_t)d->w) | ((uintptr_t)d_k) | ((uintptr_t)d_v)) % 16)
+    return M3S_ERR_INVALID_ARG;
+  if (d->ld_x % 8 || d->stride_x % 8 || d->stride_w % 8 || ld_kv % 8 || stride_kv % 8)
+    return M3S_ERR_INVALID_ARG;
+  if (((uintptr_t)d_o) % 8 || ld_o % 4 || stride_o % 4) return M3S_ERR_INVALID_ARG;
+  if (batch > 65535 || heads > 65535) return M3S_ERR_TOO_LARGE;
+  if (sk * ld_kv * 2 >= 0x7ffffff0 || (batch * d->stride_x + sq * d->ld_x) * 2 >= 0x7ffffff0 ||
+      (heads * 64 * d->k) * 2 >= 0x7ffffff0)
+    return M3S_ERR_TOO_LARGE;
+  QProj qp;
+  qp.x = reinterpret_cast<const bf16_t*>(d->x);
+  qp.ldx = d->ld_x;
+  qp.sx = d->stride_x;
+  qp.stats = d->stats;
+  qp.w = reinterpret_cast<const bf16_t*>(d->w);
+  qp.sw = d->stride_w;
+  qp.wmod = d->weight_mod;
+  qp.c1 = d->c1;
+  qp.c2 = d->c2;
+  qp.sc = d->stride_c;
+  qp.rope = d->rope_table;
+  qp.rope_tokens = (int)d->rope_tokens;
+  qp.K = (int)d->k;
+  qp.eps = d->ln_eps;
+  const float c_log2 = 0.125f * 1.4426950408889634f;
+  hipStream_t s = m3s_stream(stream);
+  unsigned long long* tl =
+      m3s_timeline_take(M3S_TL_ATTN, 4.0 * sq * sk * HD * heads * batch, sq, sk, heads, batch);
+  const dim3 grid((unsigned)(m3s_div_up(sq, 4 * QT) * heads * batch));
+  const int nkt = (int)m3s_div_up(sk, AKT);
+  if (sk % AKT)
+    hipLaunchKernelGGL((attn_kernel<4, 2, true, true>), grid, dim3(512), 0, s, nullptr,
+                       (int64_t)0, (int64_t)0, reinterpret_cast<const bf16_t*>(d_k),
+                       reinterpret_cast<const bf16_t*>(d_v), ld_kv, stride_kv, d_o, ld_o,
+                       stride_o, 0, (int)sq, (int)sk, (int)heads, c_log2, 1, nkt, nullptr,
+                       kv_batch_xor, tl, qp);
+  else
+    hipLaunchKernelGGL((attn_kernel<4, 2, false, true>), grid, dim3(512), 0, s, nullptr,
+                       (int64_t)0, (int64_t)0, reinterpret_cast<const bf16_t*>(d_k),
+                       reinterpret_cast<const bf16_t*>(d_v), ld_kv, stride_kv, d_o, ld_o,
+                       stride_o, 0, (int)sq, (int)sk, (int)heads, c_log2, 1, nkt, nullptr,
+                       kv_batch_xor, tl, qp);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }

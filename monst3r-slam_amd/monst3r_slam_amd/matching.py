@@ -17,10 +17,11 @@ import torch
 from . import _lib
 from .config import config as _config
 
-# refine_matches reads the candidate image's descriptors in chunk-planar layout
-# (m3s_desc_planar + m3s_refine_matches_planar, bit-identical results) in the reference
-# configuration; M3S_REFINE_PLANAR=0 keeps the [b,h,w,24] rows kernel
-_PLANAR = os.environ.get("M3S_REFINE_PLANAR", "1") != "0"
+# M3S_REFINE_PLANAR=1: refine_matches reads the candidate image's descriptors in
+# chunk-planar layout (m3s_desc_planar + m3s_refine_matches_planar, bit-identical results).
+# Off: measured 370 vs 192 us per 384x512 direction (tools/match_bench.py) — a candidate's
+# three chunks then sit in three far-apart planes instead of one 48-B row
+_PLANAR = os.environ.get("M3S_REFINE_PLANAR", "0") == "1"
 
 
 def pixel_to_lin(p1, w):

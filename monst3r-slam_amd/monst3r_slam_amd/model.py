@@ -182,6 +182,21 @@ class Ops:
                                               _p(ws), ws.numel(), kv_xor, self._s()),
                    "vit_attention")
 
+    def attn_qproj(self, x, st, w, c1, c2, rope, k, v, ldkv, skv_b, o, ldo, so_b, batch,
+                   heads, sq, sk, K, wmod, kv_xor=0):
+        """Cross-attention with the LN-folded, RoPE'd q projection fused in
+        (m3s_vit_attention_qproj): x bf16 [batch][sq][K], st its (mean, M2) statistics,
+        w [wmod][heads·64][K], c1 / c2 [wmod][heads·64], rope = (table, tokens)."""
+        d = _lib.QProjDesc()
+        d.x, d.ld_x, d.stride_x, d.stats = _p(x), K, sq * K, _p(st)
+        d.w, d.stride_w, d.weight_mod = _p(w), heads * 64 * K, wmod
+        d.c1, d.c2, d.stride_c = _p(c1), _p(c2), heads * 64
+        d.rope_table, d.rope_tokens = _p(rope[0]), rope[1]
+        d.k, d.ln_eps = K, LN_EPS
+        _lib.check(self.lib.m3s_vit_attention_qproj(ctypes.byref(d), _p(k), _p(v), ldkv, skv_b,
+                                                    _p(o), ldo, so_b, batch, heads, sq, sk,
+                                                    kv_xor, self._s()), "vit_attention_qproj")
+
     def copy_rows(self, src, dst, rows, row_bytes, src_row, dst_row, outer, inner, src_outer,
                   src_inner, src_base, dst_outer, dst_inner, dst_base):
         """m3s_copy_rows (byte strides): item (o, i) of outer x inner copies `rows` rows."""
@@ -504,10 +519,10 @@ class PairModel:
         # one-frame encoder — chain after chain, the encoder gets ahead alone
         self.interleave = None
         self.interleave_capture = os.environ.get("M3S_INTERLEAVE", "0") == "1"
-        # DPT act_postprocess branches 0 / 1 on a stream of the head set's own, beside
-        # branches 3 / 2 and refinenet4 (M3S_AP_SIDE=0: all four in turn on one stream)
-        self.ap_side = os.environ.get("M3S_AP_SIDE", "1") != "0"
-        self._ap_streams = {}
+        # M3S_FUSE_Q=1: the decoder's cross-attention q projection fused into the attention
+        # launch (m3s_vit_attention_qproj, bit-identical).  Off: 227.4 vs 231.6 frames/s in
+        # the C3 step (the per-block q prologue is latency-bound)
+        self.fuse_q = os.environ.get("M3S_FUSE_Q", "0") == "1"
 
     def set_fp8(self, on=True):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
@@ -529,12 +544,6 @@ class PairModel:
         return q[i], dict(fp8=(sc[i], 0))
 
     # ---- streams ----
-    def _ap_stream(self, tag):
-        st = self._ap_streams.get(tag)
-        if st is None:
-            st = self._ap_streams[tag] = torch.cuda.Stream(self.dev)
-        return st
-
     def _take_interleave(self):
         chains, self.interleave = list(self.interleave or []), None
         return chains
@@ -903,11 +912,18 @@ class PairModel:
                    D, S * D, Z, a.dec_heads, S, S)
             o.gemm(att, P["proj_w"], x, S, D, D, Z, sB=D * D, bias=P["proj_b"], sBias=D, **zs,
                    tile=tl("proj"), **R32S)
-            o.gemm(xb, P["q_wf"], q, S, D, D, Z, sB=D * D, bias=P["q_c2"], sBias=D,
-                   rope=(rt, D, S), ln_fold=(st, P["q_c1"], 0), tile=tl("q"), **zs)
-            # k' / v' of problem z were computed in problem z ^ 1's rows
-            o.attn(q, D, S * D, qkv[:, :, 2 * D:], qkv[:, :, 4 * D:], F5, S * F5, att, D, S * D,
-                   Z, a.dec_heads, S, S, kv_xor=1)
+            if self.fuse_q and D == a.dec_heads * 64 and D % 128 == 0 and D <= 1024:
+                # norm2 + q projection + RoPE inside the cross-attention (one launch fewer
+                # per layer; bit-identical to the q GEMM + attention below)
+                o.attn_qproj(xb, st, P["q_wf"], P["q_c1"], P["q_c2"], (rt, S),
+                             qkv[:, :, 2 * D:], qkv[:, :, 4 * D:], F5, S * F5, att, D, S * D,
+                             Z, a.dec_heads, S, S, D, wm, kv_xor=1)
+            else:
+                o.gemm(xb, P["q_wf"], q, S, D, D, Z, sB=D * D, bias=P["q_c2"], sBias=D,
+                       rope=(rt, D, S), ln_fold=(st, P["q_c1"], 0), tile=tl("q"), **zs)
+                # k' / v' of problem z were computed in problem z ^ 1's rows
+                o.attn(q, D, S * D, qkv[:, :, 2 * D:], qkv[:, :, 4 * D:], F5, S * F5, att, D,
+                       S * D, Z, a.dec_heads, S, S, kv_xor=1)
             o.gemm(att, P["cproj_w"], x, S, D, D, Z, sB=D * D, bias=P["cproj_b"], sBias=D, **zs,
                    tile=tl("cproj"), **R32S)
             o.gemm(xb, P["fc1_wf"], hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm,
@@ -1173,33 +1189,18 @@ class PairModel:
         Hw = self._hw
         F = a.feature_dim
         g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
-        ev_01 = None
         if R is None:
             R = self._rn_bufs(gh, gw, Z)
-            if self.serial and self.ap_side:
-                # act_postprocess + layer_rn (3x3, no bias → F channels) in the order the
-                # refinenets consume them: branches 3, 2 (refinenet4) on this stream, 0 and 1
-                # (needed from refinenet3 / 2 on) on a stream of this head set's own
-                main = torch.cuda.current_stream(self.dev)
-                side = self._ap_stream(tag)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    self._ap_branch(1, hooks, gh, gw, Z, R)
-                    ev_1 = torch.cuda.Event()
-                    ev_1.record(side)
-                    self._ap_branch(0, hooks, gh, gw, Z, R)
-                    ev_01 = torch.cuda.Event()
-                    ev_01.record(side)
-                self._ap_branch(3, hooks, gh, gw, Z, R)
-                self._ap_branch(2, hooks, gh, gw, Z, R)
-            else:
-                # branches 1-3 on side stream 0, branch 0 (the largest) on the current stream
-                with self._on(0):
-                    for k in (1, 2, 3):
-                        self._ap_branch(k, hooks, gh, gw, Z, R)
-                    ev_ap = self._event()
-                self._ap_branch(0, hooks, gh, gw, Z, R)
-                self._wait(ev_ap)
+            # act_postprocess + layer_rn (3x3, no bias → F channels): branches 1-3 on side
+            # stream 0, branch 0 (the largest) on the current stream (one stream when serial;
+            # branches 0 / 1 on a stream of the head set's own made capture_end segfault on
+            # this ROCm stack — DESIGN §2)
+            with self._on(0):
+                for k in (1, 2, 3):
+                    self._ap_branch(k, hooks, gh, gw, Z, R)
+                ev_ap = self._event()
+            self._ap_branch(0, hooks, gh, gw, Z, R)
+            self._wait(ev_ap)
         # refinenets: path_k = up2(out_conv(RCU2(path_{k+1} + RCU1(R_k)))) with the next
         # level's skip pre-added by the upsample (consumed as RCU1's residual addend)
         p4 = self._buf("path4", (Z, gh, gw, F), BF16)
@@ -1207,11 +1208,7 @@ class PairModel:
         # the `path + skip` that refinenet_{k-1}'s RCU1 residual takes)
         self._fusion(4, R[3], None, Z, g3h, g3w, (gh, gw), R[2], p4)
         p3 = self._buf("path3", (Z, 2 * gh, 2 * gw, F), BF16)
-        if ev_01 is not None:
-            torch.cuda.current_stream(self.dev).wait_event(ev_1)
         self._fusion(3, p4, R[2], Z, gh, gw, (2 * gh, 2 * gw), R[1], p3)
-        if ev_01 is not None:
-            torch.cuda.current_stream(self.dev).wait_event(ev_01)
         p2 = self._buf("path2", (Z, 4 * gh, 4 * gw, F), BF16)
         self._fusion(2, p3, R[1], Z, 2 * gh, 2 * gw, (4 * gh, 4 * gw), R[0], p2)
         p1 = self._buf("path1", (Z, 8 * gh, 8 * gw, F), BF16)

@@ -813,3 +813,59 @@ def test_decoder_split_by_model_matches_batched(dev):
         assert torch.isfinite(b[k]).all(), k
         rel = float((a[k] - b[k]).norm() / a[k].norm())
         assert rel < 2e-2, (k, rel)
+
+
+@pytest.mark.parametrize("gh,gw,heads,batch,wmod", [(24, 32, 12, 2, 2), (24, 32, 12, 4, 4),
+                                                    (12, 15, 4, 2, 2), (20, 24, 4, 2, 0)])
+def test_cross_attention_fused_q_bit_identical(ops, dev, monkeypatch, gh, gw, heads, batch,
+                                               wmod):
+    """m3s_vit_attention_qproj (norm2 + q projection + RoPE inside the cross-attention,
+    croco/blocks.py:180-185) equals the LN-folded q GEMM (unsplit, 8-wave 128² tiles) followed
+    by m3s_vit_attention bit for bit — the pair decoder's shape (768 tokens, 12 heads, kv of
+    problem z ^ 1), a key tail (Sk % 64 != 0) and a query tail (Sq % 128 != 0), and per-problem
+    weights with weight_mod 0 / 2 / 4; and it stays within bf16 tolerance of torch fp32
+    LayerNorm → Linear → RoPE → softmax attention."""
+    from monst3r_slam_amd.model import ln_fold, LN_EPS
+    from oracle import vit_ref as V
+    S, D = gh * gw, heads * 64
+    g = torch.Generator(device=dev).manual_seed(21)
+    x = torch.randn(batch, S, D, device=dev, generator=g) * 1.5 + 0.7
+    nw = wmod if wmod > 0 else batch
+    gam = 1.0 + 0.3 * torch.randn(nw, D, device=dev, generator=g)
+    bet = 0.2 * torch.randn(nw, D, device=dev, generator=g)
+    W = torch.randn(nw, D, D, device=dev, generator=g) / D ** 0.5
+    b = torch.randn(nw, D, device=dev, generator=g)
+    wf, c1, c2 = ln_fold(W, b, gam, bet, dev)
+    xb = x.bfloat16().contiguous()
+    st = _ln_stats_ref(x).contiguous()
+    kv = (torch.randn(batch, S, 2 * D, device=dev, generator=g)).bfloat16().contiguous()
+    pos = V.positions(1, gh, gw, dev)[0].contiguous()
+    rt = ops.rope_table(pos, 100.0)
+    q = torch.empty(batch, S, D, device=dev, dtype=torch.bfloat16)
+    ops.gemm(xb, wf, q, S, D, D, batch, sA=S * D, sB=D * D, sC=S * D, bias=c2, sBias=D,
+             rope=(rt, D, S), ln_fold=(st, c1, 0), wmod=wmod, tile=(12, 1))
+    ref = torch.empty(batch, S, D, device=dev, dtype=torch.bfloat16)
+    # the fused kernel's block shape (4 query waves x 2 key splits) for the reference too:
+    # the key-split merge order is part of the rounding
+    monkeypatch.setenv("M3S_ATTN_AW", "4")
+    monkeypatch.setenv("M3S_ATTN_KS", "2")
+    ops.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, ref, D, S * D, batch, heads, S, S,
+             kv_xor=1)
+    monkeypatch.delenv("M3S_ATTN_AW")
+    monkeypatch.delenv("M3S_ATTN_KS")
+    got = torch.zeros_like(ref)
+    ops.attn_qproj(xb, st, wf, c1, c2, (rt, S), kv, kv[:, :, D:], 2 * D, S * 2 * D, got, D,
+                   S * D, batch, heads, S, S, D, wmod, kv_xor=1)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), float((got.float() - ref.float()).abs().max())
+    # fp32 restatement: LN → Linear → RoPE2D → attention over the other problem's k / v
+    ws = torch.arange(batch, device=dev) % nw
+    ln = F.layer_norm(x, (D,), eps=LN_EPS) * gam[ws][:, None] + bet[ws][:, None]
+    qf = torch.bmm(ln, W[ws].transpose(1, 2)) + b[ws][:, None]
+    posb = V.positions(batch, gh, gw, dev)
+    qh = V.rope2d(qf.reshape(batch, S, heads, 64).transpose(1, 2), posb, 100.0)
+    kvx = kv.float()[torch.arange(batch, device=dev) ^ 1]
+    kh = kvx[..., :D].reshape(batch, S, heads, 64).transpose(1, 2)
+    vh = kvx[..., D:].reshape(batch, S, heads, 64).transpose(1, 2)
+    o = F.scaled_dot_product_attention(qh, kh, vh).transpose(1, 2).reshape(batch, S, D)
+    assert _rel(got, o) < 2e-2

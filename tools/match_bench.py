@@ -14,12 +14,13 @@ lib = _lib.load()
 h, w, F = 384, 512, 24
 n = h * w
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+J = int(sys.argv[2]) if len(sys.argv) > 2 else 4   # match jitter amplitude (px); 0 = smooth
 g = torch.Generator(device=dev).manual_seed(0)
 D11 = torch.nn.functional.normalize(torch.randn(B, h, w, F, device=dev, generator=g), dim=-1).half()
 D21 = torch.nn.functional.normalize(torch.randn(B, n, F, device=dev, generator=g), dim=-1).half()
 # matches near the identity (as after iter_proj on consecutive frames): local windows overlap
 yy, xx = torch.meshgrid(torch.arange(h, device=dev), torch.arange(w, device=dev), indexing="ij")
-jit = torch.randint(-4, 5, (B, 2, h, w), device=dev, generator=g)
+jit = torch.randint(-J, J + 1, (B, 2, h, w), device=dev, generator=g) + (3 if J == 0 else 0)
 p1 = torch.stack([(xx + jit[:, 0]).clamp(0, w - 1), (yy + jit[:, 1]).clamp(0, h - 1)], -1)
 p1 = p1.reshape(B, n, 2).contiguous()
 out = torch.empty_like(p1)
@@ -67,11 +68,11 @@ def refine_planar():
 
 tag = os.environ.get("M3S_REFINE_KERNEL", "r3")
 us = graph_us(refine)
-print(f"refine_matches 384x512 r3 d5 b={B} {tag}: {us:.1f} us ({us / B:.1f} us per pair)", flush=True)
+print(f"refine_matches 384x512 r3 d5 b={B} jitter={J} {tag}: {us:.1f} us ({us / B:.1f} us per pair)", flush=True)
 us = graph_us(planar)
 print(f"desc_planar 384x512 b={B}: {us:.1f} us", flush=True)
 us = graph_us(refine_planar)
-print(f"refine_matches_planar 384x512 r3 d5 b={B}: {us:.1f} us ({us / B:.1f} us per pair)",
+print(f"refine_matches_planar 384x512 r3 d5 b={B} jitter={J}: {us:.1f} us ({us / B:.1f} us per pair)",
       flush=True)
 torch.cuda.synchronize()
 print("planar == rows:", bool(torch.equal(out, out2)), flush=True)
