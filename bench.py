@@ -286,12 +286,19 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
                 raise RuntimeError(f"step timeline: {int((~ok).sum())} launches left no stamp")
             k, fl = kinds[a:b], flops[a:b]
             row = {"step_ms": step_ms, "span_ms": (t[:, 1].max() - t[:, 0].min()) * 1e-5}
+            dm = dims[a:b].astype(np.float64)
             for name, code in (("gemm", 1), ("attn", 2)):
                 sel = k == code
                 iv = [(int(s_), int(e)) for s_, e in t[sel]]
+                d = dm[sel]
+                if code == 1:   # A + B + C once each, bf16: (M·K + N·K + M·N)·batch·2 B
+                    ab = float(((d[:, 0] * d[:, 2] + d[:, 1] * d[:, 2] + d[:, 0] * d[:, 1])
+                                * d[:, 3] * 2).sum())
+                else:           # q, k, v read + o written once, bf16: 4·S·64·heads·batch·2 B
+                    ab = float(((2 * d[:, 0] + 2 * d[:, 1]) * 64 * d[:, 2] * d[:, 3] * 2).sum())
                 row[name] = {"launches": int(sel.sum()), "gflop": float(fl[sel].sum()) / 1e9,
                              "sum_ms": float((t[sel, 1] - t[sel, 0]).sum()) * 1e-5,
-                             "union_ms": _union_ticks(iv) * 1e-5}
+                             "union_ms": _union_ticks(iv) * 1e-5, "alg_bytes": ab}
             row["busy_union_ms"] = _union_ticks([(int(s_), int(e)) for s_, e in t]) * 1e-5
             rows.append(row)
             if rd == rounds - 1 and i == len(graphs) - 2:
@@ -309,6 +316,7 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
         sm = med(lambda r: r[name]["sum_ms"])
         nl = med(lambda r: r[name]["launches"])
         res[name] = {"launches": nl, "gflop": gf, "union_ms": un, "sum_of_launch_ms": sm,
+                     "algorithmic_bytes": med(lambda r: r[name]["alg_bytes"]),
                      "avg_launch_us": sm / nl * 1e3 if nl else None,
                      "tflops_union": gf / un if un else None,
                      "tflops_per_launch_avg": gf / sm if sm else None}
@@ -371,6 +379,8 @@ def step_pmc():
     if not os.path.exists(path):
         return None
     d = dict(json.load(open(path)))
+    if isinstance(d.get("traced"), dict):   # the per-kernel table stays in the profile file
+        d["traced"] = {k: v for k, v in d["traced"].items() if k != "kernels"}
     d["source"] = "profiles/r03_step_pmc.json"
     return d
 
@@ -408,8 +418,21 @@ def roofline_entry(tl, roof, pmc, mfma, step_ms):
              attention=tl["attn"], timeline_step_ms=tl["step_ms"],
              timeline_vs_timed_step=tl["step_ms"] / step_ms,
              gemm_or_attn_union_ms=tl["gemm_or_attn_union_ms"])
+    e["algorithmic_bytes_per_step"] = g["algorithmic_bytes"]
+    e["algorithmic_bytes_rule"] = ("floor: every GEMM reads A and B and writes C once, bf16 "
+                                   "((M·K + N·K + M·N)·batch·2 B per launch, step_timeline dims)")
     if mfma:
         e["mfma_busy"] = mfma
+        hb = (mfma.get("hbm") or {}).get("gemm")
+        if hb:   # the step's own GEMM HBM bytes (PMC passes over the replayed step)
+            e["traffic"] = hb["bytes"] / max(g["launches"], 1)
+            e["traffic_unit"] = ("HBM bytes per GEMM launch of the timed step (PMC FETCH_SIZE "
+                                 "x2 + WRITE_SIZE over tools/step_prof.py, "
+                                 + mfma.get("source", "") + ")")
+            e["traffic_per_step_bytes"] = hb["bytes"]
+            e["traffic_vs_algorithmic"] = hb["bytes"] / g["algorithmic_bytes"]
+            e.pop("traffic_per_pair_bytes", None)
+            e.pop("l2_hit_rate", None)
     return e
 
 

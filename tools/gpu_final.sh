@@ -22,7 +22,14 @@ case "$1" in
     timeout -s KILL 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU GRBM_GUI_ACTIVE \
       -d gpurun_out/${R}_pmc -o step -- python3 tools/step_prof.py --steps 20 \
       > gpurun_out/${R}_pmc.log 2>&1 || { tail -20 gpurun_out/${R}_pmc.log; exit 1; }
+    for c in FETCH_SIZE WRITE_SIZE; do
+      rm -rf gpurun_out/${R}_pmc_$c
+      timeout -s KILL 180 rocprofv3 --pmc $c -d gpurun_out/${R}_pmc_$c -o step -- \
+        python3 tools/step_prof.py --steps 20 > gpurun_out/${R}_pmc_$c.log 2>&1 \
+        || { tail -20 gpurun_out/${R}_pmc_$c.log; exit 1; }
+    done
     python tools/step_pmc_report.py --pmc gpurun_out/${R}_pmc --trace gpurun_out/${R}_trace \
+      --fetch gpurun_out/${R}_pmc_FETCH_SIZE --write gpurun_out/${R}_pmc_WRITE_SIZE \
       --steps 20 --step-ms "$ms" --out gpurun_out/${R}_step_pmc.json && tail -c 600 gpurun_out/${R}_step_pmc.json ;;
   *) echo "usage: $0 bench|prof"; exit 2 ;;
 esac

@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--step-ms", type=float, required=True, help="untraced ms per step")
     ap.add_argument("--gemm-gflop", type=float, default=None,
                     help="algorithmic GEMM GFLOP per step (bench step_timeline)")
+    ap.add_argument("--fetch", default=None, help="a --pmc FETCH_SIZE run of the same script")
+    ap.add_argument("--write", default=None, help="a --pmc WRITE_SIZE run of the same script")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     rows = _csv(a.pmc, "counter_collection.csv")
@@ -107,6 +109,27 @@ def main():
         out["traced"] = {"span_ms_per_step": (t1 - t0) * 1e-6 / S,
                          "kernel_ms_per_step": {k: v / S for k, v in cls.items()},
                          "dispatches_per_step": len(tids) / S, "kernels": kern}
+    # HBM bytes per step and kernel class: FETCH_SIZE (KiB; x2 on gfx950 for 16-B-per-lane
+    # reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE (KiB), each from its own PMC run
+    if a.fetch or a.write:
+        hbm = collections.defaultdict(lambda: {"fetch_bytes": 0.0, "write_bytes": 0.0})
+        for path, cname, key, scale in ((a.fetch, "FETCH_SIZE", "fetch_bytes", 2048.0),
+                                        (a.write, "WRITE_SIZE", "write_bytes", 1024.0)):
+            if not path:
+                continue
+            rr = _csv(path, "counter_collection.csv")
+            nm, val = {}, collections.defaultdict(float)
+            for r in rr:
+                d = int(r["Dispatch_Id"])
+                nm[d] = r["Kernel_Name"]
+                if r["Counter_Name"] == cname:
+                    val[d] += float(r["Counter_Value"])
+            for d in between_markers(sorted(nm), nm):
+                hbm[klass(nm[d])][key] += val[d] * scale / S
+        for k in hbm:
+            hbm[k]["bytes"] = hbm[k]["fetch_bytes"] + hbm[k]["write_bytes"]
+        out["hbm"] = dict(hbm)
+        out["hbm_bytes_per_step"] = sum(v["bytes"] for v in hbm.values())
     # GRBM_GUI_ACTIVE / 8 / traced kernel time reads above the 2.4 GHz maximum here (the
     # counter is not a plain per-XCD cycle count on this ROCm), so the utilisation is quoted
     # against the peak clock: a lower bound on the busy fraction at the clock actually held
