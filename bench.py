@@ -288,11 +288,13 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
             row = {"step_ms": step_ms, "span_ms": (t[:, 1].max() - t[:, 0].min()) * 1e-5}
             dm = dims[a:b].astype(np.float64)
             for name, code in (("gemm", 1), ("attn", 2)):
-                sel = k == code
+                sel = (k == 1) | (k == 3) if code == 1 else k == code
                 iv = [(int(s_), int(e)) for s_, e in t[sel]]
                 d = dm[sel]
-                if code == 1:   # A + B + C once each, bf16: (M·K + N·K + M·N)·batch·2 B
-                    ab = float(((d[:, 0] * d[:, 2] + d[:, 1] * d[:, 2] + d[:, 0] * d[:, 1])
+                if code == 1:   # A + B + C once each, bf16: (M·K + N·K + M·N)·batch·2 B; an
+                    # implicit 3x3 conv (kind 3) reads its input image once: M·K/9 for A
+                    ka = np.where(k[sel] == 3, d[:, 2] / 9.0, d[:, 2])
+                    ab = float(((d[:, 0] * ka + d[:, 1] * d[:, 2] + d[:, 0] * d[:, 1])
                                 * d[:, 3] * 2).sum())
                 else:           # q, k, v read + o written once, bf16: 4·S·64·heads·batch·2 B
                     ab = float(((2 * d[:, 0] + 2 * d[:, 1]) * 64 * d[:, 2] * d[:, 3] * 2).sum())
@@ -324,7 +326,7 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
         t, k, fl, dm, sms = keep
         t0 = int(t[:, 0].min())
         js = {"step_ms": sms, "tick_ns": 10, "launches": [
-            {"kind": {1: "gemm", 2: "attn"}[int(kk)], "dims": [int(x) for x in d],
+            {"kind": {1: "gemm", 2: "attn", 3: "conv"}[int(kk)], "dims": [int(x) for x in d],
              "gflop": float(f) / 1e9, "start_us": (int(s_) - t0) * 1e-2,
              "end_us": (int(e) - t0) * 1e-2} for (s_, e), kk, f, d in zip(t, k, fl, dm)]}
         with open(out_path, "w") as fh:
@@ -420,7 +422,9 @@ def roofline_entry(tl, roof, pmc, mfma, step_ms):
              gemm_or_attn_union_ms=tl["gemm_or_attn_union_ms"])
     e["algorithmic_bytes_per_step"] = g["algorithmic_bytes"]
     e["algorithmic_bytes_rule"] = ("floor: every GEMM reads A and B and writes C once, bf16 "
-                                   "((M·K + N·K + M·N)·batch·2 B per launch, step_timeline dims)")
+                                   "((M·K + N·K + M·N)·batch·2 B per launch, step_timeline dims; "
+                                   "an implicit 3x3 conv reads its input image once: M·K/9 "
+                                   "for A)")
     if mfma:
         e["mfma_busy"] = mfma
         hb = (mfma.get("hbm") or {}).get("gemm")

@@ -50,7 +50,8 @@ int m3s_device_count(void);
  * [min of the starts, max of the ends]; the caller fills every pair with {UINT64_MAX, 0}
  * before a run).  A null d_buf
  * disarms it (later launches carry no slot).  m3s_timeline_count() = slots taken since the
- * last set; m3s_timeline_meta() copies their kinds (1 GEMM, 2 attention), algorithmic
+ * last set; m3s_timeline_meta() copies their kinds (1 GEMM, 2 attention, 3 implicit 3x3
+ * conv GEMM), algorithmic
  * FLOPs (2·M·N·K·batch; 4·Sq·Sk·64·heads·batch) and dims ({M, N, K, batch};
  * {Sq, Sk, heads, batch}) to host arrays of `capacity` entries (dims: [capacity][4]). */
 int m3s_timeline_set(void* d_buf, int capacity);

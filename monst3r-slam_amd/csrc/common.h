@@ -49,7 +49,7 @@ __device__ __forceinline__ double m3s_wave_sum_d(double v) {
 // atomics in series and stretched the step 1.4x.  The slot pointer travels in the kernel
 // arguments, so a captured graph keeps its launches' slots; with no buffer set the pointer
 // is null and the kernels only test it.
-enum { M3S_TL_GEMM = 1, M3S_TL_ATTN = 2 };
+enum { M3S_TL_GEMM = 1, M3S_TL_ATTN = 2, M3S_TL_CONV = 3 };  // CONV: implicit 3x3 GEMM
 #define M3S_TL_SUB 64
 unsigned long long* m3s_timeline_take(int kind, double flops, int64_t d0, int64_t d1, int64_t d2,
                                         int64_t d3);  // capi.cpp; null when off

@@ -171,7 +171,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   a.a_xor = 0;
   a.ln_c1 = d->ln_c1;
   a.ln_eps = d->ln_eps;
-  a.tl = m3s_timeline_take(M3S_TL_GEMM, 2.0 * d->M * d->N * d->K * d->batch, d->M, d->N, d->K,
+  a.tl = m3s_timeline_take(d->mode != 0 ? M3S_TL_CONV : M3S_TL_GEMM, 2.0 * d->M * d->N * d->K * d->batch, d->M, d->N, d->K,
                            d->batch);
   const bool ln_stats = d->flags & M3S_EPI_LN_STATS, ln_fold = d->flags & M3S_EPI_LN_FOLD;
   if (ln_stats || ln_fold) {

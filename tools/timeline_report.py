@@ -11,8 +11,9 @@ def main(path):
     L = d["launches"]
     ev = []
     for x in L:
-        ev.append((x["start_us"], 1, x["kind"]))
-        ev.append((x["end_us"], -1, x["kind"]))
+        kind = "gemm" if x["kind"] == "conv" else x["kind"]   # implicit-GEMM convs count as GEMM
+        ev.append((x["start_us"], 1, kind))
+        ev.append((x["end_us"], -1, kind))
     ev.sort()
     span = max(x["end_us"] for x in L) - min(x["start_us"] for x in L)
     conc = collections.Counter()
@@ -31,9 +32,9 @@ def main(path):
         active[k] += dlt
         t_prev = t
     print(f"step (HIP events) {d['step_ms']:.3f} ms; stamped span {span / 1e3:.3f} ms; "
-          f"{len(L)} launches ({sum(1 for x in L if x['kind'] == 'gemm')} GEMM, "
+          f"{len(L)} launches ({sum(1 for x in L if x['kind'] in ('gemm', 'conv'))} GEMM, "
           f"{sum(1 for x in L if x['kind'] == 'attn')} attention)")
-    gf = sum(x["gflop"] for x in L if x["kind"] == "gemm")
+    gf = sum(x["gflop"] for x in L if x["kind"] in ("gemm", "conv"))
     af = sum(x["gflop"] for x in L if x["kind"] == "attn")
     print(f"GEMM busy (union) {busy['gemm'] / 1e3:.3f} ms -> {gf / busy['gemm'] * 1e3:.0f} TF/s "
           f"({gf:.0f} GF); attention busy {busy['attn'] / 1e3:.3f} ms -> "
