@@ -37,10 +37,13 @@ def main():
         ms = bench.time_replays(g, dev, 5) / reps
         M, N, K, b, flags = key
         cin = K // 9
-        alg = (M * cin + N * K + M * N) * b * 2
+        # input image once (stride 1) + weights + output (the fused DPT tail writes 16 B
+        # per pixel instead of the 128-channel map)
+        out_b = M * 16 if flags & 512 else M * N * 2
+        alg = (M * cin * 2 + out_b) * b + N * K * 2
         print(f"conv M={M} N={N} K={K} b={b} flags={flags}: {ms * 1e3:.1f} us, "
               f"{fl / ms / 1e9:.0f} TF/s, algorithmic {alg / 1e6:.1f} MB "
-              f"({alg / ms / 1e9:.0f} GB/s)", flush=True)
+              f"({alg / ms / 1e6:.0f} GB/s)", flush=True)
         del g
 
 
