@@ -180,7 +180,7 @@ class Tracker:
 
 
 class FramePipeline:
-    """Streaming tracking with the next frames' encoder prefetched: the MonST3R encoder of a
+    """Streaming tracking with future frames' encoder prefetched: the MonST3R encoder of a
     future frame depends only on its image, so it runs on a side stream concurrently with
     the current frame's decoders, heads, matching and pose solve (which leave most CUs idle
     at 768 tokens).  Per-frame work and results are those of Tracker.track; only the
@@ -188,17 +188,17 @@ class FramePipeline:
 
     group = 1: step(k) tracks the frame encoded by the previous step into buffer k % 2 and
     encodes the next frame into buffer (k + 1) % 2 (24 dependent blocks per step).
-    group = 2: frames are encoded two at a time (M = 2 x 768 tokens per GEMM, one attention
-    launch for both), the 24 blocks spread over the two steps that track the previous pair:
-    step k runs blocks 0-11 (k even: embed the pair first) or 12-23 + enc_norm (k odd) of
-    the pair that steps k + 2 and k + 3 track — the side chain per step is half as long and
-    each launch twice as wide.  Feature slots: pair buffer (k // 2) % 2, row k % 2; the
-    graphs repeat with period 4 (`period`).  Frame latency +1 (features ready one step
-    earlier than needed)."""
+    group = g > 1: frames are encoded g at a time (M = g x 768 tokens per GEMM, one
+    attention launch for all), the 24 blocks spread over the g steps that track the
+    previous group: step k runs part k % g (blocks 24·p/g .. 24·(p+1)/g; part 0 embeds the
+    group first, part g-1 ends with enc_norm) of the group that steps
+    g·(k // g + 1) .. g·(k // g + 1) + g - 1 track.  Feature slots: group buffer
+    (k // g) % 2, row k % g; the graphs repeat with period 2g (`period`).  Frame latency
+    +g - 1 steps (features ready before they are needed)."""
 
     def __init__(self, tracker, shape_hw, side_priority=0, group=1):
-        if group not in (1, 2):
-            raise ValueError("group must be 1 or 2")
+        if group not in (1, 2, 3, 4, 6):
+            raise ValueError("group must divide the 24 encoder blocks and be <= 6")
         self.tr = tracker
         m = tracker.model
         H, W = shape_hw
@@ -210,9 +210,10 @@ class FramePipeline:
             self.feat = [torch.empty((1, S, m.a.enc_dim), dtype=torch.bfloat16, device=m.dev)
                          for _ in range(2)]
         else:
-            self.pairs = [torch.empty((2, S, m.a.enc_dim), dtype=torch.bfloat16, device=m.dev)
-                          for _ in range(2)]
-            self.feat = [self.pairs[j // 2][j % 2:j % 2 + 1] for j in range(4)]
+            self.pairs = [torch.empty((group, S, m.a.enc_dim), dtype=torch.bfloat16,
+                                      device=m.dev) for _ in range(2)]
+            self.feat = [self.pairs[j // group][j % group:j % group + 1]
+                         for j in range(2 * group)]
         self.side = torch.cuda.Stream(m.dev, priority=side_priority)
 
     def slot(self, k):
@@ -224,12 +225,20 @@ class FramePipeline:
         return self.feat[(k + 1) % 2] if self.group == 1 else None
 
     def prime(self, img, k=0):
-        """Encode the first frame (group 2: the first two frames, img [2,3,H,W]) into the
+        """Encode the first frame (group g: the first g frames, img [g,3,H,W]) into the
         buffer(s) step k tracks from (on the current stream)."""
         if self.group == 1:
             self.tr.model.encode(img, out=self.feat[k % 2])
         else:
-            self.tr.model.encode(img, out=self.pairs[(k // 2) % 2], concurrent=True)
+            self.tr.model.encode(img, out=self.pairs[(k // self.group) % 2], concurrent=True)
+
+    def _part(self, img_next, k, gen):
+        g = self.group
+        H, W = self.shape_hw
+        part = k % g
+        return self.tr.model.encode_part(
+            (g, 3, H, W), part, g, img=img_next if part == 0 else None,
+            out=self.pairs[(k // g + 1) % 2] if part == g - 1 else None, gen=gen)
 
     def encode_side_gen(self, img_next, k):
         """encode_side as a generator yielding after each encoder block (the caller issues
@@ -237,28 +246,22 @@ class FramePipeline:
         m = self.tr.model
         if self.group == 1:
             return m.encode_gen(img_next, out=self.feat[(k + 1) % 2], concurrent=True)
-        H, W = self.shape_hw
-        part = k % 2
-        return m.encode_part((2, 3, H, W), part, 2, img=img_next if part == 0 else None,
-                             out=self.pairs[(k // 2 + 1) % 2] if part == 1 else None, gen=True)
+        return self._part(img_next, k, True)
 
     def encode_side(self, img_next, k):
         """Issue step k's share of the prefetch on the current (side) stream: group 1 the
-        whole encoder of img_next [1,3,H,W]; group 2 half of the pair encode (img_next
-        [2,3,H,W] is read by the even step only)."""
+        whole encoder of img_next [1,3,H,W]; group g its part k % g of the group encode
+        (img_next [g,3,H,W] is read by part 0 only)."""
         m = self.tr.model
         if self.group == 1:
             m.encode(img_next, out=self.feat[(k + 1) % 2], concurrent=True)
             return
-        H, W = self.shape_hw
-        part = k % 2
-        m.encode_part((2, 3, H, W), part, 2, img=img_next if part == 0 else None,
-                      out=self.pairs[(k // 2 + 1) % 2] if part == 1 else None)
+        self._part(img_next, k, False)
 
     def step(self, img_cur, img_next, k, T_WCf_init=None):
         """group 1 only: track img_cur, prefetch img_next."""
         if self.group != 1:
-            raise RuntimeError("FramePipeline.step drives group=1; SequenceLoop drives group=2")
+            raise RuntimeError("FramePipeline.step drives group=1; SequenceLoop drives groups")
         main = torch.cuda.current_stream(self.tr.model.dev)
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):

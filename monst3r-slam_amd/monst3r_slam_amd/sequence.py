@@ -258,8 +258,8 @@ class SequenceLoop:
         if m is not None:
             if pipe is not None:
                 feat_i = pipe.slot(k)
-                # group 2: the odd step continues the pair encode its even step started
-                gathers = pipe.group == 1 or k % 2 == 0
+                # group g: only part 0 of a group encode reads the images
+                gathers = k % pipe.group == 0
                 dp = k % 2 if m.defer_mast3r else None
                 delay = m.layer_event_at is not None
                 if delay:   # the pair first: the encoder waits for its decoder layer event

