@@ -502,6 +502,7 @@ class PairModel:
         self.layer_event = None
         # split heads: the local-feature MLP runs on the side chain ahead of the MASt3R heads
         self.lf_side = os.environ.get("M3S_LF_SIDE", "1") != "0"
+        self.mast3r_own_stream = os.environ.get("M3S_MAST3R_STREAM", "0") == "1"
         self._tag = None      # buffer-key prefix of the head set being issued (split heads)
         self._wbase = 0       # first head-weight stack of that set
         self._wm = 4
@@ -1072,7 +1073,15 @@ class PairModel:
                     desc, desc16, dconf, _ = self._local_features(hooks, G, S, E, D, H, W)
                     ev_lf = torch.cuda.Event()
                     ev_lf.record(side)
-                sub = {k: v[2:4] for k, v in hooks.items()}
+            sub = {k: v[2:4] for k, v in hooks.items()}
+            # M3S_MAST3R_STREAM=1: the MASt3R heads on the decoder's second stream (idle by
+            # now) beside the local features instead of behind them on the side chain
+            hs = self.side[1] if self.mast3r_own_stream else side
+            if hs is not side:
+                hs.wait_stream(main)
+                for ev in self._early_ev:
+                    hs.wait_event(ev)
+            with torch.cuda.stream(hs):
                 self.ops.tile_default = st.get("dpt")
                 try:
                     # M3S_ABLATE_MAST3R_DPT=1: diagnostic ablation only (tools/step_ablation):
@@ -1083,7 +1092,7 @@ class PairModel:
                 finally:
                     self.ops.tile_default = None
                 self._ev_heads = torch.cuda.Event()
-                self._ev_heads.record(side)
+                self._ev_heads.record(hs)
         # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle
         if models == 2 and desc is None:
             self._wm = wm
