@@ -392,12 +392,16 @@ __device__ void track_solve(TrackState* st, const float* partial, int nblocks, f
 // (a workgroup can be at most one iteration ahead) and are zeroed per call (memset node).
 // tools/track_bench.py --stamps: 38 → 11 µs per iteration at 384x512 (the fence-ordered
 // barrier + a shuffle reduction per value were 27 µs of it).
-// Exit: convergence, Cholesky failure, max_iters, or a sweep beyond `spin_limit` polls
-// (co-residency broken) — that workgroup raises st->abort, every other workgroup sees it in
-// its own sweep (or at entry, if it only got a CU after the others left) and leaves too.  No
-// workgroup can complete the iteration that timed out, so workgroup 0 still holds the pose
-// after the last completed iteration and writes it back with done = 0;
-// track_finish_kernel then runs the remaining iterations.
+// Exit: convergence, Cholesky failure, max_iters, or a sweep beyond `spin_limit` granule
+// sweeps (co-residency broken; a sweep is up to one agent-scope load per producer workgroup,
+// so the wait before recovery is spin_limit x one sweep's latency, not a fixed time) — that
+// workgroup raises st->abort, every other workgroup sees it in its own sweep (or at entry,
+// if it only got a CU after the others left) and leaves too.  Another workgroup may still
+// see every granule of the iteration that timed out (the last one can land just as the
+// waiter gives up) and take that step before it notices the abort one iteration later:
+// correctness does not rest on "nobody completes it", but on workgroup 0 alone writing
+// back ITS OWN consistent (pose, iteration, cost) with done = 0; track_finish_kernel then
+// runs the remaining iterations from that state.
 // `abort_at` >= 0 forces that exit at iteration abort_at (tests of the recovery path).
 #ifdef M3S_TRACK_STAMPS
 // debug build (tools/track_bench.py --stamps): workgroup 0, lane 0, s_memrealtime (100 MHz)
