@@ -503,6 +503,7 @@ class PairModel:
         # split heads: the local-feature MLP runs on the side chain ahead of the MASt3R heads
         self.lf_side = os.environ.get("M3S_LF_SIDE", "1") != "0"
         self.mast3r_own_stream = os.environ.get("M3S_MAST3R_STREAM", "0") == "1"
+        self.mast3r_late = os.environ.get("M3S_MAST3R_LATE", "0") == "1"
         self._tag = None      # buffer-key prefix of the head set being issued (split heads)
         self._wbase = 0       # first head-weight stack of that set
         self._wm = 4
@@ -1073,6 +1074,7 @@ class PairModel:
                     desc, desc16, dconf, _ = self._local_features(hooks, G, S, E, D, H, W)
                     ev_lf = torch.cuda.Event()
                     ev_lf.record(side)
+        def _mast3r_heads():
             sub = {k: v[2:4] for k, v in hooks.items()}
             # M3S_MAST3R_STREAM=1: the MASt3R heads on the decoder's second stream (idle by
             # now) beside the local features instead of behind them on the side chain
@@ -1093,6 +1095,9 @@ class PairModel:
                     self.ops.tile_default = None
                 self._ev_heads = torch.cuda.Event()
                 self._ev_heads.record(hs)
+
+        if split and not self.mast3r_late:
+            _mast3r_heads()
         # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle
         if models == 2 and desc is None:
             self._wm = wm
@@ -1105,6 +1110,10 @@ class PairModel:
             sub = {k: v[0:2] for k, v in hooks.items()}
             self._dpt(sub, gh, gw, H, W, 2, 0, 2, None, pts[0:2], conf[0:2],
                       R=None if R is None else [r[0:2] for r in R])
+            if self.mast3r_late:
+                # M3S_MAST3R_LATE=1: the MASt3R heads captured after the MonST3R heads
+                # (same streams and dependencies, later in the graph's node order)
+                _mast3r_heads()
         else:
             self._dpt(hooks, gh, gw, H, W, Z, 0, wm, None, pts, conf, R=R)
         self._wait(ev_lf)
