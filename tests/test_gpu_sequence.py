@@ -246,3 +246,32 @@ def test_c3_sequence_200_pipelined_vs_oracle(dev, parity_log):
                new_keyframes=n_new, idx_valid="bit-exact", max_abs_dT=dT_max, tol_dT=1e-4,
                ate_m=ate, prefetched_features_checked=n_feat,
                gn_iterations_hist=summ["gn_iterations_hist"])
+
+
+@pytest.mark.parametrize("group", [3, 4])
+def test_grouped_prefetch_encodes_the_right_frames(dev, group):
+    """FramePipeline(group=g) through SequenceLoop: every completed g-frame group of
+    prefetched features equals one direct g-frame encode of exactly the frames the next g
+    steps track (part 0 gathers frames t + g .. t + 2g - 1, part g - 1 writes the buffer),
+    over two full periods replayed from the captured step graphs."""
+    import bench
+    from monst3r_slam_amd import sequence as S
+    from monst3r_slam_amd.frontend import FramePipeline
+    model, tr, seq = bench.setup(dev, 0, 6 * group + 2)
+    pipe = FramePipeline(tr, (seq.h, seq.w), group=group)
+    loop = S.SequenceLoop(tr, seq, pipe)
+    loop.reset(parity=0)
+    graphs = [bench.capture(lambda k=k: loop.step(k), dev) for k in range(pipe.period)]
+    loop.reset(parity=0)
+    torch.cuda.synchronize()
+    checked = 0
+    for i in range(2 * pipe.period):
+        graphs[i % pipe.period].replay()
+        if i % group == group - 1:
+            torch.cuda.synchronize()
+            f0 = i + 2                         # first frame the next group of steps tracks
+            got = pipe.pairs[(i // group + 1) % 2].clone()
+            imgs = seq.img[f0:f0 + group].reshape(group, 3, seq.h, seq.w)
+            assert torch.equal(got, model.encode(imgs, concurrent=True)[0]), i
+            checked += 1
+    assert checked == 2 * pipe.period // group
