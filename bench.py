@@ -64,23 +64,15 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="skip the fp8 512x512 dyn-mask leg")
     ap.add_argument("--no-retrieval", action="store_true",
                     help="skip the keyframe-retrieval (loop-closure candidate) leg")
-    ap.add_argument("--main-priority", type=int, default=0, help="tracking-chain stream priority")
-    ap.add_argument("--side-priority", type=int, default=0, help="prefetch stream priority")
     ap.add_argument("--no-split-heads", action="store_true",
                     help="run the MASt3R DPT heads batched on the tracking chain")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="encode each frame inside its own step (no next-frame encoder overlap)")
-    ap.add_argument("--streams", action="store_true",
-                    help="overlap independent chains on side streams (measured slower)")
-    ap.add_argument("--prefetch-after", type=int, default=None,
-                    help="start the next frame's encoder after this MonST3R decoder layer "
-                         "(default: at the step's start)")
-    ap.add_argument("--defer-mast3r", type=int, default=None,
-                    help="1: run each frame's MASt3R DPT heads (outputs unread by the "
-                         "tracking) during the next frame's decoder; 0: at the frame's end")
     ap.add_argument("--group", type=int, default=2,
                     help="frames per prefetched encoder batch (1: the next frame's encoder each "
                          "step; 2: two frames at M = 1536, spread over two steps)")
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="(tests) each rank only joins a gloo group and reports; no GPU work")
     ap.add_argument("--timeline-out", default=None,
                     help="write one replayed step's per-launch GEMM / attention timeline (JSON)")
     ap.add_argument("--no-timeline", action="store_true",
@@ -176,18 +168,12 @@ def kernel_rooflines(tr, out, dev):
     return res
 
 
-def capture(fn, dev, priority=0):
-    s = torch.cuda.Stream(dev, priority=priority)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(s):
-        fn()
-    torch.cuda.current_stream(dev).wait_stream(s)
-    torch.cuda.synchronize(dev)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
-        fn()
-    torch.cuda.synchronize(dev)
-    return g
+def capture(fn, dev):
+    """fn run once eagerly, then captured into a HIP graph with its stream fork / join
+    topology checked before capture_end (capture.capture_graph: TopologyError, not a
+    runtime segfault, on an unjoined side stream or a capture wider than the HW queues)."""
+    from monst3r_slam_amd.capture import capture_graph
+    return capture_graph(fn, dev)
 
 
 def time_replays(g, dev, n):
@@ -236,13 +222,9 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
     def cap_tl(k):
         loop.step(k)                      # warm / allocate outside the timeline
         torch.cuda.synchronize(dev)
-        s = torch.cuda.Stream(dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        g = torch.cuda.CUDAGraph()
         n0 = int(lib.m3s_timeline_count())
-        with torch.cuda.graph(g, stream=s):
-            loop.step(k)
-        torch.cuda.synchronize(dev)
+        from monst3r_slam_amd.capture import capture_graph
+        g = capture_graph(lambda: loop.step(k), dev, warmup=False)
         return g, n0, int(lib.m3s_timeline_count())
 
     _lib.check(lib.m3s_timeline_set(P(buf), cap), "timeline_set")
@@ -540,7 +522,7 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
     graph._solve_sharded("rays")
     gn_ms = (time.perf_counter() - t1) * 1e3
     gn_it = max(1, int(graph.gn_iterations))
-    valid_frac = float(graph.valid_match_j.float().mean()) if graph.valid_match_j.numel() else 0.0
+    valid_frac = graph.valid_match_fraction()   # every rank's accepted edges (all-reduce)
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -844,30 +826,70 @@ def sequence_report(loop, seq, steps):
             "ate_rmse_m": ate}
 
 
+def launch_ranks(n, argv):
+    """`--gpus N` with no launcher around this process: start N ranks of this same script
+    under torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1, RCCL between
+    them), wait for them and exit with their status.  Only torch.cuda.device_count() is
+    called first (it does not initialise the GPU), and N above it is an error, never a
+    silent fallback to fewer ranks.  Rank 0 prints the one JSON line."""
+    import socket
+    import subprocess
+    if "--launcher-selftest" not in argv:
+        avail = torch.cuda.device_count()
+        if n > avail:
+            sys.stderr.write(f"bench.py --gpus {n}: only {avail} GPU(s) visible\n")
+            sys.exit(2)
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL on this host
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def launcher_selftest(world, rank):
+    """What each rank of a launched `--gpus N` job sees (gloo, no GPU): world size, its
+    rank, and every rank's id gathered — the CPU test of launch_ranks."""
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    got = [None] * dist.get_world_size()
+    dist.all_gather_object(got, (rank, os.environ.get("LOCAL_RANK")))
+    if rank == 0:
+        print(json.dumps({"launcher_selftest": True, "n_gpus": dist.get_world_size(),
+                          "world_env": world, "ranks": got}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        launch_ranks(args.gpus, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}\n")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
+    if args.launcher_selftest:
+        launcher_selftest(world, rank)
+        return
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
+        world = dist.get_world_size()          # n_gpus as RCCL sees it
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     n_frames = max(SEQ_FRAMES, args.steps, args.warmup + 2) + 1
     model, tr, seq = setup(dev, rank, n_frames)
-    model.serial = not args.streams
     tr.split_heads = not args.no_split_heads
-    if args.prefetch_after is not None:
-        model.layer_event_at = args.prefetch_after
-    if args.defer_mast3r is not None:
-        model.defer_mast3r = bool(args.defer_mast3r)
 
     from monst3r_slam_amd import sequence as S
     from monst3r_slam_amd.frontend import FramePipeline
-    pipe = None if args.no_prefetch else FramePipeline(tr, (H, W), args.side_priority,
-                                                       group=args.group)
+    pipe = None if args.no_prefetch else FramePipeline(tr, (H, W), group=args.group)
     loop = S.SequenceLoop(tr, seq, pipe)
     loop.reset(parity=0)
     for w in range(args.warmup):
@@ -875,7 +897,7 @@ def main():
     torch.cuda.synchronize(dev)
     # one graph per step of the prefetch period (feature slots rotated), replayed in turn
     period = pipe.period if pipe is not None else 2
-    graphs = None if args.eager else [capture(lambda k=k: loop.step(k), dev, args.main_priority)
+    graphs = None if args.eager else [capture(lambda k=k: loop.step(k), dev)
                                       for k in range(period)]
     elapsed = run_sequence(loop, graphs, args.steps, dev, world)
 

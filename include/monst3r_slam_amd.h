@@ -78,16 +78,6 @@ int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21, const int64
                        int64_t* d_p1_new, int64_t b, int64_t h, int64_t w, int64_t n,
                        int64_t fdim, int radius, int dilation_max, void* stream);
 
-/* refine_matches in the reference configuration (F = 24, radius 3, n == h*w) reading D11 in
- * chunk-planar layout [b][3][h*w][8] f16 (written by m3s_desc_planar or by
- * m3s_vit_local_features_planar): results identical to m3s_refine_matches on the same
- * descriptors; the layout coalesces the candidate loads.  D21 stays [b][h*w][24]. */
-int m3s_refine_matches_planar(const uint16_t* d_D11p, const uint16_t* d_D21, const int64_t* d_p1,
-                              int64_t* d_p1_new, int64_t b, int64_t h, int64_t w, int radius,
-                              int dilation_max, void* stream);
-/* [b][n][24] f16 descriptor rows → chunk-planar [b][3][n][8] (16-B aligned buffers). */
-int m3s_desc_planar(const uint16_t* d_D, uint16_t* d_Dp, int64_t b, int64_t n, void* stream);
-
 /* Fused replacement for matching.prep_for_iter_proj (matching.py:25-49) and
  * image.img_gradient (image.py:5-38): rays = X11/max(|X11|,1e-12);
  * g{x,y} = 3×3 Scharr/32 on reflect-padded rays;  pts = X21/max(|X21|,1e-12);
@@ -389,35 +379,6 @@ int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q, const voi
                       int64_t stride_o, int o_fp8, int64_t batch, int64_t heads, int64_t sq,
                       int64_t sk, float rope_base, void* d_workspace, int64_t workspace_bytes,
                       int kv_batch_xor, void* stream);
-
-/* Cross-attention with the q projection fused in (the pair decoder's cross block,
- * croco/blocks.py:180-185: q = projq(norm2(x)) with RoPE2D, then attention over k / v):
- * each workgroup computes its Q tile from the bf16 LayerNorm input x and the producer's
- * per-128-column (mean, M2) statistics, q = RoPE(rstd·(x Wᵀ − mean·c1) + c2) with the
- * gamma-folded weight W (model.ln_fold) — the same arithmetic, MFMA order and epilogue as
- * m3s_vit_gemm with M3S_EPI_LN_FOLD | M3S_EPI_ROPE | M3S_EPI_BIAS unsplit, so the output
- * equals that GEMM followed by m3s_vit_attention bit for bit.  Head dim 64; k % 128 == 0,
- * k ≤ 1024; q columns = heads·64; problem z uses weight / c1 / c2 set z % weight_mod
- * (weight_mod 0: z). */
-typedef struct m3s_qproj_desc {
-  const void* x;            /* bf16 [batch][sq][k] (ld_x, stride_x elements) */
-  int64_t ld_x, stride_x;
-  const float* stats;       /* f32 [batch][sq][k/128][2] */
-  const void* w;            /* bf16 [weight_mod][heads*64][k] (stride_w elements) */
-  int64_t stride_w;
-  int32_t weight_mod;
-  const float* c1;          /* f32 [weight_mod][heads*64] (stride_c) */
-  const float* c2;
-  int64_t stride_c;
-  const float* rope_table;  /* f32 [rope_tokens][2][32] (m3s_vit_rope_table) */
-  int64_t rope_tokens;
-  int64_t k;
-  float ln_eps;
-} m3s_qproj_desc;
-int m3s_vit_attention_qproj(const m3s_qproj_desc* d, const void* d_k, const void* d_v,
-                            int64_t ld_kv, int64_t stride_kv, void* d_o, int64_t ld_o,
-                            int64_t stride_o, int64_t batch, int64_t heads, int64_t sq,
-                            int64_t sk, int kv_batch_xor, void* stream);
 
 /* Patch-embed im2col: img f32 NCHW [B][3][H][W] → bf16 [B][(H/16)(W/16)][3*16*16]
  * with K ordered (c, ky, kx) like the conv weight [1024][3][16][16]. */

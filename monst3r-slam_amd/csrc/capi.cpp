@@ -1,4 +1,5 @@
 // Library-level entry points of the C ABI (include/monst3r_slam_amd.h).
+#include <mutex>
 #include <vector>
 #include <hip/hip_runtime.h>
 #include "../../include/monst3r_slam_amd.h"
@@ -19,7 +20,10 @@ extern "C" int m3s_version(void) { return (0 << 16) | (1 << 8) | 0; }
 
 // ---- step timeline (common.h) ----
 #define M3S_TL_SUB_HOST 64   // = M3S_TL_SUB: stamp pairs per slot
+// The slot globals are shared by every host thread that launches (a mutex: two threads
+// capturing at once must not hand out one slot twice or tear the metadata vectors).
 namespace {
+std::mutex g_tl_mu;
 unsigned long long* g_tl = nullptr;
 int g_tl_cap = 0, g_tl_n = 0;
 std::vector<int> g_tl_kind;
@@ -29,6 +33,7 @@ std::vector<int64_t> g_tl_dims;
 
 unsigned long long* m3s_timeline_take(int kind, double flops, int64_t d0, int64_t d1, int64_t d2,
                                       int64_t d3) {
+  std::lock_guard<std::mutex> lk(g_tl_mu);
   if (!g_tl || g_tl_n >= g_tl_cap) return nullptr;
   g_tl_kind.push_back(kind);
   g_tl_flops.push_back(flops);
@@ -38,6 +43,7 @@ unsigned long long* m3s_timeline_take(int kind, double flops, int64_t d0, int64_
 
 extern "C" int m3s_timeline_set(void* d_buf, int capacity) {
   if (d_buf && capacity <= 0) return M3S_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(g_tl_mu);
   g_tl = reinterpret_cast<unsigned long long*>(d_buf);
   g_tl_cap = d_buf ? capacity : 0;
   if (d_buf) {
@@ -49,10 +55,14 @@ extern "C" int m3s_timeline_set(void* d_buf, int capacity) {
   return M3S_OK;
 }
 
-extern "C" int m3s_timeline_count(void) { return g_tl_n; }
+extern "C" int m3s_timeline_count(void) {
+  std::lock_guard<std::mutex> lk(g_tl_mu);
+  return g_tl_n;
+}
 
 extern "C" int m3s_timeline_meta(int* kinds, double* flops, int64_t* dims, int capacity) {
   if (!kinds || !flops || !dims || capacity < 0) return M3S_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(g_tl_mu);
   for (int i = 0; i < g_tl_n && i < capacity; i++) {
     kinds[i] = g_tl_kind[i];
     flops[i] = g_tl_flops[i];

@@ -251,13 +251,7 @@ __global__ __launch_bounds__(kBlock) void refine_matches_kernel(
 //    is remapped so each XCD takes a contiguous band of tiles and its L2 holds one band's
 //    windows instead of windows from all over the image;
 //  * 32-bit in-image offsets (h*w < 2^31 is checked by the host).
-// PLANAR: D11 in chunk-planar layout [b][3][h*w][8] (m3s_desc_planar): the c-th 16-B
-// chunk of 16 neighbouring candidates is one contiguous 256-B run, so a wave's candidate
-// load touches 2 cache lines per query row instead of the 6 of the interleaved [h*w][24]
-// rows read 16 B out of every 48 (the kernel is bound by the vector-memory address path:
-// 3 loads x lines touched per candidate, not by its f16 VALU work).  Same scores, order
-// and results.
-template <int R, bool PLANAR = false>
+template <int R>
 __global__ __launch_bounds__(kBlock) void refine_matches_r_kernel(
     const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
     const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
@@ -301,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void refine_matches_r_kernel(
         const int off = ok[jj] ? (int)v * w + (int)u : 0;
 #pragma unroll
         for (int c = 0; c < 3; c++)
-          buf[jj][c] = PLANAR ? img[(int64_t)c * n + off] : img[off * 3 + c];
+          buf[jj][c] = img[off * 3 + c];
       }
 #pragma unroll
       for (int jj = 0; jj < S; jj++) {
@@ -482,49 +476,6 @@ extern "C" int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21,
                        m3s_stream(stream), D11, D21, d_p1, d_p1_new, (int)h, (int)w, n,
                        (int)fdim, radius, dilation_max);
   }
-  M3S_LAUNCH_CHECK();
-  return M3S_OK;
-}
-
-// [b][n][24] f16 descriptor rows → chunk-planar [b][3][n][8] (refine_matches_r_kernel
-// PLANAR): one 16-B chunk per thread, coalesced 16-B loads and stores.
-__global__ __launch_bounds__(kBlock) void desc_planar_kernel(const uint4* __restrict__ src,
-                                                             uint4* __restrict__ dst, int64_t n,
-                                                             int64_t total) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // (b, c, pixel)
-  if (i >= total) return;
-  const int64_t pix = i % n, bc = i / n, c = bc % 3, b = bc / 3;
-  dst[i] = src[(b * n + pix) * 3 + c];
-}
-
-extern "C" int m3s_desc_planar(const uint16_t* d_D, uint16_t* d_Dp, int64_t b, int64_t n,
-                               void* stream) {
-  if (b < 0 || n < 0) return M3S_ERR_INVALID_ARG;
-  if (b == 0 || n == 0) return M3S_OK;
-  if (!d_D || !d_Dp || (((uintptr_t)d_D | (uintptr_t)d_Dp) % 16)) return M3S_ERR_INVALID_ARG;
-  const int64_t total = b * 3 * n;
-  hipLaunchKernelGGL(desc_planar_kernel, dim3(m3s_div_up(total, kBlock)), dim3(kBlock), 0,
-                     m3s_stream(stream), reinterpret_cast<const uint4*>(d_D),
-                     reinterpret_cast<uint4*>(d_Dp), n, total);
-  M3S_LAUNCH_CHECK();
-  return M3S_OK;
-}
-
-extern "C" int m3s_refine_matches_planar(const uint16_t* d_D11p, const uint16_t* d_D21,
-                                         const int64_t* d_p1, int64_t* d_p1_new, int64_t b,
-                                         int64_t h, int64_t w, int radius, int dilation_max,
-                                         void* stream) {
-  if (b < 0 || h < 1 || w < 1) return M3S_ERR_INVALID_ARG;
-  if (b == 0) return M3S_OK;
-  if (!d_D11p || !d_D21 || !d_p1 || !d_p1_new) return M3S_ERR_INVALID_ARG;
-  if ((((uintptr_t)d_D11p | (uintptr_t)d_D21) % 16)) return M3S_ERR_INVALID_ARG;
-  if (radius != 3) return M3S_ERR_INVALID_ARG;   // the reference configuration only
-  if (b > 65535 || h * w >= (1LL << 31)) return M3S_ERR_TOO_LARGE;
-  dim3 grid2((unsigned)(m3s_div_up(w, 16) * m3s_div_up(h, 16)), (unsigned)b);
-  hipLaunchKernelGGL((refine_matches_r_kernel<3, true>), grid2, dim3(kBlock), 0,
-                     m3s_stream(stream), reinterpret_cast<const _Float16*>(d_D11p),
-                     reinterpret_cast<const _Float16*>(d_D21), d_p1, d_p1_new, (int)h, (int)w,
-                     dilation_max);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }

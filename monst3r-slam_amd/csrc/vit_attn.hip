@@ -131,48 +131,15 @@ constexpr int RED_FLOATS = 8 * 64 * 4 + 64 * 2;  // one wave's partial: O^T 32x6
 // variant instantiated, and only in the peeled last trip: with both variants in the loop
 // the compiler merged them into one block that ran the MFMAs and softmax of BOTH and
 // selected the results (32 MFMAs, 855 instructions per tile instead of 16 / 422).
-// Fused cross-attention q projection (QP): the block computes its own Q tile,
-//   q = RoPE(rstd·(x Wq'ᵀ − mean·c1) + c2)  (the LayerNorm-folded q GEMM of the decoder,
-//   croco/blocks.py:180-185 norm2 + projq, with RoPE2D on q),
-// for its AW·32 query rows and head h from the bf16 LN input x and the producer's row
-// statistics, instead of reading q written by a separate GEMM launch.  The K loop, the
-// MFMA shape / operand order and the epilogue arithmetic are the GEMM's (vit_gemm_kern.h
-// ln_row_stats, the LN_FOLD epilogue, rope8), so Q — and the attention output — are
-// bit-identical to the two-launch path with an unsplit q GEMM.
-struct QProj {
-  const bf16_t* x;      // [batch][Sq][K] bf16 rows (ld ldx, batch stride sx)
-  int64_t ldx, sx;
-  const float* stats;   // [batch][Sq][K/128] (mean, M2) of x's producer
-  const bf16_t* w;      // [wmod][heads·64][K] gamma-folded q weight (stride sw)
-  int64_t sw;
-  int wmod;
-  const float* c1;      // [wmod][heads·64] row sums of w, stride sc
-  const float* c2;      // [wmod][heads·64] folded bias, stride sc
-  int64_t sc;
-  const float* rope;    // [rope_tokens][2][32] cos | sin (rope_table_kernel)
-  int rope_tokens;
-  int K;
-  float eps;
-};
-constexpr int QP_A_BYTES = 128 * 128;                // 128 rows x 64 k bf16
-constexpr int QP_B_BYTES = 64 * 128;                 // 64 cols x 64 k bf16
-constexpr int QP_ST = QP_A_BYTES + QP_B_BYTES;       // one k-chunk stage
-constexpr int QP_NST = 5;                            // stages: 4 k-chunks in flight
-constexpr int QP_QROW = 144;                         // Q tile row pitch (64 bf16 + 16 B)
-// the Q tile and row statistics reuse the stage buffers once the k loop is done
-constexpr int QP_LDS = QP_NST * QP_ST;
-static_assert(128 * QP_QROW + 128 * 8 <= QP_LDS, "Q tile fits the stages");
-
 // (A 3-stage K/V ring for the 2-key-split blocks — two key tiles in flight behind the one
 // being computed, one block per CU — measured 228.1 vs 230.5 frames/s in the C3 step:
 // removed)
-template <int AW, int KS, bool TAILS, bool QP = false>
+template <int AW, int KS, bool TAILS>
 __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
     const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, void* __restrict__ o,
     int64_t ldo, int64_t so_b, int o_fp8, int Sq, int Sk, int heads, float c_log2, int splits,
-    int tiles_per_split, float* __restrict__ part, int kv_xor, unsigned long long* tl,
-    QProj qp) {
+    int tiles_per_split, float* __restrict__ part, int kv_xor, unsigned long long* tl) {
   m3s_tl_begin(tl);
   const M3sTlEnd tl_end{tl};
   constexpr int GT = AW * 64;                        // threads of one key-split group
@@ -180,10 +147,8 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
   constexpr int NST = KS == 1 ? ASTAGES : 2;         // ring depth per key split
   static_assert(KS == 1 || (KS - 1) * AW * RED_FLOATS * 4 <= KS * NST * STAGE_BYTES,
                 "partials must fit in the ring");
-  static_assert(!QP || (AW == 4 && KS == 2), "q projection: 4 query waves x 2 key splits");
   constexpr int RING_BYTES = KS * NST * STAGE_BYTES;
-  constexpr int LDS_BYTES = QP && QP_LDS > RING_BYTES ? QP_LDS : RING_BYTES;
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[RING_BYTES];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wall = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -215,119 +180,9 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
   const int qrow = q0 + r;
   bf16x8 qf[4];
   const bf16x8 zero8 = {};
-  if constexpr (QP) {
-    // ---- the block's Q tile [128 queries][64 d] = LN-folded x Wq'ᵀ + RoPE ----
-    (void)Q;
-    char* const sQ = lds;
-    float2* const sS = reinterpret_cast<float2*>(sQ + 128 * QP_QROW);
-    const int qb0 = qt * (AW * QT);                  // first query row of the block
-    const int wsel = qp.wmod > 0 ? (int)(b % qp.wmod) : (int)b;
-    const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<bf16_t*>(qp.x + b * qp.sx), (short)0, 0x7ffffff0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<bf16_t*>(qp.w + (int64_t)wsel * qp.sw + (int64_t)h * HD * qp.K), (short)0,
-        0x7ffffff0, 0x00020000);
-    // DMA chunks (16 B): A = 128 rows x 8 chunks (2 per thread), B = 64 rows x 8 (1 per
-    // thread); chunk c lands at image row c >> 3, slot c & 7 and carries logical k-chunk
-    // slot ^ k_swz(row) (the K-tile image and swizzle of the attention main loop)
-    uint32_t xa_off[2];
 #pragma unroll
-    for (int i = 0; i < 2; i++) {
-      const int c = i * 512 + tid, row = c >> 3, slot = c & 7;
-      xa_off[i] = qb0 + row < Sq
-                      ? (uint32_t)(((int64_t)(qb0 + row) * qp.ldx + (slot ^ k_swz(row)) * 8) * 2)
-                      : OOB;
-    }
-    const uint32_t wb_off =
-        (uint32_t)(((int64_t)(tid >> 3) * qp.K + ((tid & 7) ^ k_swz(tid >> 3)) * 8) * 2);
-    // 3 DMA instructions per thread and k-chunk; QP_NST - 1 chunks in flight (the chunks
-    // are short: with one in flight the loop paid an L2 round trip per chunk)
-    auto issue_qp = [&](int kc, int buf) {
-      const uint32_t k0 = (uint32_t)kc * 64 * 2;
-      char* st = lds + buf * QP_ST;
-#pragma unroll
-      for (int i = 0; i < 2; i++)
-        glds16(rX, st + (i * 512 + wall * 64) * 16, xa_off[i] == OOB ? OOB : xa_off[i] + k0);
-      glds16(rW, st + QP_A_BYTES + (wall * 64) * 16, wb_off + k0);
-    };
-    const int rg = wall & 3, cg = wall >> 2;         // this wave's 32 rows / 32 columns
-    f32x16 qacc;
-#pragma unroll
-    for (int i = 0; i < 16; i++) qacc[i] = 0.f;
-    const int nkc = qp.K / 64;
-#pragma unroll
-    for (int t = 0; t < QP_NST - 1; t++)
-      if (t < nkc) issue_qp(t, t);
-    for (int t = 0; t < nkc; t++) {
-      // retire chunk t; min(QP_NST - 2, nkc - 1 - t) younger chunks stay in flight
-      const int ahead = min(QP_NST - 2, nkc - 1 - t);
-      if (ahead >= 3) vm_wait<9>();
-      else if (ahead == 2) vm_wait<6>();
-      else if (ahead == 1) vm_wait<3>();
-      else vm_wait<0>();
-      block_sync_lds();                              // chunk t visible; t - 1 fully read
-      if (t + QP_NST - 1 < nkc) issue_qp(t + QP_NST - 1, (t + QP_NST - 1) % QP_NST);
-      const char* a_img = lds + (t % QP_NST) * QP_ST;
-      const char* b_img = a_img + QP_A_BYTES;
-      const int ar = rg * 32 + r, br = cg * 32 + r;
-#pragma unroll
-      for (int kk = 0; kk < 4; kk++) {
-        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(
-            a_img + ar * 128 + (((2 * kk + hh) ^ k_swz(ar)) * 16));
-        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(
-            b_img + br * 128 + (((2 * kk + hh) ^ k_swz(br)) * 16));
-        qacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, qacc, 0, 0, 0);
-      }
-    }
-    block_sync_lds();                                // stage buffers free for the Q tile
-    // row statistics (vit_gemm_kern.h ln_row_stats, same order) of the block's 128 rows
-    if (tid < 128) {
-      const int m = qb0 + tid;
-      float2 st8[8];
-      const int groups = qp.K >> 7;
-      const float2* st = reinterpret_cast<const float2*>(qp.stats) + (b * Sq + m) * groups;
-#pragma unroll
-      for (int t = 0; t < 8; t++) st8[t] = (t < groups && m < Sq) ? st[t] : make_float2(0.f, 0.f);
-      float sm = 0.f, m2 = 0.f;
-#pragma unroll
-      for (int t = 0; t < 8; t++) sm += st8[t].x;
-      const float mean = sm / (float)groups;
-#pragma unroll
-      for (int t = 0; t < 8; t++) {
-        const float d = t < groups ? st8[t].x - mean : 0.f;
-        m2 += fmaf(128.f * d, d, st8[t].y);
-      }
-      sS[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (128.f * (float)groups) + qp.eps));
-    }
-    block_sync_lds();
-    // LN_FOLD epilogue + RoPE (rope8: pairs (i, i + 16) of each 32-wide half; the partner
-    // column is lane r ^ 16), bf16 into the Q tile
-    const int nl = cg * 32 + r;                      // column inside the head
-    const int n = h * HD + nl;
-    const float c1v = qp.c1[wsel * qp.sc + n], c2v = qp.c2[wsel * qp.sc + n];
-    const int i0 = r & 15;
-    const float sg = (r & 16) ? 1.f : -1.f;          // lower: u c - v s; upper: v c + u s
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int rl = rg * 32 + 8 * (i >> 2) + 4 * hh + (i & 3);
-      const float2 ms = sS[rl];
-      const float xv = fmaf(ms.y, fmaf(-ms.x, c1v, qacc[i]), c2v);
-      const float pv = __shfl_xor(xv, 16, 64);
-      const int m = qb0 + rl;
-      const float* tt = qp.rope + ((int64_t)(m % qp.rope_tokens) * 2 + cg) * 32;
-      const float val = xv * tt[i0] + sg * pv * tt[16 + i0];
-      *reinterpret_cast<bf16_t*>(sQ + rl * QP_QROW + nl * 2) = m < Sq ? f2bf(val) : f2bf(0.f);
-    }
-    block_sync_lds();
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++)
-      qf[ks] = *reinterpret_cast<const bf16x8*>(sQ + (wid * QT + r) * QP_QROW + (ks * 16 + 8 * hh) * 2);
-    block_sync_lds();                                // Q tile read before the K/V ring reuses it
-  } else {
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++)
-      qf[ks] = qrow < Sq ? load8(Q + (int64_t)qrow * ldq + ks * 16 + 8 * hh) : zero8;
-  }
+  for (int ks = 0; ks < 4; ks++)
+    qf[ks] = qrow < Sq ? load8(Q + (int64_t)qrow * ldq + ks * 16 + 8 * hh) : zero8;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // Q ready before the DMA queue fills
   // launder: the compiler would otherwise wait vmcnt(0) (draining the DMA ring) at every
   // use of these ordinary-load results inside the loop
@@ -569,301 +424,6 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
     }
 }
 
-// Ping-pong variant of attn_kernel for 8-wave blocks (AW x KS = 8, KS = 2 or 4): the same
-// per-wave arithmetic in the same order (bit-identical results), scheduled so that each
-// SIMD's two waves — w and w + 4, i.e. the early and the late half of the key splits —
-// alternate between a matrix block and a vector block instead of running both in lockstep
-// behind one barrier per tile:
-//   M(j) = P·V of tile j-1 + S = K·Qᵀ of tile j   (16 MFMAs)
-//   V(j) = online softmax of tile j                (exp / max / sum / rescale: VALU)
-// Half-period h (one block barrier each): the early groups run M(h/2) / V((h-1)/2) for even /
-// odd h, the late groups the same one half-period later, so while one wave of a SIMD
-// keeps the matrix pipe busy its partner issues the softmax (cdna_hip_programming.md
-// 'Two waves per SIMD'; the lockstep loop serialised MFMA and softmax on every SIMD).
-// Ring: NST slots per key split; tile j+1 is issued at M(j) (3 slots) or V(j) (2 slots:
-// its slot held tile j-1, read by M(j)'s P·V), and retired (vmcnt 0) before M(j+1).
-template <int AW, int KS, bool TAILS>
-__global__ __launch_bounds__(AW * KS * 64, 1) void attn_pp_kernel(
-    const bf16_t* __restrict__ q, int64_t ldq, int64_t sq_b, const bf16_t* __restrict__ k,
-    const bf16_t* __restrict__ v, int64_t ldkv, int64_t skv_b, void* __restrict__ o,
-    int64_t ldo, int64_t so_b, int o_fp8, int Sq, int Sk, int heads, float c_log2, int splits,
-    int tiles_per_split, float* __restrict__ part, int kv_xor, unsigned long long* tl) {
-  static_assert(AW * KS == 8 && (KS == 2 || KS == 4), "8 waves: w and w + 4 share a SIMD");
-  m3s_tl_begin(tl);
-  const M3sTlEnd tl_end{tl};
-  constexpr int GT = AW * 64;
-  constexpr int ACH = TILE_BYTES / 16 / GT;
-  constexpr int NST = KS == 2 ? 3 : 2;
-  static_assert((KS - 1) * AW * RED_FLOATS * 4 <= KS * NST * STAGE_BYTES, "merge space");
-  __shared__ __attribute__((aligned(16))) char lds[KS * NST * STAGE_BYTES];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wall = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wid = wall % AW;
-  const int ksp = wall / AW;
-  const bool late = ksp >= KS / 2;    // waves 4..7
-  const int gtid = tid - ksp * GT;
-  char* const ring = lds + ksp * NST * STAGE_BYTES;
-  const int r = lane & 31, hh = lane >> 5;
-  const int nqt = (Sq + AW * QT - 1) / (AW * QT);
-  const int total = gridDim.x, orig = blockIdx.x;
-  int lin = orig;
-  if (total >= 16) {
-    const int qq = total / 8, rr = total % 8, xcd = orig % 8;
-    lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
-  }
-  const int qt = lin % nqt;
-  const int hz = lin / nqt;
-  const int h = hz % heads;
-  const int bz = hz / heads;
-  const int q0 = qt * (AW * QT) + wid * QT;
-  const int64_t b = bz / splits;
-  const int sp = bz - (int)b * splits;
-  const bf16_t* Q = q + b * sq_b + h * HD;
-  const int qrow = q0 + r;
-  bf16x8 qf[4];
-  const bf16x8 zero8 = {};
-#pragma unroll
-  for (int ks = 0; ks < 4; ks++)
-    qf[ks] = qrow < Sq ? load8(Q + (int64_t)qrow * ldq + ks * 16 + 8 * hh) : zero8;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int ks = 0; ks < 4; ks++) asm volatile("" : "+v"(qf[ks]));
-
-  const __amdgpu_buffer_rsrc_t rK = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(k + (b ^ kv_xor) * skv_b + h * HD), (short)0, 0x7ffffff0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rV = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(v + (b ^ kv_xor) * skv_b + h * HD), (short)0, 0x7ffffff0, 0x00020000);
-  int k_row[ACH];
-  uint32_t k_off[ACH], v_off[ACH];
-#pragma unroll
-  for (int i = 0; i < ACH; i++) {
-    const int c = i * GT + gtid;
-    const int row = c >> 3, slot = c & 7;
-    k_row[i] = row;
-    k_off[i] = (uint32_t)(((int64_t)row * ldkv + (slot ^ k_swz(row)) * 8) * 2);
-    v_off[i] = (uint32_t)(((int64_t)row * ldkv + (slot ^ v_swz(row)) * 8) * 2);
-  }
-  const int nkt_all = (Sk + AKT - 1) / AKT;
-  const int kt0 = sp * tiles_per_split;
-  const int nkt = max(0, min(nkt_all - kt0, tiles_per_split));
-  const int nkt_g = nkt > ksp ? (nkt - ksp + KS - 1) / KS : 0;
-  const int nj = (nkt + KS - 1) / KS;
-  auto issue = [&](int j) {
-    const int kt = kt0 + ksp + KS * j;
-    char* sb = ring + (j % NST) * STAGE_BYTES;
-    const uint32_t t0 = (uint32_t)((int64_t)kt * AKT * ldkv * 2);
-#pragma unroll
-    for (int i = 0; i < ACH; i++) {
-      const bool ok = kt * AKT + k_row[i] < Sk;
-      glds16(rK, sb + (i * GT + wid * 64) * 16, ok ? t0 + k_off[i] : OOB);
-      glds16(rV, sb + TILE_BYTES + (i * GT + wid * 64) * 16, ok ? t0 + v_off[i] : OOB);
-    }
-  };
-
-  f32x16 oacc[2];
-#pragma unroll
-  for (int d = 0; d < 2; d++)
-#pragma unroll
-    for (int i = 0; i < 16; i++) oacc[d][i] = 0.f;
-  float m = -INFINITY, l = 0.f;
-  const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gsel = (lane >> 4) & 1;
-  f32x16 s[2];                 // S^T of the tile between its M and V blocks
-  bf16x8 pf[4];                // P^T of the tile between its V block and the next M block
-
-  auto qk = [&](int j) {
-    const char* sK = ring + (j % NST) * STAGE_BYTES;
-#pragma unroll
-    for (int hs = 0; hs < 2; hs++) {
-#pragma unroll
-      for (int i = 0; i < 16; i++) s[hs][i] = 0.f;
-      const int row = hs * 32 + r;
-#pragma unroll
-      for (int ks = 0; ks < 4; ks++) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(
-            sK + row * 128 + (((2 * ks + hh) ^ k_swz(row)) * 16));
-        s[hs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[hs], 0, 0, 0);
-      }
-    }
-  };
-  auto sm = [&](int j, auto tail_tag) {
-    constexpr bool TAIL = decltype(tail_tag)::value;
-    const int kt = kt0 + ksp + KS * j;
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int hs = 0; hs < 2; hs++)
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        if constexpr (TAIL) {
-          const int key = kt * AKT + hs * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (key >= Sk) s[hs][i] = -INFINITY;
-        }
-        tmax = fmaxf(tmax, s[hs][i]);
-      }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m, tmax);
-    const float alpha = __builtin_amdgcn_exp2f((m - m_new) * c_log2);
-    const float mc = m_new * c_log2;
-    float rs = 0.f;
-#pragma unroll
-    for (int hs = 0; hs < 2; hs++)
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const float p = __builtin_amdgcn_exp2f(s[hs][i] * c_log2 - mc);
-        rs += p;
-        pf[2 * hs + (i >> 3)][i & 7] = f2bf(p);
-      }
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = m_new;
-#pragma unroll
-    for (int d = 0; d < 2; d++)
-#pragma unroll
-      for (int i = 0; i < 16; i++) oacc[d][i] *= alpha;
-  };
-  auto pv = [&](int j) {
-    const char* sV = ring + (j % NST) * STAGE_BYTES + TILE_BYTES;
-    s16x4 vt[2][4][2];
-#pragma unroll
-    for (int d = 0; d < 2; d++) {
-      const int d0 = d * 32 + 16 * gsel + 4 * gp;
-#pragma unroll
-      for (int c = 0; c < 4; c++)
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-          const int rr = 16 * c + 8 * x + 4 * hh + gq;
-          vt[d][c][x] = tr_read(sV + rr * 128 + (((d0 >> 3) ^ v_swz(rr)) * 16) + (d0 & 7) * 2);
-        }
-    }
-#define M3S_VT(d) "+v"(vt[d][0][0]), "+v"(vt[d][0][1]), "+v"(vt[d][1][0]), "+v"(vt[d][1][1]), \
-                  "+v"(vt[d][2][0]), "+v"(vt[d][2][1]), "+v"(vt[d][3][0]), "+v"(vt[d][3][1])
-    asm volatile("s_waitcnt lgkmcnt(8)" : M3S_VT(0)::"memory");
-#pragma unroll
-    for (int d = 0; d < 2; d++) {
-      if (d == 1) asm volatile("s_waitcnt lgkmcnt(0)" : M3S_VT(1)::"memory");
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const bf16x4 lob = __builtin_bit_cast(bf16x4, vt[d][c][0]);
-        const bf16x4 hib = __builtin_bit_cast(bf16x4, vt[d][c][1]);
-        bf16x8 vf;
-        vf[0] = lob[0];
-        vf[1] = lob[1];
-        vf[2] = lob[2];
-        vf[3] = lob[3];
-        vf[4] = hib[0];
-        vf[5] = hib[1];
-        vf[6] = hib[2];
-        vf[7] = hib[3];
-        oacc[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[c], oacc[d], 0, 0, 0);
-      }
-    }
-#undef M3S_VT
-  };
-  // the tile that may be partial is the globally last one: only its softmax masks
-  auto sm_any = [&](int j) {
-    if constexpr (TAILS) {
-      if ((kt0 + ksp + KS * j + 1) * AKT > Sk) {
-        sm(j, std::true_type{});
-        return;
-      }
-    }
-    sm(j, std::false_type{});
-  };
-
-  // prologue: tile 0 of every key split resident before the first half-period
-  if (nkt_g > 0) issue(0);
-  vm_wait<0>();
-  block_sync_lds();
-  const int HP = 2 * nj + 2;
-  for (int hp = 0; hp < HP; hp++) {
-    const int hl = late ? hp - 1 : hp;      // this group's own half-period index
-    if (hl >= 0) {
-      if ((hl & 1) == 0) {                  // M(j): P·V of j-1, then K·Qᵀ of j
-        const int j = hl >> 1;
-        if (NST == 3 && j + 1 < nkt_g) issue(j + 1);
-        if (j >= 1 && j - 1 < nkt_g) pv(j - 1);
-        if (j < nkt_g) qk(j);
-      } else {                              // V(j): softmax of j
-        const int j = hl >> 1;
-        if (NST == 2 && j + 1 < nkt_g) issue(j + 1);
-        if (j < nkt_g) sm_any(j);
-        vm_wait<0>();                       // tile j+1 resident before M(j+1)
-      }
-    }
-    block_sync_lds();
-  }
-  // merge the key splits (as attn_kernel: every ring read above is complete)
-  {
-    float* red = reinterpret_cast<float*>(lds);
-    if (ksp > 0) {
-      float* P = red + ((ksp - 1) * AW + wid) * RED_FLOATS;
-#pragma unroll
-      for (int i4 = 0; i4 < 8; i4++)
-        reinterpret_cast<float4*>(P)[i4 * 64 + lane] =
-            make_float4(oacc[i4 >> 2][(i4 & 3) * 4], oacc[i4 >> 2][(i4 & 3) * 4 + 1],
-                        oacc[i4 >> 2][(i4 & 3) * 4 + 2], oacc[i4 >> 2][(i4 & 3) * 4 + 3]);
-      reinterpret_cast<float2*>(P + 2048)[lane] = make_float2(m, l);
-    }
-    block_sync_lds();
-    if (ksp > 0) return;
-#pragma unroll
-    for (int s2 = 1; s2 < KS; s2++) {
-      const float* P = red + ((s2 - 1) * AW + wid) * RED_FLOATS;
-      const float2 ml = reinterpret_cast<const float2*>(P + 2048)[lane];
-      const float M = fmaxf(m, ml.x);
-      const float a0 = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - M) * c_log2);
-      const float a1 = ml.x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((ml.x - M) * c_log2);
-#pragma unroll
-      for (int i4 = 0; i4 < 8; i4++) {
-        const float4 w = reinterpret_cast<const float4*>(P)[i4 * 64 + lane];
-        const int d = i4 >> 2, e = (i4 & 3) * 4;
-        oacc[d][e] = oacc[d][e] * a0 + w.x * a1;
-        oacc[d][e + 1] = oacc[d][e + 1] * a0 + w.y * a1;
-        oacc[d][e + 2] = oacc[d][e + 2] * a0 + w.z * a1;
-        oacc[d][e + 3] = oacc[d][e + 3] * a0 + w.w * a1;
-      }
-      l = l * a0 + ml.y * a1;
-      m = M;
-    }
-  }
-  if (qrow >= Sq) return;
-  if (part) {
-    const int64_t nb = (int64_t)total / ((int64_t)nqt * heads * splits);
-    float* P = part + ((((int64_t)sp * nb + b) * heads + h) * Sq + qrow) * PART_LD;
-#pragma unroll
-    for (int d = 0; d < 2; d++)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; g4++)
-        *reinterpret_cast<float4*>(P + d * 32 + 8 * g4 + 4 * hh) =
-            make_float4(oacc[d][4 * g4], oacc[d][4 * g4 + 1], oacc[d][4 * g4 + 2],
-                        oacc[d][4 * g4 + 3]);
-    if (hh == 0) *reinterpret_cast<float2*>(P + HD) = make_float2(m, l);
-    return;
-  }
-  const float inv_l = 1.0f / l;
-  if (o_fp8) {
-    uint8_t* O8 = reinterpret_cast<uint8_t*>(o) + b * so_b + (int64_t)qrow * ldo + h * HD;
-#pragma unroll
-    for (int d = 0; d < 2; d++)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; g4++)
-        *reinterpret_cast<uint32_t*>(O8 + d * 32 + 8 * g4 + 4 * hh) =
-            pack4_fp8(oacc[d][4 * g4] * inv_l, oacc[d][4 * g4 + 1] * inv_l,
-                      oacc[d][4 * g4 + 2] * inv_l, oacc[d][4 * g4 + 3] * inv_l);
-    return;
-  }
-  bf16_t* O = reinterpret_cast<bf16_t*>(o) + b * so_b + (int64_t)qrow * ldo + h * HD;
-#pragma unroll
-  for (int d = 0; d < 2; d++)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; g4++) {
-      bf16x4 w;
-#pragma unroll
-      for (int j = 0; j < 4; j++) w[j] = f2bf(oacc[d][4 * g4 + j] * inv_l);
-      *reinterpret_cast<bf16x4*>(O + d * 32 + 8 * g4 + 4 * hh) = w;
-    }
-}
-
 // Merge the key splits: M = max m_s, O = sum_s O_s 2^((m_s - M) c) / sum_s l_s 2^((m_s - M) c).
 // One thread per (b, h, q, 8 head dims).
 __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part,
@@ -982,30 +542,14 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   hipStream_t s = m3s_stream(stream);
   unsigned long long* tl =
       m3s_timeline_take(M3S_TL_ATTN, 4.0 * sq * sk * HD * heads * batch, sq, sk, heads, batch);
-  // ping-pong kernel: opt-in (M3S_ATTN_PP=1) — bit-identical but measured slower (encoder
-  // 10.1 → 11.8 us, decoder 13.4 → 16.1 us replayed; C3 223 → 217 frames/s)
-  const char* pp_env = getenv("M3S_ATTN_PP");
-  const bool pp = pp_env && atoi(pp_env) != 0;
-  const QProj qp0 = {};
 #define M3S_ATTN_LAUNCH2(AWV, KSV, TL)                                                       \
-  if constexpr (AWV * KSV == 8)                                                              \
-    if (pp) {                                                                                \
-      hipLaunchKernelGGL((attn_pp_kernel<AWV, KSV, TL>),                                     \
-                         dim3((unsigned)(m3s_div_up(sq, AWV * QT) * heads * batch * splits)),\
-                         dim3(AWV * KSV * 64), 0, s,                                         \
-                         reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,               \
-                         reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
-                         ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,      \
-                         (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl);     \
-      break;                                                                                 \
-    }                                                                                        \
   hipLaunchKernelGGL((attn_kernel<AWV, KSV, TL>),                                           \
                      dim3((unsigned)(m3s_div_up(sq, AWV * QT) * heads * batch * splits)),    \
                      dim3(AWV * KSV * 64), 0, s,                                             \
                      reinterpret_cast<const bf16_t*>(d_q), ld_q, stride_q,                   \
                      reinterpret_cast<const bf16_t*>(d_k), reinterpret_cast<const bf16_t*>(d_v), \
                      ld_kv, stride_kv, d_o, ld_o, stride_o, o_fp8 ? 1 : 0, (int)sq,          \
-                     (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl, qp0)
+                     (int)sk, (int)heads, c_log2, splits, tps, part, kv_batch_xor, tl)
 #define M3S_ATTN_LAUNCH(AWV, KSV)                                                            \
   do {                                                                                       \
     if (sk % AKT) {                                                                          \
@@ -1028,65 +572,6 @@ extern "C" int m3s_vit_attention(const void* d_q, int64_t ld_q, int64_t stride_q
   }
 #undef M3S_ATTN_LAUNCH
 #undef M3S_ATTN_LAUNCH2
-  M3S_LAUNCH_CHECK();
-  return M3S_OK;
-}
-
-// Cross-attention with the q projection fused in (QProj above).  Only the pair decoder's
-// configuration: 4 query waves x 2 key splits per block, K % 64 == 0, K ≤ 1024, head dim 64.
-extern "C" int m3s_vit_attention_qproj(const m3s_qproj_desc* d, const void* d_k, const void* d_v,
-                                       int64_t ld_kv, int64_t stride_kv, void* d_o,
-                                       int64_t ld_o, int64_t stride_o, int64_t batch,
-                                       int64_t heads, int64_t sq, int64_t sk,
-                                       int kv_batch_xor, void* stream) {
-  if (!d || !d->x || !d->stats || !d->w || !d->c1 || !d->c2 || !d->rope_table || !d_k || !d_v ||
-      !d_o || batch <= 0 || heads <= 0 || sq <= 0 || sk <= 0)
-    return M3S_ERR_INVALID_ARG;
-  if (kv_batch_xor < 0 || kv_batch_xor > 1 || (kv_batch_xor && batch % 2)) return M3S_ERR_INVALID_ARG;
-  if (d->k % 128 || d->k > 1024 || d->k < 128 || d->rope_tokens <= 0 || d->weight_mod < 0)
-    return M3S_ERR_INVALID_ARG;
-  if ((((uintptr_t)d->x) | ((uintptr_t)d->w) | ((uintptr_t)d_k) | ((uintptr_t)d_v)) % 16)
-    return M3S_ERR_INVALID_ARG;
-  if (d->ld_x % 8 || d->stride_x % 8 || d->stride_w % 8 || ld_kv % 8 || stride_kv % 8)
-    return M3S_ERR_INVALID_ARG;
-  if (((uintptr_t)d_o) % 8 || ld_o % 4 || stride_o % 4) return M3S_ERR_INVALID_ARG;
-  if (batch > 65535 || heads > 65535) return M3S_ERR_TOO_LARGE;
-  if (sk * ld_kv * 2 >= 0x7ffffff0 || (batch * d->stride_x + sq * d->ld_x) * 2 >= 0x7ffffff0 ||
-      (heads * 64 * d->k) * 2 >= 0x7ffffff0)
-    return M3S_ERR_TOO_LARGE;
-  QProj qp;
-  qp.x = reinterpret_cast<const bf16_t*>(d->x);
-  qp.ldx = d->ld_x;
-  qp.sx = d->stride_x;
-  qp.stats = d->stats;
-  qp.w = reinterpret_cast<const bf16_t*>(d->w);
-  qp.sw = d->stride_w;
-  qp.wmod = d->weight_mod;
-  qp.c1 = d->c1;
-  qp.c2 = d->c2;
-  qp.sc = d->stride_c;
-  qp.rope = d->rope_table;
-  qp.rope_tokens = (int)d->rope_tokens;
-  qp.K = (int)d->k;
-  qp.eps = d->ln_eps;
-  const float c_log2 = 0.125f * 1.4426950408889634f;
-  hipStream_t s = m3s_stream(stream);
-  unsigned long long* tl =
-      m3s_timeline_take(M3S_TL_ATTN, 4.0 * sq * sk * HD * heads * batch, sq, sk, heads, batch);
-  const dim3 grid((unsigned)(m3s_div_up(sq, 4 * QT) * heads * batch));
-  const int nkt = (int)m3s_div_up(sk, AKT);
-  if (sk % AKT)
-    hipLaunchKernelGGL((attn_kernel<4, 2, true, true>), grid, dim3(512), 0, s, nullptr,
-                       (int64_t)0, (int64_t)0, reinterpret_cast<const bf16_t*>(d_k),
-                       reinterpret_cast<const bf16_t*>(d_v), ld_kv, stride_kv, d_o, ld_o,
-                       stride_o, 0, (int)sq, (int)sk, (int)heads, c_log2, 1, nkt, nullptr,
-                       kv_batch_xor, tl, qp);
-  else
-    hipLaunchKernelGGL((attn_kernel<4, 2, false, true>), grid, dim3(512), 0, s, nullptr,
-                       (int64_t)0, (int64_t)0, reinterpret_cast<const bf16_t*>(d_k),
-                       reinterpret_cast<const bf16_t*>(d_v), ld_kv, stride_kv, d_o, ld_o,
-                       stride_o, 0, (int)sq, (int)sk, (int)heads, c_log2, 1, nkt, nullptr,
-                       kv_batch_xor, tl, qp);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }

@@ -171,8 +171,6 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   a.a_xor = 0;
   a.ln_c1 = d->ln_c1;
   a.ln_eps = d->ln_eps;
-  a.tl = m3s_timeline_take(d->mode != 0 ? M3S_TL_CONV : M3S_TL_GEMM, 2.0 * d->M * d->N * d->K * d->batch, d->M, d->N, d->K,
-                           d->batch);
   const bool ln_stats = d->flags & M3S_EPI_LN_STATS, ln_fold = d->flags & M3S_EPI_LN_FOLD;
   if (ln_stats || ln_fold) {
     // GEMM mode, bf16 operands, biased, 128-column groups, 16-B aligned row vectors
@@ -214,6 +212,10 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
         !d->dpt_w4 || !d->dpt_b4 || !d->dpt_pts || !d->dpt_conf)
       return M3S_ERR_INVALID_ARG;
   }
+  // the step-timeline slot (if armed) is taken only once every check has passed, so a
+  // rejected launch never holds a slot that no kernel stamps
+  a.tl = m3s_timeline_take(d->mode != 0 ? M3S_TL_CONV : M3S_TL_GEMM,
+                           2.0 * d->M * d->N * d->K * d->batch, d->M, d->N, d->K, d->batch);
   hipStream_t s = m3s_stream(stream);
 
   // Tile choice (measured on the pair shapes, tools/gemm_tune.py): 128x128 tiles (one
@@ -248,16 +250,8 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     else if (tiles128 < 256 && nk <= 16) cfg = T64;
     else if (tiles128 >= 256 && tiles128 <= 512 && nk <= 16) cfg = T128O2;
     else cfg = T128;
-    // 96-row tiles (768 = 8 bands) whose grid is one well-filled round of 256 CUs or whole
-    // rounds: faster launch by launch (graph-replayed sweep, tools/gemm_depth.py: enc qkv
-    // 12.3 → 11.1 us, dec fc1 30.1 → 27.4, dec fc2 25.8 → 23.5) but, filling every CU
-    // with one 86-KB-LDS block, they leave no room for the concurrently prefetched encoder:
-    // the tracking pipeline measured 182 vs 184.6 frames/s (2 x 200 steps, A/B).  Opt-in.
-    const int64_t tiles96 = (int64_t)((d->M + 95) / 96) * ((d->N + 127) / 128) * d->batch;
-    static const bool use96 = getenv("M3S_T96") != nullptr;
-    if (!conv && use96 && d->M % 96 == 0 && nk >= 8 &&
-        ((tiles96 >= 160 && tiles96 <= 256) || tiles96 % 256 == 0))
-      cfg = T96;
+    // (96-row tiles, 768 tokens = 8 bands, measured faster launch by launch but slower in
+    // the pipelined step: 182 vs 184.6 frames/s, DESIGN §2 — reachable by tile hint only)
   }
   if (cfg < 1 || cfg > 14 || cfg == 4 || cfg == 5) cfg = T128;
   if (conv && (cfg == T64D || cfg == T128D)) cfg = T64;

@@ -31,8 +31,6 @@ SIGNATURES = {
     "m3s_timeline_meta": (_I, [_P, _P, _P, _I]),
     "m3s_iter_proj": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _F, _F, _P]),
     "m3s_refine_matches": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
-    "m3s_refine_matches_planar": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I, _I, _P]),
-    "m3s_desc_planar": (_I, [_P, _P, _I64, _I64, _P]),
     "m3s_match_prep": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P]),
     "m3s_match_occlusion": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _P]),
     "m3s_pixel_to_lin": (_I, [_P, _P, _I64, _I64, _I64, _P]),
@@ -69,8 +67,6 @@ SIGNATURES = {
     "m3s_vit_attention": (_I, [_P, _I64, _I64, _P, _P, _I64, _I64, _P, _P, _I64, _P, _I64, _I64,
                                _I, _I64, _I64, _I64, _I64, _F, _P, _I64, _I, _P]),
     "m3s_vit_rope_table": (_I, [_P, _I64, _F, _P, _P]),
-    "m3s_vit_attention_qproj": (_I, [_P, _P, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _I64,
-                                     _I64, _I, _P]),
     "m3s_vit_patchify": (_I, [_P, _P, _I64, _I64, _I64, _P]),
     "m3s_copy_rows": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64,
                            _I64, _I64, _P]),
@@ -117,14 +113,6 @@ class GemmDesc(ctypes.Structure):
                 ("ln_c1", _P), ("ln_eps", ctypes.c_float),
                 ("tile_counters", _P), ("tile_counters_len", ctypes.c_int32),
                 ("tile_hint", ctypes.c_int32)]
-
-
-class QProjDesc(ctypes.Structure):
-    """m3s_qproj_desc (include/monst3r_slam_amd.h)."""
-    _fields_ = [("x", _P), ("ld_x", _I64), ("stride_x", _I64), ("stats", _P),
-                ("w", _P), ("stride_w", _I64), ("weight_mod", ctypes.c_int32),
-                ("c1", _P), ("c2", _P), ("stride_c", _I64), ("rope_table", _P),
-                ("rope_tokens", _I64), ("k", _I64), ("ln_eps", ctypes.c_float)]
 
 
 (EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT,

@@ -232,21 +232,13 @@ class FramePipeline:
         else:
             self.tr.model.encode(img, out=self.pairs[(k // self.group) % 2], concurrent=True)
 
-    def _part(self, img_next, k, gen):
+    def _part(self, img_next, k):
         g = self.group
         H, W = self.shape_hw
         part = k % g
         return self.tr.model.encode_part(
             (g, 3, H, W), part, g, img=img_next if part == 0 else None,
-            out=self.pairs[(k // g + 1) % 2] if part == g - 1 else None, gen=gen)
-
-    def encode_side_gen(self, img_next, k):
-        """encode_side as a generator yielding after each encoder block (the caller issues
-        it on the side stream, interleaved with the decoders: PairModel.interleave)."""
-        m = self.tr.model
-        if self.group == 1:
-            return m.encode_gen(img_next, out=self.feat[(k + 1) % 2], concurrent=True)
-        return self._part(img_next, k, True)
+            out=self.pairs[(k // g + 1) % 2] if part == g - 1 else None)
 
     def encode_side(self, img_next, k):
         """Issue step k's share of the prefetch on the current (side) stream: group 1 the
@@ -256,7 +248,7 @@ class FramePipeline:
         if self.group == 1:
             m.encode(img_next, out=self.feat[(k + 1) % 2], concurrent=True)
             return
-        self._part(img_next, k, False)
+        self._part(img_next, k)
 
     def step(self, img_cur, img_next, k, T_WCf_init=None):
         """group 1 only: track img_cur, prefetch img_next."""

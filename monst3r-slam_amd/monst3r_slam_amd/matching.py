@@ -10,19 +10,10 @@ prep_for_iter_proj :25-49) over the fused HIP kernels:
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from . import _lib
 from .config import config as _config
-
-# M3S_REFINE_PLANAR=1: refine_matches reads the candidate image's descriptors in
-# chunk-planar layout (m3s_desc_planar + m3s_refine_matches_planar, bit-identical results).
-# Off: measured 370 vs 192 us per 384x512 direction (tools/match_bench.py) — a candidate's
-# three chunks then sit in three far-apart planes instead of one 48-B row
-_PLANAR = os.environ.get("M3S_REFINE_PLANAR", "0") == "1"
-
 
 def pixel_to_lin(p1, w):
     return p1[..., 0] + (w * p1[..., 1])
@@ -77,19 +68,10 @@ def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None, idx
         d11 = D11.half().contiguous()
         d21 = D21.reshape(b, n, -1).half().contiguous()
         p1n = torch.empty_like(p1)
-        if _PLANAR and int(cfg["radius"]) == 3 and d11.shape[-1] == 24 and \
-                tuple(d11.shape[1:3]) == (h, w):
-            d11p = torch.empty((b, 3, n, 8), dtype=torch.float16, device=dev)
-            _lib.check(lib.m3s_desc_planar(_lib.ptr(d11), _lib.ptr(d11p), b, n, s),
-                       "desc_planar")
-            _lib.check(lib.m3s_refine_matches_planar(
-                _lib.ptr(d11p), _lib.ptr(d21), _lib.ptr(p1), _lib.ptr(p1n), b, h, w, 3,
-                int(cfg["dilation_max"]), s), "refine_matches_planar")
-        else:
-            _lib.check(lib.m3s_refine_matches(_lib.ptr(d11), _lib.ptr(d21), _lib.ptr(p1),
-                                              _lib.ptr(p1n), b, h, w, n, d11.shape[-1],
-                                              int(cfg["radius"]), int(cfg["dilation_max"]), s),
-                       "refine_matches")
+        _lib.check(lib.m3s_refine_matches(_lib.ptr(d11), _lib.ptr(d21), _lib.ptr(p1),
+                                          _lib.ptr(p1n), b, h, w, n, d11.shape[-1],
+                                          int(cfg["radius"]), int(cfg["dilation_max"]), s),
+                   "refine_matches")
         p1 = p1n
     if idx_out is not None:
         if idx_out.shape != (b, n) or idx_out.dtype != torch.int64 or not idx_out.is_contiguous():

@@ -182,21 +182,6 @@ class Ops:
                                               _p(ws), ws.numel(), kv_xor, self._s()),
                    "vit_attention")
 
-    def attn_qproj(self, x, st, w, c1, c2, rope, k, v, ldkv, skv_b, o, ldo, so_b, batch,
-                   heads, sq, sk, K, wmod, kv_xor=0):
-        """Cross-attention with the LN-folded, RoPE'd q projection fused in
-        (m3s_vit_attention_qproj): x bf16 [batch][sq][K], st its (mean, M2) statistics,
-        w [wmod][heads·64][K], c1 / c2 [wmod][heads·64], rope = (table, tokens)."""
-        d = _lib.QProjDesc()
-        d.x, d.ld_x, d.stride_x, d.stats = _p(x), K, sq * K, _p(st)
-        d.w, d.stride_w, d.weight_mod = _p(w), heads * 64 * K, wmod
-        d.c1, d.c2, d.stride_c = _p(c1), _p(c2), heads * 64
-        d.rope_table, d.rope_tokens = _p(rope[0]), rope[1]
-        d.k, d.ln_eps = K, LN_EPS
-        _lib.check(self.lib.m3s_vit_attention_qproj(ctypes.byref(d), _p(k), _p(v), ldkv, skv_b,
-                                                    _p(o), ldo, so_b, batch, heads, sq, sk,
-                                                    kv_xor, self._s()), "vit_attention_qproj")
-
     def copy_rows(self, src, dst, rows, row_bytes, src_row, dst_row, outer, inner, src_outer,
                   src_inner, src_base, dst_outer, dst_inner, dst_base):
         """m3s_copy_rows (byte strides): item (o, i) of outer x inner copies `rows` rows."""
@@ -231,27 +216,6 @@ def _drain(gen):
             next(gen)
         except StopIteration as e:
             return e.value
-
-
-def _round_robin(chains):
-    """Issue [(stream, generator)] chains one step (one block) each in turn, each step on
-    its chain's stream, until all are exhausted; the chains' return values in order.
-    HIP graphs are submitted node by node in capture order, so a chain captured behind
-    another's complete node list starts that many submissions (≈3 µs each) late."""
-    live = list(range(len(chains)))
-    res = [None] * len(chains)
-    while live:
-        nxt = []
-        for c in live:
-            stream, g = chains[c]
-            with torch.cuda.stream(stream):
-                try:
-                    next(g)
-                    nxt.append(c)
-                except StopIteration as e:
-                    res[c] = e.value
-        live = nxt
-    return res
 
 
 def _conv_pack(w):
@@ -467,10 +431,6 @@ class PairModel:
         # the critical path and the graph gains dependency edges, 118.5 vs 124.9 frames/s
         # serial, so one stream is the default.
         self.side = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
-        # DPT act_postprocess branches started mid-decoder (pair(split_heads=True))
-        self.side_early = torch.cuda.Stream(device)
-        self.early_heads = os.environ.get("M3S_EARLY_HEADS", "0") == "1"  # measured slower
-        self._early_ev = []
         self.serial = True
         self.fp8 = False
         # bf16 path: the blocks' LayerNorms folded into the following projections (ln_fold;
@@ -492,39 +452,12 @@ class PairModel:
         # the pair decoder split by model onto two streams (decode_multi; M3S_DEC_SPLIT=0
         # restores the single batch-4 chain): 214.0 → 218.3 frames/s (2 × A/B)
         self.dec_split = os.environ.get("M3S_DEC_SPLIT", "1") == "1"
-        # schedule knob: an event recorded on the MonST3R decoder chain after layer
-        # `layer_event_at` (None: no event) — the pipelined loop starts the next frame's
-        # encoder behind it instead of at the step's start (M3S_PREFETCH_AFTER)
-        # the MASt3R DPT heads deferred into the next pair (SequenceLoop; M3S_DEFER_MAST3R)
-        self.defer_mast3r = os.environ.get("M3S_DEFER_MAST3R", "0") == "1"
-        e = os.environ.get("M3S_PREFETCH_AFTER")
-        self.layer_event_at = int(e) if e not in (None, "") else None
-        self.layer_event = None
         # split heads: the local-feature MLP runs on the side chain ahead of the MASt3R heads
         self.lf_side = os.environ.get("M3S_LF_SIDE", "1") != "0"
-        self.mast3r_own_stream = os.environ.get("M3S_MAST3R_STREAM", "0") == "1"
-        self.mast3r_late = os.environ.get("M3S_MAST3R_LATE", "0") == "1"
         self._tag = None      # buffer-key prefix of the head set being issued (split heads)
         self._wbase = 0       # first head-weight stack of that set
         self._wm = 4
         self._ev_heads = None
-        # deferred MASt3R DPT heads (pair(defer_parity=k)): their pts3d / conf are never
-        # read by the tracking (monst3r_utils.py:290), so frame t's run during frame t+1's
-        # decoder on their own stream, from hooks kept in a parity double buffer
-        self._hsuf = ""
-        self.side_defer = torch.cuda.Stream(device)
-        self._ev_defer = None
-        # side chains to issue block by block between the split decoders' blocks:
-        # [(stream, generator)], consumed by the next decode (SequenceLoop sets the
-        # prefetched encoder here).  Off by default (M3S_INTERLEAVE=1): measured in the C3
-        # step, 200.0 vs 223.8 frames/s with the two-frame encoder, 223.4 vs 224.3 with the
-        # one-frame encoder — chain after chain, the encoder gets ahead alone
-        self.interleave = None
-        self.interleave_capture = os.environ.get("M3S_INTERLEAVE", "0") == "1"
-        # M3S_FUSE_Q=1: the decoder's cross-attention q projection fused into the attention
-        # launch (m3s_vit_attention_qproj, bit-identical).  Off: 227.4 vs 231.6 frames/s in
-        # the C3 step (the per-block q prologue is latency-bound)
-        self.fuse_q = os.environ.get("M3S_FUSE_Q", "0") == "1"
 
     def set_fp8(self, on=True):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
@@ -546,16 +479,6 @@ class PairModel:
         return q[i], dict(fp8=(sc[i], 0))
 
     # ---- streams ----
-    def _take_interleave(self):
-        chains, self.interleave = list(self.interleave or []), None
-        return chains
-
-    def _drain_interleave(self):
-        """Issue what is left of the interleaved side chains, each on its own stream."""
-        for stream, g in self._take_interleave():
-            with torch.cuda.stream(stream):
-                _drain(g)
-
     def _on(self, k):
         """Context: launch on side stream k (after everything queued so far on the current
         stream), or on the current stream when serial."""
@@ -577,11 +500,6 @@ class PairModel:
             torch.cuda.current_stream(self.dev).wait_event(ev)
 
     # ---- buffers ----
-    def _hk(self, name):
-        """Decoder hook buffer key: parity-suffixed while pair(defer_parity=...) runs, so the
-        previous frame's hooks survive for its deferred MASt3R heads."""
-        return name + self._hsuf
-
     def _buf(self, key, shape, dtype):
         """Persistent scratch per (name, shape, dtype): a buffer is never freed or
         reallocated, so HIP graphs captured over it stay valid when other batch sizes run."""
@@ -623,13 +541,7 @@ class PairModel:
                            self.enc_tiles_concurrent if concurrent else {})
         return self._encode(img.shape, img, out, tiles)
 
-    def encode_gen(self, img, out=None, concurrent=False):
-        """encode() as a generator that yields after each block (interleaved capture)."""
-        tiles = _tile_knob("M3S_ENC_TILE", ("qkv", "proj", "fc1", "fc2"),
-                           self.enc_tiles_concurrent if concurrent else {})
-        return self._encode_gen(img.shape, img, out, tiles)
-
-    def encode_part(self, shape, part, parts, img=None, out=None, gen=False):
+    def encode_part(self, shape, part, parts, img=None, out=None):
         """Part `part` of `parts` of a prefetched encode (concurrent tile hints) of a batch of
         `shape` = [B,3,H,W] images: part 0 embeds `img` and runs the first depth/parts blocks,
         the last part runs the remaining blocks and writes enc_norm into `out` [B,S,E].  The
@@ -644,7 +556,7 @@ class PairModel:
         g = self._encode_gen(shape, img if part == 0 else None,
                              out if part == parts - 1 else None, tiles, (lo, hi),
                              begin=part == 0, end=part == parts - 1)
-        return g if gen else _drain(g)
+        return _drain(g)
 
     def _encode(self, *args, **kw):
         return _drain(self._encode_gen(*args, **kw))
@@ -738,7 +650,7 @@ class PairModel:
         wm = 2 * models
         self._wm = wm
         Z = wm * G
-        h0 = self._buf(self._hk("h0"), (Z, S, E), BF16)
+        h0 = self._buf("h0", (Z, S, E), BF16)
         # h0[(g·models + m)·2 + side] = (feat1 | feat2)[g] for every model m: one row copy
         # per side (in-tree kernel), feat_* [G,S,E] contiguous
         fb = S * E * 2
@@ -762,26 +674,21 @@ class PairModel:
             # the two models' decoders (z 0-1 MonST3R, 2-3 MASt3R: independent chains) as two
             # batch-2 chains on two streams, so each fills the other's kernel tails / gaps
             main = torch.cuda.current_stream(self.dev)
-            side = self.side[1]
+            # (the side chain's stream is the heads' side stream too: the decoder joins the
+            # capture stream before any head is issued, so the step captures three streams —
+            # DESIGN §5 "Capture topology")
+            side = self.side[0]
             side.wait_stream(main)
             g0 = self._decode_folded_gen(x, xb, st, h0, Z, S, E, D, gh, gw, wm, None, part=0)
             g1 = self._decode_folded_gen(x, xb, st, h0, Z, S, E, D, gh, gw, wm, None, part=1)
-            if self.interleave_capture:
-                # capture order = the order the runtime submits the graph's nodes (serially,
-                # ≈3 µs each): the two chains and the caller's side chains (self.interleave)
-                # are issued block by block in turn, so none waits behind another's whole
-                # node list at the step's start
-                hooks = _round_robin([(main, g0), (side, g1)] + self._take_interleave())[0]
-            else:
-                hooks = _drain(g0)
-                with torch.cuda.stream(side):
-                    _drain(g1)
+            hooks = _drain(g0)
+            with torch.cuda.stream(side):
+                _drain(g1)
             main.wait_stream(side)
-            h12 = self._buf(self._hk("h12"), (Z, S, D), BF16)
+            h12 = self._buf("h12", (Z, S, D), BF16)
             o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
             hooks["h12"] = h12
             return hooks
-        self._drain_interleave()
         if fold:
             return self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm, on_hook)
         adt = U8 if self.fp8 else BF16
@@ -851,12 +758,12 @@ class PairModel:
             o.gemm(hid, w, x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D, bias=P["fc2_b"],
                    sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
             if (i + 1) in hk:
-                hb = self._buf(self._hk(f"h{i + 1}"), (Z, S, D), BF16)
+                hb = self._buf(f"h{i + 1}", (Z, S, D), BF16)
                 hb.copy_(x)
                 hooks[f"h{i + 1}"] = hb
                 if on_hook is not None:
                     on_hook(f"h{i + 1}", hooks)
-        h12 = self._buf(self._hk("h12"), (Z, S, D), BF16)
+        h12 = self._buf("h12", (Z, S, D), BF16)
         o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
         hooks["h12"] = h12
         if on_hook is not None:
@@ -882,7 +789,7 @@ class PairModel:
         att = self._buf("dec_att", (Z, S, D), BF16)
         hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), BF16)
         hooks = {"h0": h0}
-        hook_bufs = {k: self._buf(self._hk(f"h{k}"), (Z, S, D), BF16) for k in a.hooks[1:3]}
+        hook_bufs = {k: self._buf(f"h{k}", (Z, S, D), BF16) for k in a.hooks[1:3]}
         sl = None
         if part is not None:
             # one model's two problems (decode_multi's per-model split): every buffer, the
@@ -914,31 +821,20 @@ class PairModel:
                    D, S * D, Z, a.dec_heads, S, S)
             o.gemm(att, P["proj_w"], x, S, D, D, Z, sB=D * D, bias=P["proj_b"], sBias=D, **zs,
                    tile=tl("proj"), **R32S)
-            if self.fuse_q and D == a.dec_heads * 64 and D % 128 == 0 and D <= 1024:
-                # norm2 + q projection + RoPE inside the cross-attention (one launch fewer
-                # per layer; bit-identical to the q GEMM + attention below)
-                o.attn_qproj(xb, st, P["q_wf"], P["q_c1"], P["q_c2"], (rt, S),
-                             qkv[:, :, 2 * D:], qkv[:, :, 4 * D:], F5, S * F5, att, D, S * D,
-                             Z, a.dec_heads, S, S, D, wm, kv_xor=1)
-            else:
-                o.gemm(xb, P["q_wf"], q, S, D, D, Z, sB=D * D, bias=P["q_c2"], sBias=D,
-                       rope=(rt, D, S), ln_fold=(st, P["q_c1"], 0), tile=tl("q"), **zs)
-                # k' / v' of problem z were computed in problem z ^ 1's rows
-                o.attn(q, D, S * D, qkv[:, :, 2 * D:], qkv[:, :, 4 * D:], F5, S * F5, att, D,
-                       S * D, Z, a.dec_heads, S, S, kv_xor=1)
+            o.gemm(xb, P["q_wf"], q, S, D, D, Z, sB=D * D, bias=P["q_c2"], sBias=D,
+                   rope=(rt, D, S), ln_fold=(st, P["q_c1"], 0), tile=tl("q"), **zs)
+            # k' / v' of problem z were computed in problem z ^ 1's rows
+            o.attn(q, D, S * D, qkv[:, :, 2 * D:], qkv[:, :, 4 * D:], F5, S * F5, att, D,
+                   S * D, Z, a.dec_heads, S, S, kv_xor=1)
             o.gemm(att, P["cproj_w"], x, S, D, D, Z, sB=D * D, bias=P["cproj_b"], sBias=D, **zs,
                    tile=tl("cproj"), **R32S)
             o.gemm(xb, P["fc1_wf"], hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm,
                    bias=P["fc1_c2"], sBias=Dm, flags=_lib.EPI_GELU, wmod=wm,
                    ln_fold=(st, P["fc1_c1"], 0), tile=tl("fc1"))
-            if part in (None, 0) and self.layer_event_at is not None and \
-                    i + 1 == self.layer_event_at:
-                self.layer_event = torch.cuda.Event()
-                self.layer_event.record(torch.cuda.current_stream(self.dev))
             xc = xb
             if (i + 1) in hk:
                 xc = hook_bufs[i + 1]
-                hooks[f"h{i + 1}"] = self._buf(self._hk(f"h{i + 1}"), (2 * wm if sl is not None else Z,
+                hooks[f"h{i + 1}"] = self._buf(f"h{i + 1}", (2 * wm if sl is not None else Z,
                                                              S, D), BF16)
             o.gemm(hid, P["fc2_w"], x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D,
                    bias=P["fc2_b"], sBias=D, wmod=wm, tile=tl("fc2"),
@@ -948,7 +844,7 @@ class PairModel:
             yield i
         if sl is not None:
             return hooks
-        h12 = self._buf(self._hk("h12"), (Z, S, D), BF16)
+        h12 = self._buf("h12", (Z, S, D), BF16)
         o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
         hooks["h12"] = h12
         if on_hook is not None:
@@ -1036,15 +932,14 @@ class PairModel:
         t = self.w.h[key]
         return t[self._wbase:] if self._wbase else t
 
-    def heads(self, hooks, gh, gw, H, W, models=2, split=False, R=None, mast3r_dpt=True):
+    def heads(self, hooks, gh, gw, H, W, models=2, split=False):
         """DPT heads of all 2*models*G problems (z = (g*models + model)*2 + side, head weights
         z % (2*models)) + MASt3R local features of the model-1 problems (models=2 only).
         split (one pair, G = 1): the MASt3R DPT heads — whose pts3d/conf the tracking never
         reads (monst3r_utils.py:290) — are issued on side stream 0 as their own 2-problem
-        set, concurrent with the MonST3R heads, the local features and the caller's
-        matching / pose solve; the caller joins with `join()` before the next frame.
-        R: the layer_rn outputs of all Z problems computed ahead by early_branch (events in
-        self._early_ev); the refinenets then start from them.
+        set, behind the local-feature MLP (which the matching waits for) and concurrent with
+        the MonST3R heads and the caller's matching / pose solve; the caller joins with
+        `join()` before the next frame.
         Returns pts3d f32 [Z,H,W,3], conf f32 [Z,H,W], desc16 f16 [2G,H,W,24],
         desc f32 [2G,H,W,24], desc_conf f32 [2G,H,W] (the latter three: (g, side) of model 1;
         None with models=1)."""
@@ -1061,61 +956,37 @@ class PairModel:
             main = torch.cuda.current_stream(self.dev)
             side = self.side[0]
             side.wait_stream(main)
-            for ev in self._early_ev:
-                side.wait_event(ev)
             # side-chain tile hints (M3S_SIDE_TILE experiment knob: lf / dpt; default table)
             st = _tile_knob("M3S_SIDE_TILE", ("lf", "dpt"), self.side_tiles)
             with torch.cuda.stream(side):
-                if self.lf_side:
-                    # the local features (needed by the matching) first on the side chain,
-                    # overlapping the MonST3R heads; then the MASt3R heads (joined later)
-                    self._wm = wm
-                    self.ops.tile_default = st.get("lf")
-                    desc, desc16, dconf, _ = self._local_features(hooks, G, S, E, D, H, W)
-                    ev_lf = torch.cuda.Event()
-                    ev_lf.record(side)
-        def _mast3r_heads():
-            sub = {k: v[2:4] for k, v in hooks.items()}
-            # M3S_MAST3R_STREAM=1: the MASt3R heads on the decoder's second stream (idle by
-            # now) beside the local features instead of behind them on the side chain
-            hs = self.side[1] if self.mast3r_own_stream else side
-            if hs is not side:
-                hs.wait_stream(main)
-                for ev in self._early_ev:
-                    hs.wait_event(ev)
-            with torch.cuda.stream(hs):
-                self.ops.tile_default = st.get("dpt")
                 try:
+                    if self.lf_side:
+                        # the local features (needed by the matching) first on the side
+                        # chain, overlapping the MonST3R heads; then the MASt3R heads
+                        self._wm = wm
+                        self.ops.tile_default = st.get("lf")
+                        desc, desc16, dconf, _ = self._local_features(hooks, G, S, E, D, H, W)
+                        ev_lf = torch.cuda.Event()
+                        ev_lf.record(side)
+                    sub = {k: v[2:4] for k, v in hooks.items()}
+                    self.ops.tile_default = st.get("dpt")
                     # M3S_ABLATE_MAST3R_DPT=1: diagnostic ablation only (tools/step_ablation):
                     # the discarded MASt3R pts3d / conf heads are not issued
-                    if mast3r_dpt and os.environ.get("M3S_ABLATE_MAST3R_DPT") != "1":
-                        self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4],
-                                  R=None if R is None else [r[2:4] for r in R])
+                    if os.environ.get("M3S_ABLATE_MAST3R_DPT") != "1":
+                        self._dpt(sub, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4])
                 finally:
                     self.ops.tile_default = None
                 self._ev_heads = torch.cuda.Event()
-                self._ev_heads.record(hs)
-
-        if split and not self.mast3r_late:
-            _mast3r_heads()
+                self._ev_heads.record(side)
         # MASt3R local features (z = 2, 3): cat(enc, dec_last) → MLP → pixel shuffle
         if models == 2 and desc is None:
             self._wm = wm
             desc, desc16, dconf, ev_lf = self._local_features(hooks, G, S, E, D, H, W)
-        for ev in self._early_ev:
-            main_s = torch.cuda.current_stream(self.dev)
-            main_s.wait_event(ev)
-        self._early_ev = []
         if split:
             sub = {k: v[0:2] for k, v in hooks.items()}
-            self._dpt(sub, gh, gw, H, W, 2, 0, 2, None, pts[0:2], conf[0:2],
-                      R=None if R is None else [r[0:2] for r in R])
-            if self.mast3r_late:
-                # M3S_MAST3R_LATE=1: the MASt3R heads captured after the MonST3R heads
-                # (same streams and dependencies, later in the graph's node order)
-                _mast3r_heads()
+            self._dpt(sub, gh, gw, H, W, 2, 0, 2, None, pts[0:2], conf[0:2])
         else:
-            self._dpt(hooks, gh, gw, H, W, Z, 0, wm, None, pts, conf, R=R)
+            self._dpt(hooks, gh, gw, H, W, Z, 0, wm, None, pts, conf)
         self._wait(ev_lf)
         return pts, conf, desc16, desc, dconf
 
@@ -1124,35 +995,6 @@ class PairModel:
         if self._ev_heads is not None:
             torch.cuda.current_stream(self.dev).wait_event(self._ev_heads)
             self._ev_heads = None
-        if self._ev_defer is not None:
-            torch.cuda.current_stream(self.dev).wait_event(self._ev_defer)
-            self._ev_defer = None
-
-    def _rn_bufs_early(self, gh, gw, Z):
-        saved, self._tag = self._tag, "early"
-        try:
-            return self._rn_bufs(gh, gw, Z)
-        finally:
-            self._tag = saved
-
-    def _early_branch(self, name, hooks, gh, gw, R):
-        """Enqueue hook `name`'s act_postprocess + layer_rn branch (all Z problems, weight
-        stacks z % 4) on self.side_early after the work queued so far on the current
-        stream; heads() waits for the recorded events before the refinenets."""
-        k = {"h0": 0, "h6": 1, "h9": 2, "h12": 3}[name]
-        main = torch.cuda.current_stream(self.dev)
-        st = self.side_early
-        st.wait_stream(main)
-        saved = (self._tag, self._wbase, self._wm)
-        self._tag, self._wbase, self._wm = "early", 0, 4
-        try:
-            with torch.cuda.stream(st):
-                self._ap_branch(k, hooks, gh, gw, hooks[name].shape[0], R)
-                ev = torch.cuda.Event()
-                ev.record(st)
-        finally:
-            self._tag, self._wbase, self._wm = saved
-        self._early_ev.append(ev)
 
     def _rn_bufs(self, gh, gw, Z):
         F = self.a.feature_dim
@@ -1198,27 +1040,23 @@ class PairModel:
             self._conv3(t3, "ap3c_w", L3, Z, gh, gw, Ld[3], Ld[3], stride=2, bias_key="ap3c_b")
             self._conv3(L3, "rn3_w", R[3], Z, g3h, g3w, Ld[3], F)
 
-    def _dpt(self, hooks, gh, gw, H, W, Z, wbase, wm, tag, pts, conf, R=None):
+    def _dpt(self, hooks, gh, gw, H, W, Z, wbase, wm, tag, pts, conf):
         """act_postprocess + refinenets + head of Z problems whose hooks are given (views),
-        head weights from stack wbase with weight_mod wm, scratch keyed by tag.  R: the
-        four layer_rn outputs when already computed (early_branch), else computed here."""
+        head weights from stack wbase with weight_mod wm, scratch keyed by tag."""
         o, a = self.ops, self.a
         self._tag, self._wbase, self._wm = tag, wbase, wm
         Hw = self._hw
         F = a.feature_dim
         g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
-        if R is None:
-            R = self._rn_bufs(gh, gw, Z)
-            # act_postprocess + layer_rn (3x3, no bias → F channels): branches 1-3 on side
-            # stream 0, branch 0 (the largest) on the current stream (one stream when serial;
-            # branches 0 / 1 on a stream of the head set's own made capture_end segfault on
-            # this ROCm stack — DESIGN §2)
-            with self._on(0):
-                for k in (1, 2, 3):
-                    self._ap_branch(k, hooks, gh, gw, Z, R)
-                ev_ap = self._event()
-            self._ap_branch(0, hooks, gh, gw, Z, R)
-            self._wait(ev_ap)
+        R = self._rn_bufs(gh, gw, Z)
+        # act_postprocess + layer_rn (3x3, no bias → F channels): branches 1-3 on side
+        # stream 0, branch 0 (the largest) on the current stream (one stream when serial)
+        with self._on(0):
+            for k in (1, 2, 3):
+                self._ap_branch(k, hooks, gh, gw, Z, R)
+            ev_ap = self._event()
+        self._ap_branch(0, hooks, gh, gw, Z, R)
+        self._wait(ev_ap)
         # refinenets: path_k = up2(out_conv(RCU2(path_{k+1} + RCU1(R_k)))) with the next
         # level's skip pre-added by the upsample (consumed as RCU1's residual addend)
         p4 = self._buf("path4", (Z, gh, gw, F), BF16)
@@ -1246,36 +1084,7 @@ class PairModel:
 
 
     # ---- monst3r_asymmetric_inference ----
-    def _deferred_mast3r_heads(self, parity, gh, gw, H, W, stream_ready=False):
-        """The MASt3R DPT heads of the PREVIOUS pair (hooks of parity (parity + 1) % 2) on
-        side_defer, ordered only after the work enqueued before this pair: they overlap
-        this pair's decoder (the tracking chain does not read them)."""
-        a = self.a
-        S, E, D = gh * gw, a.enc_dim, a.dec_dim
-        prev = f"#{(parity + 1) % 2}"
-        hk = {}
-        for name, dim in (("h0", E), ("h6", D), ("h9", D), ("h12", D)):
-            key = (None, name + prev, (4, S, dim), BF16)
-            if key not in self._bufs:      # first use: defined contents, not stale memory
-                self._bufs[key] = torch.zeros((4, S, dim), dtype=BF16, device=self.dev)
-            hk[name] = self._bufs[key][2:4]
-        pts = self._buf("pts3d", (4, H, W, 3), F32)
-        conf = self._buf("conf", (4, H, W), F32)
-        sd = self.side_defer
-        if not stream_ready:
-            sd.wait_stream(torch.cuda.current_stream(self.dev))
-        st = _tile_knob("M3S_SIDE_TILE", ("lf", "dpt"), self.side_tiles)
-        with torch.cuda.stream(sd):
-            self.ops.tile_default = st.get("dpt")
-            try:
-                self._dpt(hk, gh, gw, H, W, 2, 2, 2, "mast3r", pts[2:4], conf[2:4])
-            finally:
-                self.ops.tile_default = None
-            self._ev_defer = torch.cuda.Event()
-            self._ev_defer.record(sd)
-
-    def pair(self, img_i, feat_j=None, img_j=None, feat_i=None, split_heads=False,
-             defer_parity=None):
+    def pair(self, img_i, feat_j=None, img_j=None, feat_i=None, split_heads=False):
         """Frame i vs keyframe j (keyframe features cached as in monst3r_utils.py:262-269).
         feat_i: frame i's encoder features when already computed (the prefetched encode of
         frontend.FramePipeline); img_i then only gives the size.
@@ -1293,37 +1102,8 @@ class PairModel:
             feat_i, pos = self.encode(img_i)
         else:
             pos = self.positions(1, gh, gw)
-        R = None
-        on_hook = None
-        if self.early_heads and split_heads:
-            # the DPT act_postprocess / layer_rn branch of each hook starts on its own
-            # stream as soon as the decoder has produced that hook (h0: before the first
-            # decoder layer; h6 / h9: mid-decoder), for all 4 problems at once
-            R = self._rn_bufs_early(gh, gw, 4)
-            on_hook = lambda name, hk: self._early_branch(name, hk, gh, gw, R)  # noqa: E731
-        defer = defer_parity is not None and split_heads and on_hook is None
-        if defer:
-            if self.interleave_capture:
-                # issued after the decoders' first blocks (an interleaved chain that
-                # starts one round late), not ahead of them
-                sd = self.side_defer
-                sd.wait_stream(torch.cuda.current_stream(self.dev))
-
-                def _deferred():
-                    yield None
-                    self._deferred_mast3r_heads(defer_parity, gh, gw, H, W, stream_ready=True)
-                self.interleave = list(self.interleave or []) + [(sd, _deferred())]
-            else:
-                self._deferred_mast3r_heads(defer_parity, gh, gw, H, W)
-            self._hsuf = f"#{defer_parity % 2}"
-        try:
-            hooks = self.decode(feat_i[0], feat_j.reshape(-1, a.enc_dim), pos, gh, gw,
-                                on_hook=on_hook)
-        finally:
-            self._hsuf = ""
-            self._drain_interleave()
-        pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W, split=split_heads, R=R,
-                                                    mast3r_dpt=not defer)
+        hooks = self.decode(feat_i[0], feat_j.reshape(-1, a.enc_dim), pos, gh, gw)
+        pts, conf, desc16, desc, dconf = self.heads(hooks, gh, gw, H, W, split=split_heads)
         return dict(X=pts[0:2], C=conf[0:2], D16=desc16, D=desc, Q=dconf, feat_i=feat_i,
                     mast3r_X=pts[2:4], mast3r_C=conf[2:4])
 

@@ -285,6 +285,33 @@ class ShardedFactorGraph(FactorGraph):
             self.Q_jj2ii = torch.cat([self.Q_jj2ii, r["Qi"][okm]])
         return bool(ok.sum() > 0)
 
+    def prep_two_way_edges(self):
+        """The base class pairs ii / jj with idx / valid / Q row by row; with world > 1 ii / jj
+        are global while those records are this rank's own edges, so the pairing would be
+        silently misaligned: only the sharded solver (_solve_sharded) may read them."""
+        if _world(self.group)[0] > 1:
+            raise RuntimeError("ShardedFactorGraph.prep_two_way_edges: with world > 1 the match "
+                               "records are rank-local (use solve_GN_* / local_edge_ids)")
+        return super().prep_two_way_edges()
+
+    def local_valid_fraction(self):
+        """(valid match pixels, pixels) over this rank's accepted edges, both directions."""
+        v = torch.cat((self.valid_match_j, self.valid_match_i))
+        return float(v.sum()), float(v.numel())
+
+    def valid_match_fraction(self):
+        """Valid-match fraction over ALL accepted edges of the graph (every rank's records,
+        summed with one all-reduce when world > 1)."""
+        num, den = self.local_valid_fraction()
+        world, _ = _world(self.group)
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([num, den], dtype=torch.float64,
+                             device="cpu" if _is_gloo(self.group) else self.device)
+            dist.all_reduce(t, group=self.group)
+            num, den = float(t[0]), float(t[1])
+        return num / den if den else 0.0
+
     def local_edge_ids(self):
         """Global two-way edge ids of this rank's rows (prep_two_way_edges order: the E
         i→j edges, then the same E as j→i)."""

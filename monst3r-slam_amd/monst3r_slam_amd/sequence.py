@@ -206,6 +206,12 @@ class SequenceLoop:
         self.log_T.zero_()
         if self.pipe is not None:
             g = self.pipe.group
+            if parity % g:
+                # prime() fills rows 0..g-1 of the group buffer (parity // g) % 2, and step
+                # k tracks row k % g: a parity inside a group would track rows that part 0
+                # of that group never embedded
+                raise ValueError(f"reset: parity {parity} must be a multiple of the prefetch "
+                                 f"group {g}")
             if first + g >= s.n_frames:
                 raise ValueError("sequence too short for the prefetch group")
             self.pipe.prime(s.img[first + 1:first + 1 + g].reshape(g, 3, s.h, s.w), parity)
@@ -260,33 +266,15 @@ class SequenceLoop:
                 feat_i = pipe.slot(k)
                 # group g: only part 0 of a group encode reads the images
                 gathers = k % pipe.group == 0
-                dp = k % 2 if m.defer_mast3r else None
-                delay = m.layer_event_at is not None
-                if delay:   # the pair first: the encoder waits for its decoder layer event
-                    m.layer_event = None
-                    ev_start = torch.cuda.Event()
-                    ev_start.record(main)          # main's work before this frame's pair
-                    out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i,
-                                 split_heads=split, defer_parity=dp)
-                    pipe.side.wait_event(ev_start)
-                    if m.layer_event is not None:
-                        pipe.side.wait_event(m.layer_event)
-                else:
-                    pipe.side.wait_stream(main)
+                pipe.side.wait_stream(main)
                 with torch.cuda.stream(pipe.side):
                     if gathers:   # group g: the frames g .. 2g-1 after the tracked one
                         for j in range(pipe.group):
                             self.gather(self.img_next[j:j + 1], pipe.group + j if
                                         pipe.group > 1 else 1)
                         self._gathered.record(pipe.side)
-                    if delay or not m.interleave_capture:
-                        pipe.encode_side(self.img_next, k)
-                if not (delay or not m.interleave_capture):
-                    # the encoder's blocks are captured between the decoders' blocks
-                    m.interleave = [(pipe.side, pipe.encode_side_gen(self.img_next, k))]
-                if not delay:
-                    out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i,
-                                 split_heads=split, defer_parity=dp)
+                    pipe.encode_side(self.img_next, k)
+                out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i, split_heads=split)
             else:
                 self.gather(self.img_cur, 0)
                 out = m.pair(self.img_cur, feat_j=tr.kf.feat, split_heads=split)

@@ -72,42 +72,6 @@ def test_refine_matches_scattered(oracle, dev, radius, dmax):
     np.testing.assert_array_equal(got.cpu().numpy(), ref)
 
 
-def _refine_planar(d11, d21, p1, dmax):
-    """m3s_desc_planar + m3s_refine_matches_planar on device tensors."""
-    from monst3r_slam_amd import _lib
-    lib, P = _lib.load(), _lib.ptr
-    b, h, w, _ = d11.shape
-    n = h * w
-    d11p = torch.empty((b, 3, n, 8), dtype=torch.float16, device=d11.device)
-    _lib.check(lib.m3s_desc_planar(P(d11), P(d11p), b, n, _lib.stream(d11.device)), "planar")
-    out = torch.empty_like(p1)
-    _lib.check(lib.m3s_refine_matches_planar(P(d11p), P(d21), P(p1), P(out), b, h, w, 3, dmax,
-                                             _lib.stream(d11.device)), "refine_planar")
-    return d11p, out
-
-
-@pytest.mark.parametrize("b,h,w,scatter", [(1, 384, 512, False), (2, 96, 128, False),
-                                           (3, 70, 90, True), (1, 31, 37, True)])
-def test_refine_matches_planar_bit_exact(oracle, dev, b, h, w, scatter):
-    """The chunk-planar D11 path (the tracker's layout) vs the oracle: bit-exact p1, incl.
-    scattered windows off every image edge and tile counts not a multiple of 8; the planar
-    image is the exact chunk transpose of the [b,h,w,24] rows."""
-    rng = np.random.default_rng(5 + b + h)
-    d11 = rng.normal(size=(b, h, w, 24)).astype(np.float16)
-    d21 = rng.normal(size=(b, h * w, 24)).astype(np.float16)
-    if scatter:
-        p1 = rng.integers(0, [w, h], size=(b, h * w, 2)).astype(np.int64)
-    else:
-        yy, xx = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
-        p1 = np.stack([xx, yy], -1).reshape(1, -1, 2).repeat(b, 0)
-        p1 = np.clip(p1 + rng.integers(-4, 5, p1.shape), 0, [w - 1, h - 1]).astype(np.int64)
-    ref = oracle.refine_matches(d11, d21, p1, 3, 5)
-    d11p, got = _refine_planar(_t(d11, dev), _t(d21, dev), _t(p1, dev), 5)
-    np.testing.assert_array_equal(got.cpu().numpy(), ref)
-    want = d11.reshape(b, h * w, 3, 8).transpose(0, 2, 1, 3)
-    np.testing.assert_array_equal(d11p.cpu().numpy(), want)
-
-
 def test_refine_generic_fdim(oracle, dev):
     import mast3r_slam_backends as mb
     rng = np.random.default_rng(4)

@@ -275,3 +275,71 @@ def test_grouped_prefetch_encodes_the_right_frames(dev, group):
             assert torch.equal(got, model.encode(imgs, concurrent=True)[0]), i
             checked += 1
     assert checked == 2 * pipe.period // group
+
+
+def test_c3_sequence_200_graph_replay_equals_eager(dev, parity_log):
+    """The bench's timed path is the captured step graphs replayed frame after frame
+    (bench.run_sequence); the oracle tests step eagerly.  This closes the gap: all 200 frames
+    run eagerly (loop.step) and then from the captured graphs (the bench's capture, stream
+    topology checked) — the per-frame log (GN iterations, new-keyframe / lost decisions,
+    keyframe frame, T_WC) and the final keyframe state / match seed are bit-identical.  The
+    step captures three streams (capture, prefetch, decoder + heads side chain)."""
+    import bench
+    from monst3r_slam_amd import sequence as S
+    from monst3r_slam_amd.frontend import FramePipeline
+    model, tr, seq = bench.setup(dev, 0, bench.SEQ_FRAMES + 1)
+    tr.split_heads = True
+    pipe = FramePipeline(tr, (seq.h, seq.w), group=2)
+    loop = S.SequenceLoop(tr, seq, pipe)
+
+    def snap():
+        torch.cuda.synchronize()
+        return (loop.log_i.clone(), loop.log_T.clone(), tr.kf.X_canon.clone(), tr.kf.C.clone(),
+                tr.kf.T_WC.clone(), tr.idx_f2k.clone())
+
+    loop.reset(parity=0)
+    for i in range(bench.SEQ_FRAMES):
+        loop.step(i % pipe.period)
+    eager = snap()
+    loop.reset(parity=0)
+    graphs = [bench.capture(lambda k=k: loop.step(k), dev) for k in range(pipe.period)]
+    assert all(g.m3s_streams == 3 for g in graphs), [g.m3s_streams for g in graphs]
+    bench.run_sequence(loop, graphs, bench.SEQ_FRAMES, dev, 1)
+    replay = snap()
+    names = ("log_i", "log_T", "X_canon", "C", "T_WC", "idx_f2k")
+    for nm, a, b in zip(names, eager, replay):
+        assert torch.equal(a, b), nm
+    summ = loop.summary()
+    assert summ["keyframes_added"] >= 2
+    parity_log("test_c3_sequence_200_graph_replay_equals_eager", frames=bench.SEQ_FRAMES,
+               keyframes_added=summ["keyframes_added"], equal="bit-identical",
+               capture_streams=graphs[0].m3s_streams)
+
+
+def test_malformed_capture_raises_not_crashes(dev):
+    """capture.capture_graph checks the fork / join topology on the eager warm-up run, before
+    any capture begins: a side stream forked from the capture stream and never joined back
+    raises TopologyError (the HIP runtime segfaulted at capture_end on malformed / over-wide
+    captures); the same fn with the join captures and replays."""
+    from monst3r_slam_amd.capture import TopologyError, capture_graph
+    x = torch.zeros(1 << 16, device=dev)
+    side = torch.cuda.Stream(dev)
+
+    def unjoined():
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            x.add_(1.0)
+
+    def joined():
+        unjoined()
+        torch.cuda.current_stream(dev).wait_stream(side)
+
+    with pytest.raises(TopologyError, match="not joined"):
+        capture_graph(unjoined, dev)
+    torch.cuda.synchronize()
+    g = capture_graph(joined, dev)
+    assert g.m3s_streams == 2
+    before = float(x[0])
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(x[0]) == before + 1.0

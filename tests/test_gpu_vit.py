@@ -150,34 +150,34 @@ def test_attention(ops, dev, monkeypatch, S, heads, batch, ks):
     (196, 196, 12, 4, "2", 0, 0, "1"), (12, 12, 4, 2, "4", 0, 0, "1"),
     (64, 100, 3, 2, "2", 0, 0, "1"), (768, 768, 12, 2, "2", 0, 1, "1"),
     (768, 768, 12, 2, "2", 0, 0, "3"), (768, 768, 16, 1, "4", 0, 0, "2")])
-def test_attention_pingpong_bit_identical(ops, dev, monkeypatch, Sq, Sk, heads, batch, ks, kv_xor,
-                                          fp8, splits):
-    """attn_pp_kernel (opt-in M3S_ATTN_PP=1; 8-wave blocks whose two halves of the key
-    splits alternate matrix and softmax blocks) performs each wave's arithmetic in the
-    lockstep kernel's order: its output must equal M3S_ATTN_PP=0's bit for bit — full and partial key tiles, Sq != Sk,
-    the cross-attention batch xor, e4m3 output, grid-level key splits."""
+def test_attention_shapes_vs_fp32(ops, dev, monkeypatch, Sq, Sk, heads, batch, ks, kv_xor, fp8,
+                                  splits):
+    """attn_kernel over the block shapes the launcher picks (in-block key splits 2 / 4) and
+    the grid-level key splits (attn_combine_kernel) vs torch fp32 softmax attention: full and
+    partial key tiles, Sq != Sk, the cross-attention batch xor, e4m3 output (every element
+    written; values within one e4m3 step of the bf16 path)."""
     monkeypatch.setenv("M3S_ATTN_KS", ks)
     monkeypatch.setenv("M3S_ATTN_SPLITS", splits)
     g = torch.Generator(device=dev).manual_seed(40 + Sq + heads)
     D = heads * 64
     q = torch.randn(batch, Sq, D, device=dev, generator=g).bfloat16()
     kv = (torch.randn(batch, Sk, 2 * D, device=dev, generator=g) * 2).bfloat16()
-    outs = []
-    for pp in ("0", "1"):
-        monkeypatch.setenv("M3S_ATTN_PP", pp)
-        o = torch.full((batch, Sq, D), 7, device=dev,
-                       dtype=torch.uint8 if fp8 else torch.bfloat16)
-        ops.attn(q, D, Sq * D, kv, kv[:, :, D:], 2 * D, Sk * 2 * D, o, D, Sq * D, batch, heads,
-                 Sq, Sk, kv_xor=kv_xor)
-        outs.append(o)
-    assert torch.equal(outs[0], outs[1])
-    if not fp8:
-        kk, vv = kv.float().reshape(batch, Sk, 2, heads, 64).permute(2, 0, 3, 1, 4)
-        if kv_xor:
-            kk, vv = kk[[1, 0]], vv[[1, 0]]
-        qq = q.float().reshape(batch, Sq, heads, 64).transpose(1, 2)
-        ref = (torch.softmax(qq @ kk.transpose(-1, -2) / 8.0, -1) @ vv).transpose(1, 2)
-        assert _rel(outs[1], ref.reshape(batch, Sq, D)) < 2e-2
+    o = torch.full((batch, Sq, D), 0x7F if fp8 else 7, device=dev,
+                   dtype=torch.uint8 if fp8 else torch.bfloat16)
+    ops.attn(q, D, Sq * D, kv, kv[:, :, D:], 2 * D, Sk * 2 * D, o, D, Sq * D, batch, heads,
+             Sq, Sk, kv_xor=kv_xor)
+    kk, vv = kv.float().reshape(batch, Sk, 2, heads, 64).permute(2, 0, 3, 1, 4)
+    if kv_xor:
+        kk, vv = kk[[1, 0]], vv[[1, 0]]
+    qq = q.float().reshape(batch, Sq, heads, 64).transpose(1, 2)
+    ref = (torch.softmax(qq @ kk.transpose(-1, -2) / 8.0, -1) @ vv).transpose(1, 2)
+    ref = ref.reshape(batch, Sq, D)
+    if fp8:
+        got = o.view(torch.float8_e4m3fn).float()
+        assert torch.isfinite(got).all()
+        assert float(((got - ref).abs() - 0.07 * ref.abs()).max()) < 2e-2
+    else:
+        assert _rel(o, ref) < 2e-2
 
 
 def test_cross_attention_lengths(ops, dev):
@@ -562,28 +562,6 @@ def test_split_heads_match_batched(dev):
     assert torch.equal(b["D16"], a["D16"]) and torch.equal(b["Q"], a["Q"])
 
 
-def test_early_heads_match_split(dev):
-    """M3S_EARLY_HEADS A/B knob (model.early_heads): the DPT act_postprocess / layer_rn
-    branches started mid-decoder on their own stream (4 problems at once) give the split
-    heads' outputs up to the bf16 GEMM tiling; descriptors (no DPT) exact."""
-    from monst3r_slam_amd import model as Mdl
-    m, _ = Mdl.build(dev, small=True)
-    g = torch.Generator(device=dev).manual_seed(43)
-    img_i = torch.rand(1, 3, 96, 128, device=dev, generator=g) * 2 - 1
-    img_j = torch.rand(1, 3, 96, 128, device=dev, generator=g) * 2 - 1
-    outs = []
-    for early in (False, True):
-        m.early_heads = early
-        o = m.pair(img_i, img_j=img_j, split_heads=True)
-        m.join()
-        outs.append({k: v.clone() for k, v in o.items() if torch.is_tensor(v)})
-    m.early_heads = False
-    a, b = outs
-    for k in ("X", "mast3r_X", "C", "mast3r_C"):
-        assert _rel(b[k], a[k]) < 1e-2, k
-    assert torch.equal(b["D16"], a["D16"]) and torch.equal(b["Q"], a["Q"])
-
-
 def _ln_stats_ref(x):
     """(mean, M2) per 128-column group of the rows of x [.., M, N]."""
     g = x.float().reshape(*x.shape[:-1], x.shape[-1] // 128, 128)
@@ -813,59 +791,3 @@ def test_decoder_split_by_model_matches_batched(dev):
         assert torch.isfinite(b[k]).all(), k
         rel = float((a[k] - b[k]).norm() / a[k].norm())
         assert rel < 2e-2, (k, rel)
-
-
-@pytest.mark.parametrize("gh,gw,heads,batch,wmod", [(24, 32, 12, 2, 2), (24, 32, 12, 4, 4),
-                                                    (12, 15, 4, 2, 2), (20, 24, 4, 2, 0)])
-def test_cross_attention_fused_q_bit_identical(ops, dev, monkeypatch, gh, gw, heads, batch,
-                                               wmod):
-    """m3s_vit_attention_qproj (norm2 + q projection + RoPE inside the cross-attention,
-    croco/blocks.py:180-185) equals the LN-folded q GEMM (unsplit, 8-wave 128² tiles) followed
-    by m3s_vit_attention bit for bit — the pair decoder's shape (768 tokens, 12 heads, kv of
-    problem z ^ 1), a key tail (Sk % 64 != 0) and a query tail (Sq % 128 != 0), and per-problem
-    weights with weight_mod 0 / 2 / 4; and it stays within bf16 tolerance of torch fp32
-    LayerNorm → Linear → RoPE → softmax attention."""
-    from monst3r_slam_amd.model import ln_fold, LN_EPS
-    from oracle import vit_ref as V
-    S, D = gh * gw, heads * 64
-    g = torch.Generator(device=dev).manual_seed(21)
-    x = torch.randn(batch, S, D, device=dev, generator=g) * 1.5 + 0.7
-    nw = wmod if wmod > 0 else batch
-    gam = 1.0 + 0.3 * torch.randn(nw, D, device=dev, generator=g)
-    bet = 0.2 * torch.randn(nw, D, device=dev, generator=g)
-    W = torch.randn(nw, D, D, device=dev, generator=g) / D ** 0.5
-    b = torch.randn(nw, D, device=dev, generator=g)
-    wf, c1, c2 = ln_fold(W, b, gam, bet, dev)
-    xb = x.bfloat16().contiguous()
-    st = _ln_stats_ref(x).contiguous()
-    kv = (torch.randn(batch, S, 2 * D, device=dev, generator=g)).bfloat16().contiguous()
-    pos = V.positions(1, gh, gw, dev)[0].contiguous()
-    rt = ops.rope_table(pos, 100.0)
-    q = torch.empty(batch, S, D, device=dev, dtype=torch.bfloat16)
-    ops.gemm(xb, wf, q, S, D, D, batch, sA=S * D, sB=D * D, sC=S * D, bias=c2, sBias=D,
-             rope=(rt, D, S), ln_fold=(st, c1, 0), wmod=wmod, tile=(12, 1))
-    ref = torch.empty(batch, S, D, device=dev, dtype=torch.bfloat16)
-    # the fused kernel's block shape (4 query waves x 2 key splits) for the reference too:
-    # the key-split merge order is part of the rounding
-    monkeypatch.setenv("M3S_ATTN_AW", "4")
-    monkeypatch.setenv("M3S_ATTN_KS", "2")
-    ops.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, ref, D, S * D, batch, heads, S, S,
-             kv_xor=1)
-    monkeypatch.delenv("M3S_ATTN_AW")
-    monkeypatch.delenv("M3S_ATTN_KS")
-    got = torch.zeros_like(ref)
-    ops.attn_qproj(xb, st, wf, c1, c2, (rt, S), kv, kv[:, :, D:], 2 * D, S * 2 * D, got, D,
-                   S * D, batch, heads, S, S, D, wmod, kv_xor=1)
-    torch.cuda.synchronize()
-    assert torch.equal(got, ref), float((got.float() - ref.float()).abs().max())
-    # fp32 restatement: LN → Linear → RoPE2D → attention over the other problem's k / v
-    ws = torch.arange(batch, device=dev) % nw
-    ln = F.layer_norm(x, (D,), eps=LN_EPS) * gam[ws][:, None] + bet[ws][:, None]
-    qf = torch.bmm(ln, W[ws].transpose(1, 2)) + b[ws][:, None]
-    posb = V.positions(batch, gh, gw, dev)
-    qh = V.rope2d(qf.reshape(batch, S, heads, 64).transpose(1, 2), posb, 100.0)
-    kvx = kv.float()[torch.arange(batch, device=dev) ^ 1]
-    kh = kvx[..., :D].reshape(batch, S, heads, 64).transpose(1, 2)
-    vh = kvx[..., D:].reshape(batch, S, heads, 64).transpose(1, 2)
-    o = F.scaled_dot_product_attention(qh, kh, vh).transpose(1, 2).reshape(batch, S, D)
-    assert _rel(got, o) < 2e-2
