@@ -144,6 +144,11 @@ int m3s_gauss_newton_points(float* d_Twc, const float* d_Xs, const float* d_Cs,
                             int max_iter, float delta_thresh, float* d_dx_out,
                             void* d_workspace, int* h_status_out, void* stream);
 
+/* Diagnostic: 1 = run every backend GN solve on the global-memory dense path instead of the
+ * LDS-resident one used while 7(P-1) <= 126 (both give bit-identical poses; tests compare
+ * them).  Not thread-scoped; returns M3S_OK. */
+int m3s_gn_force_global_solve(int on);
+
 /* Edge-sharded backend GN (the iteration of gn_kernels.cu:1140-1228 split at
  * its reduction).  Each rank holds the data rows of ITS two-way edges only (idx / valid /
  * Q [E_local,...], global edge ids d_edge_ids i32 [E_local]) plus the replicated poses

@@ -493,6 +493,293 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_kernel(
   }
 }
 
+// ---- the LDS-resident solve (n = 7(P-1) <= kLdsN) ----
+// The system is small (P = 16 keyframes: n = 105, 88 KB of f64), so it lives in LDS for
+// the whole solve instead of in global memory, and the per-edge serial assembly loop of
+// gn_solve_kernel (four barriers and global read-modify-writes per edge) becomes:
+//  * per edge, in parallel over the workgroup's 16 waves: the f64 reduction of its S
+//    partials (or its all-gathered G row), M (apply_Sim3_adj_inv of pose i), A = M G Mᵀ and
+//    v = M v' — the same operations in the same order as gn_solve_kernel — written to EB;
+//  * assembly by ownership: each matrix entry is owned by one thread, which adds the
+//    contributions of the edges touching its 7x7 block in edge order (per-block lists built
+//    once per solve by gn_lists_kernel) — the same additions in the same order as the serial
+//    loop, so the system, and everything after it, is bit-identical;
+//  * right-looking Cholesky in LDS (one barrier per phase), the two triangular solves by
+//    one wave with the right-hand side in registers (no barriers), retraction and the
+//    convergence test as before.
+constexpr int kLdsN = 126;            // P <= 19
+constexpr int kEB = 56;               // per edge: A (49) then v (7), f64
+
+// Contribution lists of a solve (edges touching each 7x7 block, in the serial loop's
+// order).  blk_start [(P-1)^2 + 1], blk_list [4E] (e << 2 | kind; kind 0: +A (Hii), 1: -A
+// (Hij), 2: -A (Hji), 3: +A (Hjj)); vec_start [P], vec_list [2E] (e << 1 | 0: -v at pose i,
+// 1: +v at pose j).  Indices are those of the system (pose rank - 1; rank 0 is fixed).
+__global__ __launch_bounds__(kSolveThreads) void gn_lists_kernel(
+    const int* __restrict__ rank_ii, const int* __restrict__ rank_jj, int E, int P,
+    int* __restrict__ blk_start, int* __restrict__ blk_list, int* __restrict__ vec_start,
+    int* __restrict__ vec_list) {
+  const int np = P - 1, nb = np * np;
+  __shared__ int cnt[kLdsN / 7 * kLdsN / 7 + 1];
+  __shared__ int vcnt[kLdsN / 7 + 1];
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const int bi = b / np, bj = b % np;
+    int c = 0;
+    for (int e = 0; e < E; e++) {
+      const int oi = rank_ii[e] - 1, oj = rank_jj[e] - 1;
+      c += (oi >= 0 && bi == oi && bj == oi) + (oi >= 0 && oj >= 0 && bi == oi && bj == oj) +
+           (oi >= 0 && oj >= 0 && bi == oj && bj == oi) + (oj >= 0 && bi == oj && bj == oj);
+    }
+    cnt[b] = c;
+  }
+  for (int p = threadIdx.x; p < np; p += blockDim.x) {
+    int c = 0;
+    for (int e = 0; e < E; e++) c += (rank_ii[e] - 1 == p) + (rank_jj[e] - 1 == p);
+    vcnt[p] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // exclusive scans (<= 324 + 18 entries)
+    int a = 0;
+    for (int b = 0; b < nb; b++) {
+      blk_start[b] = a;
+      a += cnt[b];
+    }
+    blk_start[nb] = a;
+    a = 0;
+    for (int p = 0; p < np; p++) {
+      vec_start[p] = a;
+      a += vcnt[p];
+    }
+    vec_start[np] = a;
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const int bi = b / np, bj = b % np;
+    int w = blk_start[b];
+    for (int e = 0; e < E; e++) {
+      const int oi = rank_ii[e] - 1, oj = rank_jj[e] - 1;
+      if (oi >= 0 && bi == oi && bj == oi) blk_list[w++] = e << 2 | 0;
+      if (oi >= 0 && oj >= 0 && bi == oi && bj == oj) blk_list[w++] = e << 2 | 1;
+      if (oi >= 0 && oj >= 0 && bi == oj && bj == oi) blk_list[w++] = e << 2 | 2;
+      if (oj >= 0 && bi == oj && bj == oj) blk_list[w++] = e << 2 | 3;
+    }
+  }
+  for (int p = threadIdx.x; p < np; p += blockDim.x) {
+    int w = vec_start[p];
+    for (int e = 0; e < E; e++) {
+      if (rank_ii[e] - 1 == p) vec_list[w++] = e << 1 | 0;
+      if (rank_jj[e] - 1 == p) vec_list[w++] = e << 1 | 1;
+    }
+  }
+}
+
+// LDS written by some lanes of a wave, then read by others of the same wave: wait for the
+// writes and keep the compiler from moving accesses across (wave-scope fence)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+struct LdsLists {
+  const int *blk_start, *blk_list, *vec_start, *vec_list;
+};
+
+__global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
+    float* __restrict__ Twc, const float* __restrict__ partial, const int* __restrict__ rank_ii,
+    double* __restrict__ EB, LdsLists lists, float* __restrict__ dx_out,
+    int* __restrict__ flags, int E, int S, int P, float delta_thresh,
+    const double* __restrict__ G_in) {
+  if (flags[0]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n = 7 * (P - 1);
+  const int nt = blockDim.x;
+  constexpr int NW = kSolveThreads / 64;
+  __shared__ double sA[kLdsN * kLdsN];
+  __shared__ double sb[kLdsN];
+  __shared__ double sW[NW][4][49];      // per wave: M, G, T (A reuses G), v' / v
+  __shared__ int s_fail;
+  __shared__ float s_red[NW];
+
+  // 1) per edge (wave w: edges w, w + NW, ...): G → M, T = M G, A = T Mᵀ, v = M v'
+  double (*M)[7] = reinterpret_cast<double(*)[7]>(sW[wv][0]);
+  double (*Gm)[7] = reinterpret_cast<double(*)[7]>(sW[wv][1]);
+  double (*T)[7] = reinterpret_cast<double(*)[7]>(sW[wv][2]);
+  double* vp = sW[wv][3];
+  for (int e = wv; e < E; e += NW) {
+    const int ix = rank_ii[e];
+    // the edge's 35 sums (the f64 reduction of gn_solve_kernel step 1, same order)
+    double g = 0.0;
+    if (lane < kAcc) {
+      if (G_in) {
+        g = G_in[e * kAcc + lane];
+      } else {
+        for (int s = 0; s < S; s++) g += (double)partial[((int64_t)e * S + s) * kAcc + lane];
+      }
+    }
+    // lanes 0..27: the packed upper triangle → symmetric G; 28..34: v'
+    if (lane < 28) {
+      int r = 0;
+      while ((r + 1) * (r + 2) / 2 <= lane) r++;
+      const int c = lane - r * (r + 1) / 2;
+      Gm[r][c] = g;
+      Gm[c][r] = g;
+    } else if (lane < kAcc) {
+      vp[lane - 28] = g;
+    }
+    if (lane < 7) {
+      const float* Ti = Twc + 8 * ix;
+      const double t[3] = {Ti[0], Ti[1], Ti[2]};
+      const double q[4] = {Ti[3], Ti[4], Ti[5], Ti[6]};
+      const double s = Ti[7];
+      double X[7] = {0, 0, 0, 0, 0, 0, 0};
+      X[lane] = 1.0;
+      double Y[7];
+      m3s_adj_inv_apply<double>(t, q, s, X, Y);
+      for (int r = 0; r < 7; r++) M[r][lane] = Y[r];
+    }
+    wave_lds_sync();                             // this wave's scratch writes visible
+    double* out = EB + (int64_t)e * kEB;
+    if (lane < 49) {  // T = M G
+      const int r = lane / 7, c = lane % 7;
+      double v = 0.0;
+      for (int k = 0; k < 7; k++) v += M[r][k] * Gm[k][c];
+      T[r][c] = v;
+    }
+    double vj = 0.0;
+    if (lane >= 56 && lane < 63) {  // vj = M v'
+      const int r = lane - 56;
+      for (int k = 0; k < 7; k++) vj += M[r][k] * vp[k];
+    }
+    wave_lds_sync();
+    if (lane < 49) {  // A = T Mᵀ
+      const int r = lane / 7, c = lane % 7;
+      double v = 0.0;
+      for (int k = 0; k < 7; k++) v += T[r][k] * M[c][k];
+      out[lane] = v;
+    } else if (lane >= 56 && lane < 63) {
+      out[49 + lane - 56] = vj;
+    }
+    wave_lds_sync();                             // scratch reused by the next edge
+  }
+  if (tid == 0) s_fail = 0;
+  __threadfence_block();
+  __syncthreads();
+
+  // 2) assembly by ownership, contributions in the serial loop's order
+  const int np = P - 1;
+  for (int idx = tid; idx < n * n; idx += nt) {
+    const int row = idx / n, col = idx - row * n;
+    const int bi = row / 7, r = row - 7 * bi, bj = col / 7, c = col - 7 * bj;
+    const int b = bi * np + bj;
+    double a = 0.0;
+    for (int k = lists.blk_start[b]; k < lists.blk_start[b + 1]; k++) {
+      const int code = lists.blk_list[k];
+      const double v = EB[(int64_t)(code >> 2) * kEB + r * 7 + c];
+      const int kind = code & 3;
+      if (kind == 0 || kind == 3) a += v;
+      else a -= v;
+    }
+    sA[idx] = a;
+  }
+  for (int row = tid; row < n; row += nt) {
+    const int p = row / 7, r = row - 7 * p;
+    double bv = 0.0;
+    for (int k = lists.vec_start[p]; k < lists.vec_start[p + 1]; k++) {
+      const int code = lists.vec_list[k];
+      const double v = EB[(int64_t)(code >> 1) * kEB + 49 + r];
+      if (code & 1) bv += v;
+      else bv -= v;
+    }
+    sb[row] = bv;
+  }
+  __syncthreads();
+
+  // 3) right-looking Cholesky in LDS (gn_solve_kernel step 3's operations and order)
+  for (int k = 0; k < n; k++) {
+    if (tid == 0) {
+      const double d = sA[k * n + k];
+      if (!(d > 0.0)) s_fail = 1;
+      sA[k * n + k] = sqrt(d);
+    }
+    __syncthreads();
+    if (s_fail) break;
+    const double piv = sA[k * n + k];
+    for (int i = k + 1 + tid; i < n; i += nt) sA[i * n + k] /= piv;
+    __syncthreads();
+    const int m = n - k - 1;
+    for (int idx = tid; idx < m * m; idx += nt) {
+      const int i = idx / m, j = idx - i * m;
+      if (j > i) continue;
+      const int gi = k + 1 + i, gj = k + 1 + j;
+      sA[gi * n + gj] -= sA[gi * n + k] * sA[gj * n + k];
+    }
+    __syncthreads();
+  }
+
+  // 4) L y = b, Lᵀ x = y by wave 0, rows i = lane + 64 t in registers (t < 2: n <= 128)
+  if (wv == 0 && !s_fail) {
+    double x0 = lane < n ? sb[lane] : 0.0, x1 = lane + 64 < n ? sb[lane + 64] : 0.0;
+    for (int j = 0; j < n; j++) {
+      const int owner = j & 63;
+      double yj = j < 64 ? x0 : x1;
+      if (lane == owner) yj = yj / sA[j * n + j];
+      yj = __shfl(yj, owner, 64);
+      if (lane == owner) {
+        if (j < 64) x0 = yj;
+        else x1 = yj;
+      }
+      if (lane > j && lane < n) x0 -= sA[lane * n + j] * yj;
+      if (lane + 64 > j && lane + 64 < n) x1 -= sA[(lane + 64) * n + j] * yj;
+    }
+    for (int j = n - 1; j >= 0; j--) {
+      const int owner = j & 63;
+      double xj = j < 64 ? x0 : x1;
+      if (lane == owner) xj = xj / sA[j * n + j];
+      xj = __shfl(xj, owner, 64);
+      if (lane == owner) {
+        if (j < 64) x0 = xj;
+        else x1 = xj;
+      }
+      if (lane < j) x0 -= sA[j * n + lane] * xj;
+      if (lane + 64 < j) x1 -= sA[j * n + lane + 64] * xj;
+    }
+    if (lane < n) sb[lane] = x0;
+    if (lane + 64 < n) sb[lane + 64] = x1;
+  }
+  __syncthreads();
+
+  // 5) dx = -x (zero on failure, gn_kernels.cu:147-150), retract poses 1..P-1
+  for (int idx = tid; idx < n; idx += nt) dx_out[idx] = s_fail ? 0.f : (float)(-sb[idx]);
+  __syncthreads();
+  for (int p = 1 + tid; p < P; p += nt) {
+    float* Tp = Twc + 8 * p;
+    const float* xi = dx_out + 7 * (p - 1);
+    float t1[3], q1[4], s1;
+    m3s_retr_sim3<float>(xi, Tp, Tp + 3, Tp[7], t1, q1, &s1);
+    Tp[0] = t1[0];
+    Tp[1] = t1[1];
+    Tp[2] = t1[2];
+    Tp[3] = q1[0];
+    Tp[4] = q1[1];
+    Tp[5] = q1[2];
+    Tp[6] = q1[3];
+    Tp[7] = s1;
+  }
+  // 6) termination: ||dx|| < delta_thresh (gn_kernels.cu:1217-1222)
+  float ss = 0.f;
+  for (int idx = tid; idx < n; idx += nt) ss += dx_out[idx] * dx_out[idx];
+  ss = m3s_wave_sum(ss);
+  if (lane == 0) s_red[wv] = ss;
+  __syncthreads();
+  if (tid == 0) {
+    float tot = 0.f;
+    for (int w = 0; w < nt / 64; w++) tot += s_red[w];
+    flags[3] += 1;
+    if (s_fail) flags[1] = 1;
+    if (sqrtf(tot) < delta_thresh) flags[0] = 1;
+  }
+}
+
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 int choose_splits(int64_t E, int64_t N) {
@@ -505,8 +792,26 @@ int choose_splits(int64_t E, int64_t N) {
 }
 
 struct Layout {
-  size_t flags, rank_ii, rank_jj, partial, A, b, G, total;
+  size_t flags, rank_ii, rank_jj, partial, A, b, G, EB, blk_start, blk_list, vec_start, vec_list,
+      total;
 };
+
+// the LDS solve's regions (EB, contribution lists) appended at `off`
+template <class L>
+size_t lds_regions(L& l, size_t off, int64_t P, int64_t E) {
+  const int64_t np = P > 1 ? P - 1 : 0;
+  l.EB = off;
+  off = align_up(off + 8 * kEB * E, 256);
+  l.blk_start = off;
+  off = align_up(off + 4 * (np * np + 1), 256);
+  l.blk_list = off;
+  off = align_up(off + 4 * 4 * E, 256);
+  l.vec_start = off;
+  off = align_up(off + 4 * (np + 1), 256);
+  l.vec_list = off;
+  off = align_up(off + 4 * 2 * E, 256);
+  return off;
+}
 
 Layout make_layout(int64_t P, int64_t E, int S) {
   Layout L;
@@ -526,8 +831,31 @@ Layout make_layout(int64_t P, int64_t E, int S) {
   off = align_up(off + 8 * n, 256);
   L.G = off;
   off = align_up(off + 8 * E * kAcc, 256);
-  L.total = off;
+  L.total = lds_regions(L, off, P, E);
   return L;
+}
+
+bool g_force_global_solve = false;   // m3s_gn_force_global_solve (diagnostic)
+bool use_lds_solve(int64_t P) { return P > 1 && 7 * (P - 1) <= kLdsN && !g_force_global_solve; }
+
+template <class L>
+LdsLists lds_lists(char* ws, const L& l) {
+  return LdsLists{reinterpret_cast<const int*>(ws + l.blk_start),
+                  reinterpret_cast<const int*>(ws + l.blk_list),
+                  reinterpret_cast<const int*>(ws + l.vec_start),
+                  reinterpret_cast<const int*>(ws + l.vec_list)};
+}
+
+template <class L>
+int launch_lists(char* ws, const L& l, const int* rii, const int* rjj, int64_t E, int64_t P,
+                 hipStream_t st) {
+  hipLaunchKernelGGL(gn_lists_kernel, dim3(1), dim3(kSolveThreads), 0, st, rii, rjj, (int)E,
+                     (int)P, reinterpret_cast<int*>(ws + l.blk_start),
+                     reinterpret_cast<int*>(ws + l.blk_list),
+                     reinterpret_cast<int*>(ws + l.vec_start),
+                     reinterpret_cast<int*>(ws + l.vec_list));
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
 }
 
 template <int MODE>
@@ -557,15 +885,25 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
   hipLaunchKernelGGL(gn_rank_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_ii, d_jj, (int)E, rii,
                      rjj, flags);
   M3S_LAUNCH_CHECK();
+  const bool lds = use_lds_solve(P);
+  if (lds) {
+    const int st_l = launch_lists(ws, L, rii, rjj, E, P, st);
+    if (st_l != M3S_OK) return st_l;
+  }
   if (P > 1) {
     for (int it = 0; it < max_iter; it++) {
       hipLaunchKernelGGL(gn_edge_kernel<MODE>, dim3((unsigned)E, (unsigned)S),
                          dim3(kEdgeThreads), 0, st, d_Twc, d_Xs, d_Cs, d_K, rii, rjj, d_idx,
                          d_valid, d_Q, partial, flags, N, S, prm, nullptr);
       M3S_LAUNCH_CHECK();
-      hipLaunchKernelGGL(gn_solve_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_Twc, partial,
-                         rii, rjj, A, b, G, d_dx, flags, (int)E, S, (int)P, delta_thresh,
-                         nullptr);
+      if (lds)
+        hipLaunchKernelGGL(gn_solve_lds_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_Twc,
+                           partial, rii, reinterpret_cast<double*>(ws + L.EB), lds_lists(ws, L),
+                           d_dx, flags, (int)E, S, (int)P, delta_thresh, nullptr);
+      else
+        hipLaunchKernelGGL(gn_solve_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_Twc, partial,
+                           rii, rjj, A, b, G, d_dx, flags, (int)E, S, (int)P, delta_thresh,
+                           nullptr);
       M3S_LAUNCH_CHECK();
     }
   }
@@ -584,7 +922,8 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
 // edges, the dense system.  S comes from E_total, so every edge's partials — hence its G
 // row — are those of the unsharded m3s_gauss_newton_* call, bit for bit.
 struct ShardLayout {
-  size_t flags, rank_ii, rank_jj, partial, A, b, total;
+  size_t flags, rank_ii, rank_jj, partial, A, b, EB, blk_start, blk_list, vec_start, vec_list,
+      total;
   int S;
 };
 
@@ -605,7 +944,7 @@ ShardLayout make_shard_layout(int64_t P, int64_t E_total, int64_t E_local, int64
   off = align_up(off + 8 * n * n, 256);
   L.b = off;
   off = align_up(off + 8 * (n > 0 ? n : 1), 256);
-  L.total = off;
+  L.total = lds_regions(L, off, P, E_total);
   return L;
 }
 
@@ -643,6 +982,11 @@ int shard_edge_pass(const float* d_Twc, const float* d_Xs, const float* d_Cs, co
 
 }  // namespace
 
+extern "C" int m3s_gn_force_global_solve(int on) {
+  g_force_global_solve = on != 0;
+  return M3S_OK;
+}
+
 extern "C" size_t m3s_gn_sharded_workspace_bytes(int64_t num_poses, int64_t num_edges_total,
                                                  int64_t num_edges_local, int64_t num_points) {
   if (!shard_sizes_ok(num_poses, num_points, num_edges_total, num_edges_local)) return 256;
@@ -666,6 +1010,9 @@ extern "C" int m3s_gn_sharded_begin(const int64_t* d_ii, const int64_t* d_jj, in
                      reinterpret_cast<int*>(ws + L.rank_ii), reinterpret_cast<int*>(ws + L.rank_jj),
                      reinterpret_cast<int*>(ws + L.flags));
   M3S_LAUNCH_CHECK();
+  if (use_lds_solve(P))
+    return launch_lists(ws, L, reinterpret_cast<const int*>(ws + L.rank_ii),
+                        reinterpret_cast<const int*>(ws + L.rank_jj), E, P, st);
   return M3S_OK;
 }
 
@@ -716,6 +1063,15 @@ extern "C" int m3s_gn_solve_step(float* d_Twc, const double* d_G, int64_t num_po
   if (!d_Twc || !d_G || !d_dx) return M3S_ERR_INVALID_ARG;
   const ShardLayout L = make_shard_layout(P, E, num_edges_local, num_points);
   char* ws = reinterpret_cast<char*>(d_ws);
+  if (use_lds_solve(P)) {
+    hipLaunchKernelGGL(gn_solve_lds_kernel, dim3(1), dim3(kSolveThreads), 0, m3s_stream(stream),
+                       d_Twc, nullptr, reinterpret_cast<const int*>(ws + L.rank_ii),
+                       reinterpret_cast<double*>(ws + L.EB), lds_lists(ws, L), d_dx,
+                       reinterpret_cast<int*>(ws + L.flags), (int)E, L.S, (int)P, delta_thresh,
+                       d_G);
+    M3S_LAUNCH_CHECK();
+    return M3S_OK;
+  }
   hipLaunchKernelGGL(gn_solve_kernel, dim3(1), dim3(kSolveThreads), 0, m3s_stream(stream), d_Twc,
                      nullptr, reinterpret_cast<const int*>(ws + L.rank_ii),
                      reinterpret_cast<const int*>(ws + L.rank_jj),

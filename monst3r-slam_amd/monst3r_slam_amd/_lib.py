@@ -41,6 +41,7 @@ SIGNATURES = {
                                     _I, _F, _F, _F, _F, _F, _I, _F, _P, _P, _P, _P]),
     "m3s_gauss_newton_points": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _F,
                                      _F, _I, _F, _P, _P, _P, _P]),
+    "m3s_gn_force_global_solve": (_I, [_I]),
     "m3s_gn_sharded_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
     "m3s_gn_sharded_begin": (_I, [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _P]),
     "m3s_gn_rays_edge_pass": (_I, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _F, _F,
