@@ -102,11 +102,17 @@ __device__ __forceinline__ void block_sync_lds() {
 // LDS images of one K/V tile (64 keys x 64 d, 128-B rows, lane-linear as the DMA writes
 // them).  16-B chunk swizzles: K (read by ds_read_b128 down 32 rows) chunk ^ ((r>>1)&7);
 // V (read by ds_read_b64_tr_b16, 4 rows x 64 B per half-wave) chunk ^ 4*((r>>1)&1).
-__device__ __forceinline__ s16x4 tr_read(const char* p) {
+// OFF: a compile-time byte offset folded into the instruction (the lane's base address is
+// computed once per tile, the chunk / row steps are immediates)
+template <int OFF>
+__device__ __forceinline__ s16x4 tr_read(uint32_t a) {
   s16x4 v;
-  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
   return v;
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
 __device__ __forceinline__ int k_swz(int r) { return (r >> 1) & 7; }
@@ -118,6 +124,7 @@ constexpr int TILE_BYTES = AKT * HD * 2;   // 8 KiB
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;
 constexpr uint32_t OOB = 0x80000000u;
 constexpr int PART_LD = HD + 4;            // split partial row: O[64], m, l, pad
+constexpr float kRescale = 8.0f;           // lazy-rescale threshold (log2 of p's headroom)
 
 // A block is AW query waves (QT query rows each) x KS key splits.  The AW waves of one
 // key split share a K/V ring and walk key tiles ks, ks + KS, ...; at the end the KS
@@ -222,14 +229,34 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
     }
   };
 
-  f32x16 oacc[2];
+  f32x16 oacc[2], lacc;
 #pragma unroll
   for (int d = 0; d < 2; d++)
 #pragma unroll
     for (int i = 0; i < 16; i++) oacc[d][i] = 0.f;
-  float m = -INFINITY, l = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; i++) lacc[i] = 0.f;
+  float m = -INFINITY;
   // tr-read lane roles inside a 16-lane group
   const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gsel = (lane >> 4) & 1;
+  // this lane's LDS offsets inside a stage, computed once: K fragment rows 32·hs + r, chunk
+  // (2 ks + hh) ^ k_swz(r) (k_swz(32 hs + r) = k_swz(r)); V^T reads of head dims d·32 + 16
+  // gsel + 4 gp at key rows 16 c + 8 x + 4 hh + gq — the chunk XOR only involves d and bit 1
+  // of gq, so (c, x) steps are the immediates c·2048 + x·1024
+  uint32_t kf_off[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ks++) kf_off[ks] = r * 128 + (((2 * ks + hh) ^ k_swz(r)) * 16);
+  uint32_t vt_off[2];
+#pragma unroll
+  for (int d = 0; d < 2; d++) {
+    const int d0 = d * 32 + 16 * gsel + 4 * gp, rr = 4 * hh + gq;
+    vt_off[d] = TILE_BYTES + rr * 128 + (((d0 >> 3) ^ v_swz(rr)) * 16) + (d0 & 7) * 2;
+  }
+  // the softmax row sum l comes out of the matrix pipe: a ones A-operand against P^T gives
+  // Σ_keys p in every accumulator row (lacc), instead of 32 adds + an exchange per tile
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; i++) ones[i] = f2bf(1.0f);
 
 #pragma unroll
   for (int st = 0; st < NST - 1; st++)
@@ -241,7 +268,7 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
     constexpr bool TAIL = decltype(tail_tag)::value;
     const int kt = kt0 + ksp + KS * j;
     const char* sK = ring + (j % NST) * STAGE_BYTES;
-    const char* sV = sK + TILE_BYTES;
+    const uint32_t sbase = lds_addr(sK);
 
     // S^T (keys x queries), two 32-key halves
     f32x16 s[2];
@@ -249,11 +276,9 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
     for (int hs = 0; hs < 2; hs++) {
 #pragma unroll
       for (int i = 0; i < 16; i++) s[hs][i] = 0.f;
-      const int row = hs * 32 + r;
 #pragma unroll
       for (int ks = 0; ks < 4; ks++) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(
-            sK + row * 128 + (((2 * ks + hh) ^ k_swz(row)) * 16));
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(sK + kf_off[ks] + hs * 32 * 128);
         s[hs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[hs], 0, 0, 0);
       }
     }
@@ -270,41 +295,47 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
         tmax = fmaxf(tmax, s[hs][i]);
       }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m, tmax);
-    const float alpha = __builtin_amdgcn_exp2f((m - m_new) * c_log2);  // m = -inf → 0
-    const float mc = m_new * c_log2;
-    float rs = 0.f;
+    // lazy rescale (cdna_hip_programming.md T13): the running max m only moves when a
+    // query's tile max exceeds it by more than 2^RESCALE in p; otherwise p = 2^((s - m) c)
+    // may grow up to 2^RESCALE (exact in f32, bf16-rounded like any p) and O / l need no
+    // rescaling — wave-uniform, so after the first tiles the 48 multiplies are skipped
+    const bool need = (tmax - m) * c_log2 > kRescale;   // m = -inf: always
+    if (__builtin_amdgcn_ballot_w64(need)) {
+      const float m_new = fmaxf(m, tmax);
+      const float alpha = __builtin_amdgcn_exp2f((m - m_new) * c_log2);  // m = -inf → 0
+      m = m_new;
+#pragma unroll
+      for (int d = 0; d < 2; d++)
+#pragma unroll
+        for (int i = 0; i < 16; i++) oacc[d][i] *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; i++) lacc[i] *= alpha;
+    }
+    const float mc = m * c_log2;
     bf16x8 pf[4];  // P^T B operands, 16-key chunks (2 hs + ss)
 #pragma unroll
     for (int hs = 0; hs < 2; hs++)
 #pragma unroll
       for (int i = 0; i < 16; i++) {
         const float p = __builtin_amdgcn_exp2f(s[hs][i] * c_log2 - mc);  // -inf → 0
-        rs += p;
         pf[2 * hs + (i >> 3)][i & 7] = f2bf(p);
       }
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = m_new;
-#pragma unroll
-    for (int d = 0; d < 2; d++)
-#pragma unroll
-      for (int i = 0; i < 16; i++) oacc[d][i] *= alpha;
     // O^T += V^T P^T; chunk (hs, ss) B rows are keys 32hs + 16ss + {0-3, 8-11} + 4hh.
     // The transposed reads are inline asm: as an intrinsic the compiler cannot tell they
     // do not alias the DMA ring and would drain it (vmcnt(0)) before each of them.
     s16x4 vt[2][4][2];
+#define M3S_TR(d, c, x) vt[d][c][x] = tr_read<(c) * 2048 + (x) * 1024>(sbase + vt_off[d])
+#define M3S_TR_D(d)                                                                        \
+  M3S_TR(d, 0, 0); M3S_TR(d, 0, 1); M3S_TR(d, 1, 0); M3S_TR(d, 1, 1); M3S_TR(d, 2, 0);     \
+  M3S_TR(d, 2, 1); M3S_TR(d, 3, 0); M3S_TR(d, 3, 1)
+    M3S_TR_D(0);
+    M3S_TR_D(1);
+#undef M3S_TR_D
+#undef M3S_TR
+    // row sums first: their MFMAs need no V and cover the transposed reads' latency
 #pragma unroll
-    for (int d = 0; d < 2; d++) {
-      const int d0 = d * 32 + 16 * gsel + 4 * gp;
-#pragma unroll
-      for (int c = 0; c < 4; c++)
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-          const int rr = 16 * c + 8 * x + 4 * hh + gq;
-          vt[d][c][x] = tr_read(sV + rr * 128 + (((d0 >> 3) ^ v_swz(rr)) * 16) + (d0 & 7) * 2);
-        }
-    }
+    for (int c = 0; c < 4; c++)
+      lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[c], lacc, 0, 0, 0);
     // the waits name the read results as operands, so no MFMA can be hoisted above them
 #define M3S_VT(d) "+v"(vt[d][0][0]), "+v"(vt[d][0][1]), "+v"(vt[d][1][0]), "+v"(vt[d][1][1]), \
                   "+v"(vt[d][2][0]), "+v"(vt[d][2][1]), "+v"(vt[d][3][0]), "+v"(vt[d][3][1])
@@ -350,6 +381,7 @@ __global__ __launch_bounds__(AW * KS * 64, 2) void attn_kernel(
   };
   for (int j = 0; j + 1 < nj; j++) trip(j, std::false_type{});
   if (nj > 0) trip(nj - 1, std::integral_constant<bool, TAILS>{});
+  float l = lacc[0];   // every accumulator row holds this query's Σ p
   if constexpr (KS > 1) {
     // merge the key splits of each query wave: lane-aligned (same accumulator layout)
     block_sync_lds();  // ring reads done (the last trip waited for all DMA)

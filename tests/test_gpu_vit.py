@@ -162,6 +162,14 @@ def test_attention_shapes_vs_fp32(ops, dev, monkeypatch, Sq, Sk, heads, batch, k
     D = heads * 64
     q = torch.randn(batch, Sq, D, device=dev, generator=g).bfloat16()
     kv = (torch.randn(batch, Sk, 2 * D, device=dev, generator=g) * 2).bfloat16()
+    if Sk > 640:
+        # a late key that dominates query 5 of every head (score ~ +230 in the key split
+        # that owns it): the running max jumps after many tiles, forcing the lazy-rescale
+        # branch (kRescale) where the earlier tiles' O and l must be rescaled
+        kb = kv.clone()
+        kb[:, Sk - 70, :D] = (q[:, 5, :] * 4).bfloat16() if not kv_xor else \
+            (q[[1, 0], 5, :] * 4).bfloat16()
+        kv = kb.contiguous()
     o = torch.full((batch, Sq, D), 0x7F if fp8 else 7, device=dev,
                    dtype=torch.uint8 if fp8 else torch.bfloat16)
     ops.attn(q, D, Sq * D, kv, kv[:, :, D:], 2 * D, Sk * 2 * D, o, D, Sq * D, batch, heads,

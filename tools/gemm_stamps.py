@@ -4,7 +4,7 @@ s_memrealtime (100 MHz, chip-wide) at block start / end: the in-kernel clock (Δ
 Δrealtime), each block's lifetime in µs, and the launch's block-start spread and span
 against the HIP-event time.  Split-K blocks that exit after publishing their partial are
 stamped too (column 'early').  Needs `make -C monst3r-slam_amd/csrc stamps`.
-  python tools/gemm_stamps.py"""
+  python tools/gemm_stamps.py ["name,M,N,K,batch,tile,split,fused" ...]"""
 import ctypes
 import os
 import sys
@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "monst3r-slam_amd")]
 from monst3r_slam_amd import _lib  # noqa: E402
 
-lib = ctypes.CDLL(os.path.join(ROOT, "monst3r-slam_amd/csrc/build/libm3s_gemm_stamps.so"))
+lib = ctypes.CDLL(os.environ.get("M3S_STAMPS_LIB") or
+                  os.path.join(ROOT, "monst3r-slam_amd/csrc/build/libm3s_gemm_stamps.so"))
 lib.m3s_vit_gemm.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 lib.m3s_debug_set_stamps.argtypes = [ctypes.c_void_p]
 dev = torch.device("cuda:0")
@@ -47,6 +48,8 @@ shapes = [("enc fc2", 768, 1024, 4096, 1, 2, 1, 0), ("enc fc2", 768, 1024, 4096,
           ("enc proj", 768, 1024, 1024, 1, 2, 1, 0), ("enc proj", 768, 1024, 1024, 1, 1, 2, 0),
           ("enc fc1", 768, 4096, 1024, 1, 1, 1, 0), ("dec fc2", 768, 768, 3072, 4, 1, 1, 0),
           ("big", 4096, 4096, 4096, 1, 1, 1, 0), ("big", 4096, 4096, 4096, 1, 7, 1, 0)]
+if len(sys.argv) > 1:   # "name,M,N,K,b,tile,split,fused" per argument
+    shapes = [(a.split(",")[0], *[int(x) for x in a.split(",")[1:]]) for a in sys.argv[1:]]
 for name, M, N, K, b, tile, split, fused in shapes:
     A = torch.randn(b, M, K, device=dev).bfloat16()
     B = (torch.randn(b, N, K, device=dev) / K ** 0.5).bfloat16()
