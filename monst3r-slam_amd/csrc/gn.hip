@@ -45,29 +45,127 @@ struct GnWork {
   double* G;           // [E][kAcc] reduced per edge (scratch for the solve kernel)
 };
 
-__device__ __forceinline__ float huber_ref(float r) {
-  // gn_kernels.cu:172-175 (constant hard-coded, compared and divided in double)
+// Huber weight (gn_kernels.cu:172-175).  The reference compares and divides in double
+// (its 1.345 is a double literal); here both are fp32: the comparison is exact (1.345f is
+// the next float above 1.345, so r < 1.345 <=> r < 1.345f for every float r) and the weight
+// 1.345f / r is within 1 ulp of (float)(1.345 / (double)r) — six fp64 divisions per point
+// were a third of the edge pass.
+__device__ __forceinline__ float huber_w(float r) {
   const float r_abs = fabsf(r);
-  return (double)r_abs < 1.345 ? 1.0f : (float)(1.345 / (double)r_abs);
+  return r_abs < 1.345f ? 1.0f : 1.345f / r_abs;
 }
 
-__device__ __forceinline__ float inv_ref(float x) { return (float)(1.0 / (double)x); }
+// 1 / x (the reference: 1.0 / x in double, rounded to float); the correctly rounded fp32
+// quotient differs from it only where the double quotient rounds twice (<= 1 ulp)
+__device__ __forceinline__ float inv_f(float x) { return 1.0f / x; }
 
-// Accumulate one weighted row into the 35 sums.
+// Accumulate one weighted row into the 35 sums.  MASK (bit n: J[n] may be nonzero) is the
+// row's compile-time sparsity: the zero entries' products are never formed (an exact zero
+// added to a finite sum leaves it unchanged), which takes the rays rows from 35 to 15-19
+// multiply-adds each.  Fused multiply-adds, as the reference's nvcc build contracts them.
+template <int MASK>
 __device__ __forceinline__ void acc_row(float* acc, float w, float e, const float* J) {
-  int l = 0;
 #pragma unroll
   for (int n = 0; n < 7; n++) {
+    if (!((MASK >> n) & 1)) continue;
     const float wj = w * J[n];
 #pragma unroll
-    for (int m = 0; m <= n; m++) {
-      acc[l] += wj * J[m];
-      l++;
-    }
+    for (int m = 0; m <= n; m++)
+      if ((MASK >> m) & 1) acc[n * (n + 1) / 2 + m] = __builtin_fmaf(wj, J[m], acc[n * (n + 1) / 2 + m]);
   }
   const float we = w * e;
 #pragma unroll
-  for (int n = 0; n < 7; n++) acc[28 + n] += we * J[n];
+  for (int n = 0; n < 7; n++)
+    if ((MASK >> n) & 1) acc[28 + n] = __builtin_fmaf(we, J[n], acc[28 + n]);
+}
+
+// One point's residual rows accumulated into the 35 sums (per-point bodies of
+// ray_align_kernel gn_kernels.cu:813-1138, calib_proj_kernel :1231-1543, point_align_kernel :455-723).
+template <int MODE>
+__device__ __forceinline__ void point_acc(float* acc, bool vm, int64_t ind, const float* Xi,
+                                          float ci, const float* Xj, float q, float cj,
+                                          const float* tij, const float* qij, float sij,
+                                          const GnParams& prm, float fx, float fy, float cx,
+                                          float cy) {
+  float P[3];
+  m3s_act_sim3<float>(tij, qij, sij, Xj, P);
+  bool valid = vm & (q > prm.Q_thresh) & (ci > prm.C_thresh) & (cj > prm.C_thresh);
+
+  if (MODE == MODE_RAYS) {
+    const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
+    const float n1i = sqrtf(n2i);
+    const float n1i_inv = inv_f(n1i);
+    const float n2j = P[0] * P[0] + P[1] * P[1] + P[2] * P[2];
+    const float n1j = sqrtf(n2j);
+    const float n1j_inv = inv_f(n1j);
+    const float rj[3] = {n1j_inv * P[0], n1j_inv * P[1], n1j_inv * P[2]};
+    const float err[4] = {rj[0] - n1i_inv * Xi[0], rj[1] - n1i_inv * Xi[1],
+                          rj[2] - n1i_inv * Xi[2], n1j - n1i};
+    const float sq = sqrtf(q);
+    const float swr = valid ? prm.s0_inv * sq : 0.f;
+    const float swd = valid ? prm.s1_inv * sq : 0.f;
+    const float cr = swr * swr, cd = swd * swd;
+    const float w[4] = {huber_w(swr * err[0]) * cr, huber_w(swr * err[1]) * cr,
+                        huber_w(swr * err[2]) * cr, huber_w(swd * err[3]) * cd};
+    const float n3_inv = n1j_inv / n2j;
+    const float dxx = n1j_inv - P[0] * P[0] * n3_inv;
+    const float dyy = n1j_inv - P[1] * P[1] * n3_inv;
+    const float dzz = n1j_inv - P[2] * P[2] * n3_inv;
+    const float dxy = -P[0] * P[1] * n3_inv;
+    const float dxz = -P[0] * P[2] * n3_inv;
+    const float dyz = -P[1] * P[2] * n3_inv;
+    const float J0[7] = {dxx, dxy, dxz, 0.f, rj[2], -rj[1], 0.f};
+    const float J1[7] = {dxy, dyy, dyz, -rj[2], 0.f, rj[0], 0.f};
+    const float J2[7] = {dxz, dyz, dzz, rj[1], -rj[0], 0.f, 0.f};
+    const float J3[7] = {rj[0], rj[1], rj[2], 0.f, 0.f, 0.f, n1j};
+    acc_row<0x37>(acc, w[0], err[0], J0);
+    acc_row<0x2F>(acc, w[1], err[1], J1);
+    acc_row<0x1F>(acc, w[2], err[2], J2);
+    acc_row<0x47>(acc, w[3], err[3], J3);
+  } else if (MODE == MODE_CALIB) {
+    const int u_t = (int)ind % prm.width;  // ind < num_points < 2^31
+    const int v_t = (int)ind / prm.width;
+    const bool valid_z = (P[2] > prm.z_eps) && (Xi[2] > prm.z_eps);
+    const float zj_inv = valid_z ? inv_f(P[2]) : 0.f;
+    const float zj_log = valid_z ? logf(P[2]) : 0.f;
+    const float zi_log = valid_z ? logf(Xi[2]) : 0.f;
+    const float xz = P[0] * zj_inv;
+    const float yz = P[1] * zj_inv;
+    const float u = fx * xz + cx;
+    const float v = fy * yz + cy;
+    const bool valid_u = (u > (float)prm.pixel_border) &&
+                         (u < (float)(prm.width - 1 - prm.pixel_border));
+    const bool valid_v = (v > (float)prm.pixel_border) &&
+                         (v < (float)(prm.height - 1 - prm.pixel_border));
+    valid = valid & valid_u & valid_v & valid_z;
+    const float err[3] = {u - (float)u_t, v - (float)v_t, zj_log - zi_log};
+    const float sq = sqrtf(q);
+    const float swp = valid ? prm.s0_inv * sq : 0.f;
+    const float swd = valid ? prm.s1_inv * sq : 0.f;
+    const float cp = swp * swp, cd = swd * swd;
+    const float w[3] = {huber_w(swp * err[0]) * cp, huber_w(swp * err[1]) * cp,
+                        huber_w(swd * err[2]) * cd};
+    const float J0[7] = {fx * zj_inv, 0.f, -fx * xz * zj_inv, -fx * xz * yz,
+                         fx * (1.f + xz * xz), -fx * yz, 0.f};
+    const float J1[7] = {0.f, fy * zj_inv, -fy * yz * zj_inv, -fy * (1.f + yz * yz),
+                         fy * xz * yz, fy * xz, 0.f};
+    const float J2[7] = {0.f, 0.f, zj_inv, yz, -xz, 0.f, 1.f};
+    acc_row<0x3D>(acc, w[0], err[0], J0);
+    acc_row<0x3E>(acc, w[1], err[1], J1);
+    acc_row<0x5C>(acc, w[2], err[2], J2);
+  } else {  // MODE_POINTS
+    const float err[3] = {P[0] - Xi[0], P[1] - Xi[1], P[2] - Xi[2]};
+    const float swp = valid ? prm.s0_inv * sqrtf(q) : 0.f;
+    const float cp = swp * swp;
+    const float w[3] = {huber_w(swp * err[0]) * cp, huber_w(swp * err[1]) * cp,
+                        huber_w(swp * err[2]) * cp};
+    const float J0[7] = {1.f, 0.f, 0.f, 0.f, P[2], -P[1], P[0]};
+    const float J1[7] = {0.f, 1.f, 0.f, -P[2], 0.f, P[0], P[1]};
+    const float J2[7] = {0.f, 0.f, 1.f, P[1], -P[0], 0.f, P[2]};
+    acc_row<0x71>(acc, w[0], err[0], J0);
+    acc_row<0x6A>(acc, w[1], err[1], J1);
+    acc_row<0x5C>(acc, w[2], err[2], J2);
+  }
 }
 
 template <int MODE>
@@ -108,92 +206,41 @@ __global__ __launch_bounds__(kEdgeThreads) void gn_edge_kernel(
   const float* Cj_base = Cs + (int64_t)jx * num_points;
   const int64_t eoff = (int64_t)e * num_points;
 
-  for (int64_t k = k0 + threadIdx.x; k < k1; k += kEdgeThreads) {
-    const bool vm = valid_match[eoff + k] != 0;
-    const int64_t ind = vm ? idx_ii2jj[eoff + k] : 0;
-    const float Xi[3] = {Xi_base[3 * ind], Xi_base[3 * ind + 1], Xi_base[3 * ind + 2]};
-    const float Xj[3] = {Xj_base[3 * k], Xj_base[3 * k + 1], Xj_base[3 * k + 2]};
-    float P[3];
-    m3s_act_sim3<float>(tij, qij, sij, Xj, P);
-    const float q = Q[eoff + k];
-    const float ci = Ci_base[ind];
-    const float cj = Cj_base[k];
-    bool valid = vm & (q > prm.Q_thresh) & (ci > prm.C_thresh) & (cj > prm.C_thresh);
-
-    if (MODE == MODE_RAYS) {
-      const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
-      const float n1i = sqrtf(n2i);
-      const float n1i_inv = inv_ref(n1i);
-      const float n2j = P[0] * P[0] + P[1] * P[1] + P[2] * P[2];
-      const float n1j = sqrtf(n2j);
-      const float n1j_inv = inv_ref(n1j);
-      const float rj[3] = {n1j_inv * P[0], n1j_inv * P[1], n1j_inv * P[2]};
-      const float err[4] = {rj[0] - n1i_inv * Xi[0], rj[1] - n1i_inv * Xi[1],
-                            rj[2] - n1i_inv * Xi[2], n1j - n1i};
-      const float sq = sqrtf(q);
-      const float swr = valid ? prm.s0_inv * sq : 0.f;
-      const float swd = valid ? prm.s1_inv * sq : 0.f;
-      const float cr = swr * swr, cd = swd * swd;
-      const float w[4] = {huber_ref(swr * err[0]) * cr, huber_ref(swr * err[1]) * cr,
-                          huber_ref(swr * err[2]) * cr, huber_ref(swd * err[3]) * cd};
-      const float n3_inv = n1j_inv / n2j;
-      const float dxx = n1j_inv - P[0] * P[0] * n3_inv;
-      const float dyy = n1j_inv - P[1] * P[1] * n3_inv;
-      const float dzz = n1j_inv - P[2] * P[2] * n3_inv;
-      const float dxy = -P[0] * P[1] * n3_inv;
-      const float dxz = -P[0] * P[2] * n3_inv;
-      const float dyz = -P[1] * P[2] * n3_inv;
-      const float J0[7] = {dxx, dxy, dxz, 0.f, rj[2], -rj[1], 0.f};
-      const float J1[7] = {dxy, dyy, dyz, -rj[2], 0.f, rj[0], 0.f};
-      const float J2[7] = {dxz, dyz, dzz, rj[1], -rj[0], 0.f, 0.f};
-      const float J3[7] = {rj[0], rj[1], rj[2], 0.f, 0.f, 0.f, n1j};
-      acc_row(acc, w[0], err[0], J0);
-      acc_row(acc, w[1], err[1], J1);
-      acc_row(acc, w[2], err[2], J2);
-      acc_row(acc, w[3], err[3], J3);
-    } else if (MODE == MODE_CALIB) {
-      const int u_t = (int)(ind % prm.width);
-      const int v_t = (int)(ind / prm.width);
-      const bool valid_z = (P[2] > prm.z_eps) && (Xi[2] > prm.z_eps);
-      const float zj_inv = valid_z ? inv_ref(P[2]) : 0.f;
-      const float zj_log = valid_z ? logf(P[2]) : 0.f;
-      const float zi_log = valid_z ? logf(Xi[2]) : 0.f;
-      const float xz = P[0] * zj_inv;
-      const float yz = P[1] * zj_inv;
-      const float u = fx * xz + cx;
-      const float v = fy * yz + cy;
-      const bool valid_u = (u > (float)prm.pixel_border) &&
-                           (u < (float)(prm.width - 1 - prm.pixel_border));
-      const bool valid_v = (v > (float)prm.pixel_border) &&
-                           (v < (float)(prm.height - 1 - prm.pixel_border));
-      valid = valid & valid_u & valid_v & valid_z;
-      const float err[3] = {u - (float)u_t, v - (float)v_t, zj_log - zi_log};
-      const float sq = sqrtf(q);
-      const float swp = valid ? prm.s0_inv * sq : 0.f;
-      const float swd = valid ? prm.s1_inv * sq : 0.f;
-      const float cp = swp * swp, cd = swd * swd;
-      const float w[3] = {huber_ref(swp * err[0]) * cp, huber_ref(swp * err[1]) * cp,
-                          huber_ref(swd * err[2]) * cd};
-      const float J0[7] = {fx * zj_inv, 0.f, -fx * xz * zj_inv, -fx * xz * yz,
-                           fx * (1.f + xz * xz), -fx * yz, 0.f};
-      const float J1[7] = {0.f, fy * zj_inv, -fy * yz * zj_inv, -fy * (1.f + yz * yz),
-                           fy * xz * yz, fy * xz, 0.f};
-      const float J2[7] = {0.f, 0.f, zj_inv, yz, -xz, 0.f, 1.f};
-      acc_row(acc, w[0], err[0], J0);
-      acc_row(acc, w[1], err[1], J1);
-      acc_row(acc, w[2], err[2], J2);
-    } else {  // MODE_POINTS
-      const float err[3] = {P[0] - Xi[0], P[1] - Xi[1], P[2] - Xi[2]};
-      const float swp = valid ? prm.s0_inv * sqrtf(q) : 0.f;
-      const float cp = swp * swp;
-      const float w[3] = {huber_ref(swp * err[0]) * cp, huber_ref(swp * err[1]) * cp,
-                          huber_ref(swp * err[2]) * cp};
-      const float J0[7] = {1.f, 0.f, 0.f, 0.f, P[2], -P[1], P[0]};
-      const float J1[7] = {0.f, 1.f, 0.f, -P[2], 0.f, P[0], P[1]};
-      const float J2[7] = {0.f, 0.f, 1.f, P[1], -P[0], 0.f, P[2]};
-      acc_row(acc, w[0], err[0], J0);
-      acc_row(acc, w[1], err[1], J1);
-      acc_row(acc, w[2], err[2], J2);
+  // U points per thread per trip: their independent loads (valid, idx, Q, Xj, Cj) issue back
+  // to back, then their gathers at the match index (Xi, Ci), then the arithmetic — two
+  // memory round trips per U points instead of per point.  Lanes past k1 load point k1 - 1
+  // and skip the accumulation.
+  constexpr int U = 4;
+  for (int64_t kb = k0 + threadIdx.x; kb < k1; kb += U * kEdgeThreads) {
+    int64_t kk[U];
+    uint8_t vmb[U];
+    int64_t raw[U];
+    float xj[U][3], qv[U], cjv[U], xi[U][3], civ[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      kk[u] = min(kb + (int64_t)u * kEdgeThreads, k1 - 1);
+      vmb[u] = valid_match[eoff + kk[u]];
+      raw[u] = idx_ii2jj[eoff + kk[u]];
+      xj[u][0] = Xj_base[3 * kk[u]];
+      xj[u][1] = Xj_base[3 * kk[u] + 1];
+      xj[u][2] = Xj_base[3 * kk[u] + 2];
+      qv[u] = Q[eoff + kk[u]];
+      cjv[u] = Cj_base[kk[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t ind = vmb[u] ? raw[u] : 0;
+      raw[u] = ind;
+      xi[u][0] = Xi_base[3 * ind];
+      xi[u][1] = Xi_base[3 * ind + 1];
+      xi[u][2] = Xi_base[3 * ind + 2];
+      civ[u] = Ci_base[ind];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (kb + (int64_t)u * kEdgeThreads < k1)
+        point_acc<MODE>(acc, vmb[u] != 0, raw[u], xi[u], civ[u], xj[u], qv[u], cjv[u], tij, qij,
+                        sij, prm, fx, fy, cx, cy);
     }
   }
 
@@ -412,21 +459,23 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_kernel(
   }
 
   // 3) right-looking Cholesky, lower triangle in place (Eigen SimplicialLLT equivalent)
+  // (column scaled by the reciprocal pivot; gn_solve_lds_kernel does the same operations)
   __shared__ int s_fail;
-  __shared__ double s_piv;
+  __shared__ double s_rpiv;
   if (tid == 0) s_fail = 0;
   __syncthreads();
   for (int k = 0; k < n; k++) {
     if (tid == 0) {
       const double d = Ag[(int64_t)k * n + k];
       if (!(d > 0.0)) s_fail = 1;
-      s_piv = sqrt(d);
-      Ag[(int64_t)k * n + k] = s_piv;
+      const double piv = sqrt(d);
+      Ag[(int64_t)k * n + k] = piv;
+      s_rpiv = 1.0 / piv;
     }
     __syncthreads();
     if (s_fail) break;
-    const double piv = s_piv;
-    for (int i = k + 1 + tid; i < n; i += nt) Ag[(int64_t)i * n + k] /= piv;
+    const double rpiv = s_rpiv;
+    for (int i = k + 1 + tid; i < n; i += nt) Ag[(int64_t)i * n + k] *= rpiv;
     __syncthreads();
     const int m = n - k - 1;  // trailing size
     const int64_t tot = (int64_t)m * (m + 1) / 2;
@@ -445,14 +494,14 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_kernel(
   // 4) solve L y = b, L^T x = y (column sweeps); x overwrites b.
   if (!s_fail) {
     for (int j = 0; j < n; j++) {
-      if (tid == 0) bg[j] /= Ag[(int64_t)j * n + j];
+      if (tid == 0) bg[j] *= 1.0 / Ag[(int64_t)j * n + j];
       __syncthreads();
       const double yj = bg[j];
       for (int i = j + 1 + tid; i < n; i += nt) bg[i] -= Ag[(int64_t)i * n + j] * yj;
       __syncthreads();
     }
     for (int j = n - 1; j >= 0; j--) {
-      if (tid == 0) bg[j] /= Ag[(int64_t)j * n + j];
+      if (tid == 0) bg[j] *= 1.0 / Ag[(int64_t)j * n + j];
       __syncthreads();
       const double xj = bg[j];
       for (int i = tid; i < j; i += nt) bg[i] -= Ag[(int64_t)j * n + i] * xj;
@@ -584,6 +633,17 @@ struct LdsLists {
   const int *blk_start, *blk_list, *vec_start, *vec_list;
 };
 
+#ifdef M3S_GN_STAMPS
+// debug build (tools/gn_stamps.py): thread 0 of the LDS solve, s_memrealtime (100 MHz) at
+// each phase boundary of the first 16 iterations
+__device__ long long g_gn_stamps[16 * 8];
+#define M3S_GS(ph) \
+  if (tid == 0 && flags[3] < 16) \
+    g_gn_stamps[flags[3] * 8 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime();
+#else
+#define M3S_GS(ph)
+#endif
+
 __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
     float* __restrict__ Twc, const float* __restrict__ partial, const int* __restrict__ rank_ii,
     double* __restrict__ EB, LdsLists lists, float* __restrict__ dx_out,
@@ -593,11 +653,12 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = 7 * (P - 1);
   const int nt = blockDim.x;
+  M3S_GS(0)
   constexpr int NW = kSolveThreads / 64;
   __shared__ double sA[kLdsN * kLdsN];
   __shared__ double sb[kLdsN];
   __shared__ double sW[NW][4][49];      // per wave: M, G, T (A reuses G), v' / v
-  __shared__ int s_fail;
+  __shared__ double sR[kLdsN];          // 1 / L[k][k]
   __shared__ float s_red[NW];
 
   // 1) per edge (wave w: edges w, w + NW, ...): G → M, T = M G, A = T Mᵀ, v = M v'
@@ -661,9 +722,9 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
     }
     wave_lds_sync();                             // scratch reused by the next edge
   }
-  if (tid == 0) s_fail = 0;
   __threadfence_block();
   __syncthreads();
+  M3S_GS(1)
 
   // 2) assembly by ownership, contributions in the serial loop's order
   const int np = P - 1;
@@ -693,63 +754,70 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
     sb[row] = bv;
   }
   __syncthreads();
+  M3S_GS(2)
 
-  // 3) right-looking Cholesky in LDS (gn_solve_kernel step 3's operations and order)
-  for (int k = 0; k < n; k++) {
-    if (tid == 0) {
+  // 3) right-looking Cholesky in LDS, one barrier per column: every thread derives the
+  //    pivot itself, thread (row i, column group cg) forms L[i][k] = A[i][k] / piv and L[j][k]
+  //    on the fly for its columns j = k+1+cg, +8, ... <= i (the same products as gn_solve_kernel's
+  //    scaled column), and L[., k] goes to the unused upper triangle (L[i][k] = sA[k n + i]) so
+  //    that no one overwrites column k while it is being read.
+  bool fail = false;
+  {
+    const int ri = tid >> 3, cg = tid & 7;  // 128 rows x 8 column groups (n - k - 1 <= 125)
+    for (int k = 0; k < n; k++) {
       const double d = sA[k * n + k];
-      if (!(d > 0.0)) s_fail = 1;
-      sA[k * n + k] = sqrt(d);
+      if (!(d > 0.0)) {
+        fail = true;
+        break;
+      }
+      const double rpiv = 1.0 / sqrt(d);
+      const int i = k + 1 + ri;
+      if (i < n) {
+        const double li = sA[i * n + k] * rpiv;
+        for (int j = k + 1 + cg; j <= i; j += 8) sA[i * n + j] -= li * (sA[j * n + k] * rpiv);
+        if (cg == 0) sA[k * n + i] = li;
+      }
+      if (tid == 0) sR[k] = rpiv;
+      __syncthreads();
     }
-    __syncthreads();
-    if (s_fail) break;
-    const double piv = sA[k * n + k];
-    for (int i = k + 1 + tid; i < n; i += nt) sA[i * n + k] /= piv;
-    __syncthreads();
-    const int m = n - k - 1;
-    for (int idx = tid; idx < m * m; idx += nt) {
-      const int i = idx / m, j = idx - i * m;
-      if (j > i) continue;
-      const int gi = k + 1 + i, gj = k + 1 + j;
-      sA[gi * n + gj] -= sA[gi * n + k] * sA[gj * n + k];
-    }
-    __syncthreads();
   }
 
+  M3S_GS(3)
   // 4) L y = b, Lᵀ x = y by wave 0, rows i = lane + 64 t in registers (t < 2: n <= 128)
-  if (wv == 0 && !s_fail) {
+  if (wv == 0 && !fail) {
     double x0 = lane < n ? sb[lane] : 0.0, x1 = lane + 64 < n ? sb[lane + 64] : 0.0;
     for (int j = 0; j < n; j++) {
       const int owner = j & 63;
       double yj = j < 64 ? x0 : x1;
-      if (lane == owner) yj = yj / sA[j * n + j];
+      if (lane == owner) yj = yj * sR[j];
       yj = __shfl(yj, owner, 64);
       if (lane == owner) {
         if (j < 64) x0 = yj;
         else x1 = yj;
       }
-      if (lane > j && lane < n) x0 -= sA[lane * n + j] * yj;
-      if (lane + 64 > j && lane + 64 < n) x1 -= sA[(lane + 64) * n + j] * yj;
+      if (lane > j && lane < n) x0 -= sA[j * n + lane] * yj;
+      if (lane + 64 > j && lane + 64 < n) x1 -= sA[j * n + lane + 64] * yj;
     }
     for (int j = n - 1; j >= 0; j--) {
       const int owner = j & 63;
       double xj = j < 64 ? x0 : x1;
-      if (lane == owner) xj = xj / sA[j * n + j];
+      if (lane == owner) xj = xj * sR[j];
       xj = __shfl(xj, owner, 64);
       if (lane == owner) {
         if (j < 64) x0 = xj;
         else x1 = xj;
       }
-      if (lane < j) x0 -= sA[j * n + lane] * xj;
-      if (lane + 64 < j) x1 -= sA[j * n + lane + 64] * xj;
+      if (lane < j) x0 -= sA[lane * n + j] * xj;
+      if (lane + 64 < j) x1 -= sA[(lane + 64) * n + j] * xj;
     }
     if (lane < n) sb[lane] = x0;
     if (lane + 64 < n) sb[lane + 64] = x1;
   }
   __syncthreads();
+  M3S_GS(4)
 
   // 5) dx = -x (zero on failure, gn_kernels.cu:147-150), retract poses 1..P-1
-  for (int idx = tid; idx < n; idx += nt) dx_out[idx] = s_fail ? 0.f : (float)(-sb[idx]);
+  for (int idx = tid; idx < n; idx += nt) dx_out[idx] = fail ? 0.f : (float)(-sb[idx]);
   __syncthreads();
   for (int p = 1 + tid; p < P; p += nt) {
     float* Tp = Twc + 8 * p;
@@ -774,16 +842,19 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
   if (tid == 0) {
     float tot = 0.f;
     for (int w = 0; w < nt / 64; w++) tot += s_red[w];
+    M3S_GS(5)
     flags[3] += 1;
-    if (s_fail) flags[1] = 1;
+    if (fail) flags[1] = 1;
     if (sqrtf(tot) < delta_thresh) flags[0] = 1;
   }
 }
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// E x S ~ 768 workgroups of 4 waves = 3 waves on each of the 1024 SIMDs, the rays kernel's
+// occupancy at 146 VGPRs: the edge pass runs in one round, with no tail
 int choose_splits(int64_t E, int64_t N) {
-  int64_t S = (2048 + E - 1) / E;
+  int64_t S = (768 + E - 1) / E;
   const int64_t max_by_points = (N + 1023) / 1024;  // >= ~1024 points per workgroup
   if (S > max_by_points) S = max_by_points;
   if (S < 1) S = 1;
@@ -981,6 +1052,13 @@ int shard_edge_pass(const float* d_Twc, const float* d_Xs, const float* d_Cs, co
 }
 
 }  // namespace
+
+#ifdef M3S_GN_STAMPS
+extern "C" int m3s_debug_gn_stamps(long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gn_stamps), sizeof(long long) * 16 * 8) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif
 
 extern "C" int m3s_gn_force_global_solve(int on) {
   g_force_global_solve = on != 0;

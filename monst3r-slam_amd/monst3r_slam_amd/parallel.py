@@ -371,8 +371,8 @@ class ShardedFactorGraph(FactorGraph):
             slot.append(torch.cat([loc, loc + E, torch.full((pad - 2 * loc.numel(),), -1,
                                                            dtype=loc.dtype, device=dev)]))
         slot = torch.cat(slot)
-        take = slot >= 0
-        dst = slot[take]
+        take = torch.nonzero(slot >= 0).flatten()    # index lists, built once: no per-
+        dst = slot.index_select(0, take)              # iteration mask (a host sync)
         _lib.check(lib.m3s_gn_sharded_begin(ptr(ii), ptr(jj), P, N, E2, El, ptr(dx), ptr(ws), s),
                    "gn_sharded_begin")
         for _ in range(int(c["max_iters"])):
@@ -391,7 +391,7 @@ class ShardedFactorGraph(FactorGraph):
             _lib.check(st, "gn_edge_pass")
             gathered = (_all_gather_fixed(G_loc, self.group) if world > 1 else G_loc).reshape(
                 world * pad, 35)
-            G_all[dst] = gathered[take]
+            G_all.index_copy_(0, dst, gathered.index_select(0, take))
             _lib.check(lib.m3s_gn_solve_step(ptr(pose), ptr(G_all), P, N, E2, El,
                                              float(c["delta_norm"]), ptr(dx), ptr(ws), s),
                        "gn_solve_step")

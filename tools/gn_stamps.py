@@ -1,0 +1,75 @@
+"""Diagnostic: the backend GN at the keyframe-graph size (P = 16 keyframes, 64 pairs as 128
+two-way edges, 384 x 512 points) — wall time per iteration of mast3r_slam_backends.
+gauss_newton_rays, and, with the debug library (make -C monst3r-slam_amd/csrc gn_stamps),
+the LDS solve's phase timeline per iteration: per-edge blocks, assembly, Cholesky,
+triangular solves, retraction / convergence (µs, thread 0, s_memrealtime).
+Usage: python tools/gn_stamps.py"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "monst3r-slam_amd")]
+import mast3r_slam_backends as mb  # noqa: E402
+from monst3r_slam_amd import _lib  # noqa: E402
+from monst3r_slam_amd import synthetic as syn  # noqa: E402
+
+dev = torch.device("cuda:0")
+torch.cuda.set_device(dev)
+ITERS = 10
+g = syn.keyframe_graph(P=16, h=384, w=512, seed=5, pairs=64, two_way=True)
+host = {k: torch.from_numpy(np.ascontiguousarray(g[k])) for k in
+        ("Twc", "Xs", "Cs", "ii", "jj", "idx", "valid", "Q")}
+dv = {k: v.to(dev) for k, v in host.items()}
+
+
+def run():
+    Twc = dv["Twc"].clone()
+    return mb.gauss_newton_rays(Twc, dv["Xs"], dv["Cs"], dv["ii"], dv["jj"], dv["idx"],
+                                dv["valid"], dv["Q"], 0.003, 10.0, 0.0, 1.5, ITERS, 0.0)
+
+
+for _ in range(3):
+    run()
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(5):
+    run()
+e1.record()
+e1.synchronize()
+print(f"product library: {e0.elapsed_time(e1) / 5:.3f} ms per solve of {ITERS} iterations "
+      f"({e0.elapsed_time(e1) / 5 / ITERS * 1e3:.0f} us per iteration)", flush=True)
+
+dbg_path = os.environ.get("M3S_GN_STAMPS_LIB") or os.path.join(
+    ROOT, "monst3r-slam_amd/csrc/build/libm3s_gn_stamps.so")   # build/ does not travel
+lib = ctypes.CDLL(dbg_path)
+real = _lib.load()
+fn = lib.m3s_gauss_newton_rays
+fn.restype = ctypes.c_int
+fn.argtypes = real.m3s_gauss_newton_rays.argtypes
+lib.m3s_debug_gn_stamps.argtypes = [ctypes.c_void_p]
+
+
+class Shim:  # route the backend's call into the debug library
+    def __getattr__(self, k):
+        return fn if k == "m3s_gauss_newton_rays" else getattr(real, k)
+
+
+_lib.load = lambda: Shim()
+for _ in range(2):
+    run()
+torch.cuda.synchronize()
+buf = (ctypes.c_longlong * 128)()
+assert lib.m3s_debug_gn_stamps(buf) == 0
+st = np.array(buf[:], dtype=np.float64).reshape(16, 8) / 100.0  # µs
+names = ["edge-blocks", "assembly", "cholesky", "solves", "retract"]
+for it in range(ITERS):
+    d = np.diff(st[it, :6])
+    print(f"iteration {it}: " + " ".join(f"{n} {v:7.2f}" for n, v in zip(names, d))
+          + f" | solve kernel {st[it, 5] - st[it, 0]:7.2f} us"
+          + (f" | to next solve {st[it + 1, 0] - st[it, 5]:7.2f}" if it < ITERS - 1 else ""),
+          flush=True)
