@@ -540,9 +540,12 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
             "valid_match_frac": valid_frac,
             "gflop_per_pair": 3603.6, "tflops_achieved": len(ii) * 3603.6e9 * steps / el / 1e12,
             "gn": {"ms": gn_ms, "iterations": gn_it, "ms_per_iteration": gn_ms / gn_it,
+                   "loop_ms_per_iteration": graph.gn_loop_ms / gn_it,
                    "edges_two_way": 2 * int(graph.ii.numel()),
                    "timing": "graph._solve_sharded('rays') from the graph's initial poses, "
-                             "host wall incl. the final status sync"},
+                             "host wall incl. its setup (two-way edge concatenation, "
+                             "workspace, rank lists) and the final status sync; "
+                             "loop_ms_per_iteration: device events around the iterations"},
             "records_kept_per_rank_bytes": int(-(-len(ii) // world) * P.record_bytes(n)),
             "allgather_bytes_per_rank": int(16 * len(ii)),
             "sharding": f"edges round-robin over {world} rank(s): records stay on the matching "

@@ -46,18 +46,22 @@ struct GnWork {
 };
 
 // Huber weight (gn_kernels.cu:172-175).  The reference compares and divides in double
-// (its 1.345 is a double literal); here both are fp32: the comparison is exact (1.345f is
-// the next float above 1.345, so r < 1.345 <=> r < 1.345f for every float r) and the weight
-// 1.345f / r is within 1 ulp of (float)(1.345 / (double)r) — six fp64 divisions per point
-// were a third of the edge pass.
+// (its 1.345 is a double literal); here the comparison is fp32 and exact (1.345f is the next
+// float above 1.345, so r < 1.345 <=> r < 1.345f for every float r) and the weight is
+// 1.345f * rcp(r) (v_rcp_f32, 1 ulp): six fp64 divisions per point were a third of the
+// edge pass, and the correctly rounded fp32 division sequences another sixth.
 __device__ __forceinline__ float huber_w(float r) {
   const float r_abs = fabsf(r);
-  return r_abs < 1.345f ? 1.0f : 1.345f / r_abs;
+  return r_abs < 1.345f ? 1.0f : 1.345f * __builtin_amdgcn_rcpf(r_abs);
 }
 
-// 1 / x (the reference: 1.0 / x in double, rounded to float); the correctly rounded fp32
-// quotient differs from it only where the double quotient rounds twice (<= 1 ulp)
+// 1 / x and sqrt(x) of the residual normalisation.  These enter the residuals themselves
+// (differences of unit rays ~1e-3): the 1-ulp v_rcp_f32 / v_sqrt_f32 bias them coherently
+// over an edge's points (P = 19 chain: poses off by 8e-5), so they stay correctly rounded —
+// the reference's 1.0 / x in double rounded to float differs from the fp32 quotient only
+// where the double quotient rounds twice (<= 1 ulp, unbiased).
 __device__ __forceinline__ float inv_f(float x) { return 1.0f / x; }
+__device__ __forceinline__ float sqrt_f(float x) { return sqrtf(x); }
 
 // Accumulate one weighted row into the 35 sums.  MASK (bit n: J[n] may be nonzero) is the
 // row's compile-time sparsity: the zero entries' products are never formed (an exact zero
@@ -93,15 +97,15 @@ __device__ __forceinline__ void point_acc(float* acc, bool vm, int64_t ind, cons
 
   if (MODE == MODE_RAYS) {
     const float n2i = Xi[0] * Xi[0] + Xi[1] * Xi[1] + Xi[2] * Xi[2];
-    const float n1i = sqrtf(n2i);
+    const float n1i = sqrt_f(n2i);
     const float n1i_inv = inv_f(n1i);
     const float n2j = P[0] * P[0] + P[1] * P[1] + P[2] * P[2];
-    const float n1j = sqrtf(n2j);
+    const float n1j = sqrt_f(n2j);
     const float n1j_inv = inv_f(n1j);
     const float rj[3] = {n1j_inv * P[0], n1j_inv * P[1], n1j_inv * P[2]};
     const float err[4] = {rj[0] - n1i_inv * Xi[0], rj[1] - n1i_inv * Xi[1],
                           rj[2] - n1i_inv * Xi[2], n1j - n1i};
-    const float sq = sqrtf(q);
+    const float sq = sqrt_f(q);
     const float swr = valid ? prm.s0_inv * sq : 0.f;
     const float swd = valid ? prm.s1_inv * sq : 0.f;
     const float cr = swr * swr, cd = swd * swd;
@@ -139,7 +143,7 @@ __device__ __forceinline__ void point_acc(float* acc, bool vm, int64_t ind, cons
                          (v < (float)(prm.height - 1 - prm.pixel_border));
     valid = valid & valid_u & valid_v & valid_z;
     const float err[3] = {u - (float)u_t, v - (float)v_t, zj_log - zi_log};
-    const float sq = sqrtf(q);
+    const float sq = sqrt_f(q);
     const float swp = valid ? prm.s0_inv * sq : 0.f;
     const float swd = valid ? prm.s1_inv * sq : 0.f;
     const float cp = swp * swp, cd = swd * swd;
@@ -155,7 +159,7 @@ __device__ __forceinline__ void point_acc(float* acc, bool vm, int64_t ind, cons
     acc_row<0x5C>(acc, w[2], err[2], J2);
   } else {  // MODE_POINTS
     const float err[3] = {P[0] - Xi[0], P[1] - Xi[1], P[2] - Xi[2]};
-    const float swp = valid ? prm.s0_inv * sqrtf(q) : 0.f;
+    const float swp = valid ? prm.s0_inv * sqrt_f(q) : 0.f;
     const float cp = swp * swp;
     const float w[3] = {huber_w(swp * err[0]) * cp, huber_w(swp * err[1]) * cp,
                         huber_w(swp * err[2]) * cp};
@@ -209,7 +213,7 @@ __global__ __launch_bounds__(kEdgeThreads) void gn_edge_kernel(
   // U points per thread per trip: their independent loads (valid, idx, Q, Xj, Cj) issue back
   // to back, then their gathers at the match index (Xi, Ci), then the arithmetic — two
   // memory round trips per U points instead of per point.  Lanes past k1 load point k1 - 1
-  // and skip the accumulation.
+  // and accumulate it as invalid (weight 0).
   constexpr int U = 4;
   for (int64_t kb = k0 + threadIdx.x; kb < k1; kb += U * kEdgeThreads) {
     int64_t kk[U];
@@ -237,10 +241,10 @@ __global__ __launch_bounds__(kEdgeThreads) void gn_edge_kernel(
       civ[u] = Ci_base[ind];
     }
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      if (kb + (int64_t)u * kEdgeThreads < k1)
-        point_acc<MODE>(acc, vmb[u] != 0, raw[u], xi[u], civ[u], xj[u], qv[u], cjv[u], tij, qij,
-                        sij, prm, fx, fy, cx, cy);
+    for (int u = 0; u < U; u++) {  // unconditional (a branch would sink the loads into it)
+      const bool in = kb + (int64_t)u * kEdgeThreads < k1;
+      point_acc<MODE>(acc, in && vmb[u] != 0, raw[u], xi[u], civ[u], xj[u], qv[u], cjv[u], tij,
+                      qij, sij, prm, fx, fy, cx, cy);
     }
   }
 
@@ -726,89 +730,139 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
   __syncthreads();
   M3S_GS(1)
 
-  // 2) assembly by ownership, contributions in the serial loop's order
+  // 2) assembly by ownership, contributions in the serial loop's order; each owner fetches
+  //    its contribution list 8 entries at a time (codes, then the 8 EB values, then the
+  //    additions in order): two memory round trips per 8 contributions, not per one — a
+  //    diagonal block collects one contribution per edge at its pose (~16 at P = 16)
+  constexpr int CH = 8;
   const int np = P - 1;
   for (int idx = tid; idx < n * n; idx += nt) {
     const int row = idx / n, col = idx - row * n;
     const int bi = row / 7, r = row - 7 * bi, bj = col / 7, c = col - 7 * bj;
     const int b = bi * np + bj;
+    const int k0 = lists.blk_start[b], k1 = lists.blk_start[b + 1];
     double a = 0.0;
-    for (int k = lists.blk_start[b]; k < lists.blk_start[b + 1]; k++) {
-      const int code = lists.blk_list[k];
-      const double v = EB[(int64_t)(code >> 2) * kEB + r * 7 + c];
-      const int kind = code & 3;
-      if (kind == 0 || kind == 3) a += v;
-      else a -= v;
+    for (int kb = k0; kb < k1; kb += CH) {
+      int code[CH];
+      double v[CH];
+#pragma unroll
+      for (int u = 0; u < CH; u++) code[u] = kb + u < k1 ? lists.blk_list[kb + u] : 0;
+#pragma unroll
+      for (int u = 0; u < CH; u++)
+        v[u] = kb + u < k1 ? EB[(int64_t)(code[u] >> 2) * kEB + r * 7 + c] : 0.0;
+#pragma unroll
+      for (int u = 0; u < CH; u++) {
+        if (kb + u >= k1) break;
+        const int kind = code[u] & 3;
+        if (kind == 0 || kind == 3) a += v[u];
+        else a -= v[u];
+      }
     }
     sA[idx] = a;
   }
   for (int row = tid; row < n; row += nt) {
     const int p = row / 7, r = row - 7 * p;
+    const int k0 = lists.vec_start[p], k1 = lists.vec_start[p + 1];
     double bv = 0.0;
-    for (int k = lists.vec_start[p]; k < lists.vec_start[p + 1]; k++) {
-      const int code = lists.vec_list[k];
-      const double v = EB[(int64_t)(code >> 1) * kEB + 49 + r];
-      if (code & 1) bv += v;
-      else bv -= v;
+    for (int kb = k0; kb < k1; kb += CH) {
+      int code[CH];
+      double v[CH];
+#pragma unroll
+      for (int u = 0; u < CH; u++) code[u] = kb + u < k1 ? lists.vec_list[kb + u] : 0;
+#pragma unroll
+      for (int u = 0; u < CH; u++)
+        v[u] = kb + u < k1 ? EB[(int64_t)(code[u] >> 1) * kEB + 49 + r] : 0.0;
+#pragma unroll
+      for (int u = 0; u < CH; u++) {
+        if (kb + u >= k1) break;
+        if (code[u] & 1) bv += v[u];
+        else bv -= v[u];
+      }
     }
     sb[row] = bv;
   }
   __syncthreads();
   M3S_GS(2)
 
-  // 3) right-looking Cholesky in LDS, one barrier per column: every thread derives the
-  //    pivot itself, thread (row i, column group cg) forms L[i][k] = A[i][k] / piv and L[j][k]
-  //    on the fly for its columns j = k+1+cg, +8, ... <= i (the same products as gn_solve_kernel's
-  //    scaled column), and L[., k] goes to the unused upper triangle (L[i][k] = sA[k n + i]) so
-  //    that no one overwrites column k while it is being read.
-  bool fail = false;
+  // 3) right-looking Cholesky in LDS, one barrier per column.  Each thread forms L[i][k] =
+  //    A[i][k] / piv and L[j][k] on the fly for its entries (i, j) of the trailing triangle
+  //    (the same products as gn_solve_kernel's scaled column); L[., k] goes to the unused
+  //    upper triangle (L[i][k] = sA[k n + i]) so that no one overwrites column k while it is
+  //    being read.  The next pivot's 1 / sqrt(d) is formed by the thread that finishes
+  //    A[k+1][k+1] (its row has one column: done long before the longest rows) and read from
+  //    sR after the barrier.
+  __shared__ int s_fail[2];  // pivot k's test in s_fail[k & 1]: written in step k - 1,
+  bool fail = false;         // read after its barrier, never while it is being read
+  if (tid == 0) {
+    const double d = sA[0];
+    s_fail[0] = !(d > 0.0);
+    s_fail[1] = 0;
+    sR[0] = 1.0 / sqrt(d);
+  }
+  __syncthreads();
   {
+    // thread (row i = k + 1 + ri, column group cg): columns j = k + 1 + cg, + 8, ... <= i.
+    // (Measured against two alternatives at P = 16: all of a thread's reads issued before
+    // its writes, 16-deep unrolled, 110 us; row pairs (ra, m - 1 - ra) balanced over 16
+    // column groups, 105 us; this plain loop is LDS-issue-bound at fewer instructions.)
     const int ri = tid >> 3, cg = tid & 7;  // 128 rows x 8 column groups (n - k - 1 <= 125)
     for (int k = 0; k < n; k++) {
-      const double d = sA[k * n + k];
-      if (!(d > 0.0)) {
+      if (s_fail[k & 1]) {  // uniform: every thread leaves at the same k
         fail = true;
         break;
       }
-      const double rpiv = 1.0 / sqrt(d);
+      const double rpiv = sR[k];
       const int i = k + 1 + ri;
       if (i < n) {
         const double li = sA[i * n + k] * rpiv;
         for (int j = k + 1 + cg; j <= i; j += 8) sA[i * n + j] -= li * (sA[j * n + k] * rpiv);
-        if (cg == 0) sA[k * n + i] = li;
+        if (cg == 0) {
+          sA[k * n + i] = li;
+          if (ri == 0) {  // row k + 1's only column: A[k+1][k+1] is final, the next pivot
+            const double d = sA[i * n + i];
+            s_fail[i & 1] = !(d > 0.0);
+            sR[i] = 1.0 / sqrt(d);
+          }
+        }
       }
-      if (tid == 0) sR[k] = rpiv;
       __syncthreads();
     }
   }
 
   M3S_GS(3)
-  // 4) L y = b, Lᵀ x = y by wave 0, rows i = lane + 64 t in registers (t < 2: n <= 128)
+  // 4) L y = b, Lᵀ x = y by wave 0, rows i = lane + 64 t in registers (t < 2: n <= 128);
+  //    the solved unknown goes to every lane by v_readlane (the owner lane is uniform)
   if (wv == 0 && !fail) {
+    auto bcast = [](double v, int l) {
+      const uint64_t u = __builtin_bit_cast(uint64_t, v);
+      const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, l);
+      const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+      return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+    };
     double x0 = lane < n ? sb[lane] : 0.0, x1 = lane + 64 < n ? sb[lane + 64] : 0.0;
     for (int j = 0; j < n; j++) {
       const int owner = j & 63;
-      double yj = j < 64 ? x0 : x1;
-      if (lane == owner) yj = yj * sR[j];
-      yj = __shfl(yj, owner, 64);
+      const double c0 = lane > j && lane < n ? sA[j * n + lane] : 0.0;
+      const double c1 = lane + 64 > j && lane + 64 < n ? sA[j * n + lane + 64] : 0.0;
+      const double yj = bcast((j < 64 ? x0 : x1) * sR[j], owner);
       if (lane == owner) {
         if (j < 64) x0 = yj;
         else x1 = yj;
       }
-      if (lane > j && lane < n) x0 -= sA[j * n + lane] * yj;
-      if (lane + 64 > j && lane + 64 < n) x1 -= sA[j * n + lane + 64] * yj;
+      if (lane > j && lane < n) x0 -= c0 * yj;
+      if (lane + 64 > j && lane + 64 < n) x1 -= c1 * yj;
     }
     for (int j = n - 1; j >= 0; j--) {
       const int owner = j & 63;
-      double xj = j < 64 ? x0 : x1;
-      if (lane == owner) xj = xj * sR[j];
-      xj = __shfl(xj, owner, 64);
+      const double c0 = lane < j ? sA[lane * n + j] : 0.0;
+      const double c1 = lane + 64 < j ? sA[(lane + 64) * n + j] : 0.0;
+      const double xj = bcast((j < 64 ? x0 : x1) * sR[j], owner);
       if (lane == owner) {
         if (j < 64) x0 = xj;
         else x1 = xj;
       }
-      if (lane < j) x0 -= sA[lane * n + j] * xj;
-      if (lane + 64 < j) x1 -= sA[(lane + 64) * n + j] * xj;
+      if (lane < j) x0 -= c0 * xj;
+      if (lane + 64 < j) x1 -= c1 * xj;
     }
     if (lane < n) sb[lane] = x0;
     if (lane + 64 < n) sb[lane + 64] = x1;

@@ -375,6 +375,8 @@ class ShardedFactorGraph(FactorGraph):
         dst = slot.index_select(0, take)              # iteration mask (a host sync)
         _lib.check(lib.m3s_gn_sharded_begin(ptr(ii), ptr(jj), P, N, E2, El, ptr(dx), ptr(ws), s),
                    "gn_sharded_begin")
+        loop_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        loop_ev[0].record()                       # the iterations alone (gn_loop_ms)
         for _ in range(int(c["max_iters"])):
             if mode == "rays":
                 st = lib.m3s_gn_rays_edge_pass(
@@ -395,6 +397,7 @@ class ShardedFactorGraph(FactorGraph):
             _lib.check(lib.m3s_gn_solve_step(ptr(pose), ptr(G_all), P, N, E2, El,
                                              float(c["delta_norm"]), ptr(dx), ptr(ws), s),
                        "gn_solve_step")
+        loop_ev[1].record()
         hs, it = ctypes.c_int(0), ctypes.c_int(0)
         _lib.check(lib.m3s_gn_sharded_status(ptr(ws), P, ctypes.byref(hs), ctypes.byref(it), s),
                    "gn_sharded_status")
@@ -402,5 +405,6 @@ class ShardedFactorGraph(FactorGraph):
             raise RuntimeError("gauss_newton (sharded): the number of unique keyframes in ii/jj "
                                "must equal Xs.size(0)")
         self.gn_iterations = it.value
+        self.gn_loop_ms = loop_ev[0].elapsed_time(loop_ev[1])   # status call synchronised
         T_WCs[:, 0, :] = pose
         self.frames.update_T_WCs(T_WCs[pin:], uniq[pin:])

@@ -45,19 +45,26 @@ def test_gn_rays_solve_paths(oracle, dev, P):
     the oracle's dense Cholesky."""
     import mast3r_slam_backends as mb
     g = syn.keyframe_graph(P=P, h=24, w=32, seed=P)
-    Twc_ref = g["Twc"].copy()
-    ref = oracle.gauss_newton("rays", Twc_ref, g["Xs"], g["Cs"], g["ii"], g["jj"], g["idx"],
-                              g["valid"], g["Q"], sig0=0.003, sig1=10.0, C_thresh=0.0,
-                              Q_thresh=1.5, max_iter=3, delta_thresh=1e-8)
-    Twc, Xs, Cs, ii, jj, idx, valid, Q = _gn_case(g, dev)
-    (dx,) = mb.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.003, 10.0, 0.0, 1.5, 3,
-                                 1e-8)
-    # a 19-24 pose chain accumulates the f32 edge-sum noise along the gauge chain (the
-    # global-memory path, unchanged since round 1, measured 2.75e-5 at P = 24 on poses of
-    # magnitude ~1.2): relative 5e-5 on top of the absolute bar; its last step is small
-    # (|dx| ~ 1e-4): relative 5 %
-    np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=POSE_TOL, rtol=5e-5)
-    np.testing.assert_allclose(dx.cpu().numpy(), ref["dx"], atol=POSE_TOL, rtol=5e-2)
+    for iters in (1, 3):
+        Twc_ref = g["Twc"].copy()
+        ref = oracle.gauss_newton("rays", Twc_ref, g["Xs"], g["Cs"], g["ii"], g["jj"], g["idx"],
+                                  g["valid"], g["Q"], sig0=0.003, sig1=10.0, C_thresh=0.0,
+                                  Q_thresh=1.5, max_iter=iters, delta_thresh=1e-8)
+        Twc, Xs, Cs, ii, jj, idx, valid, Q = _gn_case(g, dev)
+        (dx,) = mb.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.003, 10.0, 0.0, 1.5,
+                                     iters, 1e-8)
+        dx, ref_dx = dx.cpu().numpy(), ref["dx"]
+        if iters == 1:
+            # the first step (|dx| up to 0.15): f32 edge sums in another order than the
+            # oracle's, amplified along the 19-24 pose gauge chain — measured relative error
+            # of the whole step <= 1.2e-3 (poses after it off by up to 1.2e-4)
+            rel = np.linalg.norm(dx - ref_dx) / np.linalg.norm(ref_dx)
+            assert rel < 5e-3, f"first step relative error {rel:.2e}"
+        else:
+            # converged poses: the chain's f32 noise (measured <= 3.7e-5 at P = 24 on poses of
+            # magnitude ~1.2) — relative 5e-5 on top of the absolute bar.  The third step
+            # itself (|dx| ~ 1e-5 at P = 2) is the rounding noise of the gradient sums.
+            np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=POSE_TOL, rtol=5e-5)
 
 
 @pytest.mark.parametrize("P", [2, 16, 19])

@@ -44,32 +44,38 @@ e1.synchronize()
 print(f"product library: {e0.elapsed_time(e1) / 5:.3f} ms per solve of {ITERS} iterations "
       f"({e0.elapsed_time(e1) / 5 / ITERS * 1e3:.0f} us per iteration)", flush=True)
 
-dbg_path = os.environ.get("M3S_GN_STAMPS_LIB") or os.path.join(
-    ROOT, "monst3r-slam_amd/csrc/build/libm3s_gn_stamps.so")   # build/ does not travel
-lib = ctypes.CDLL(dbg_path)
+# debug libraries (comma-separated in M3S_GN_STAMPS_LIB: A/B builds of gn.hip)
+paths = (os.environ.get("M3S_GN_STAMPS_LIB") or os.path.join(
+    ROOT, "monst3r-slam_amd/csrc/build/libm3s_gn_stamps.so")).split(",")  # build/ stays here
 real = _lib.load()
-fn = lib.m3s_gauss_newton_rays
-fn.restype = ctypes.c_int
-fn.argtypes = real.m3s_gauss_newton_rays.argtypes
-lib.m3s_debug_gn_stamps.argtypes = [ctypes.c_void_p]
-
-
-class Shim:  # route the backend's call into the debug library
-    def __getattr__(self, k):
-        return fn if k == "m3s_gauss_newton_rays" else getattr(real, k)
-
-
-_lib.load = lambda: Shim()
-for _ in range(2):
-    run()
-torch.cuda.synchronize()
-buf = (ctypes.c_longlong * 128)()
-assert lib.m3s_debug_gn_stamps(buf) == 0
-st = np.array(buf[:], dtype=np.float64).reshape(16, 8) / 100.0  # µs
 names = ["edge-blocks", "assembly", "cholesky", "solves", "retract"]
-for it in range(ITERS):
-    d = np.diff(st[it, :6])
-    print(f"iteration {it}: " + " ".join(f"{n} {v:7.2f}" for n, v in zip(names, d))
-          + f" | solve kernel {st[it, 5] - st[it, 0]:7.2f} us"
-          + (f" | to next solve {st[it + 1, 0] - st[it, 5]:7.2f}" if it < ITERS - 1 else ""),
-          flush=True)
+for dbg_path in paths:
+    lib = ctypes.CDLL(dbg_path)
+    fn = lib.m3s_gauss_newton_rays
+    fn.restype = ctypes.c_int
+    fn.argtypes = real.m3s_gauss_newton_rays.argtypes
+    lib.m3s_debug_gn_stamps.argtypes = [ctypes.c_void_p]
+
+    class Shim:  # route the backend's call into the debug library
+        def __getattr__(self, k):
+            return fn if k == "m3s_gauss_newton_rays" else getattr(real, k)
+
+    _lib.load = lambda: Shim()
+    for _ in range(2):
+        run()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(5):
+        run()
+    e1.record()
+    e1.synchronize()
+    print(f"{os.path.basename(dbg_path)}: {e0.elapsed_time(e1) / 5 / ITERS * 1e3:.0f} us per "
+          "iteration", flush=True)
+    buf = (ctypes.c_longlong * 128)()
+    assert lib.m3s_debug_gn_stamps(buf) == 0
+    st = np.array(buf[:], dtype=np.float64).reshape(16, 8) / 100.0  # µs
+    for it in range(3):
+        d = np.diff(st[it, :6])
+        print(f"  iteration {it}: " + " ".join(f"{n} {v:7.2f}" for n, v in zip(names, d))
+              + f" | solve kernel {st[it, 5] - st[it, 0]:7.2f} us"
+              + f" | to next solve {st[it + 1, 0] - st[it, 5]:7.2f}", flush=True)
