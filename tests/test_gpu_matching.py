@@ -59,8 +59,9 @@ def test_refine_matches_bit_exact(oracle, dev, b, h, w):
 @pytest.mark.parametrize("radius,dmax", [(3, 5), (2, 3), (3, 1)])
 def test_refine_matches_scattered(oracle, dev, radius, dmax):
     # scattered p1 (windows off every image edge), 24-d descriptors, 3 directions, a tile
-    # count (5 x 6 = 30) that is not a multiple of the 8 XCDs: the radius-3 latency-hiding
-    # kernel and the generic 16x16-tile kernel (radius 2) on the same inputs
+    # count (5 x 6 = 30) that is not a multiple of the 8 XCDs: the radius-3 LDS-staged kernel
+    # (every box spans the image: its global-memory path) and the generic 16x16-tile kernel
+    # (radius 2) on the same inputs
     import mast3r_slam_backends as mb
     rng = np.random.default_rng(11 + radius)
     b, h, w = 3, 70, 90
@@ -69,6 +70,33 @@ def test_refine_matches_scattered(oracle, dev, radius, dmax):
     p1 = rng.integers(0, [w, h], size=(b, h * w, 2)).astype(np.int64)
     ref = oracle.refine_matches(d11, d21, p1, radius, dmax)
     (got,) = mb.refine_matches(_t(d11, dev), _t(d21, dev), _t(p1, dev), radius, dmax)
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("case", ["outliers", "shifted", "wide_jitter"])
+def test_refine_matches_match_fields(oracle, dev, case):
+    """Radius-3 refine on match fields between the smooth and the scattered tests: smooth
+    matches with 2 % scattered outliers (a tile's windows both local and spread over the
+    image), a large shift (windows cut by the image edges) and +-12 px jitter (a tile's
+    windows wider than at +-4) — bit-exact against the oracle."""
+    import mast3r_slam_backends as mb
+    rng = np.random.default_rng({"outliers": 21, "shifted": 22, "wide_jitter": 23}[case])
+    b, h, w = 2, 96, 160
+    d11 = rng.normal(size=(b, h, w, 24)).astype(np.float16)
+    d21 = rng.normal(size=(b, h * w, 24)).astype(np.float16)
+    yy, xx = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    p1 = np.stack([xx, yy], -1).reshape(1, -1, 2).repeat(b, 0).astype(np.int64)
+    if case == "outliers":
+        p1 += rng.integers(-3, 4, p1.shape)
+        out = rng.uniform(size=p1.shape[:2]) < 0.02
+        p1[out] = rng.integers(0, [w, h], size=(int(out.sum()), 2))
+    elif case == "shifted":
+        p1 += np.array([37, -21]) + rng.integers(-2, 3, p1.shape)
+    else:
+        p1 += rng.integers(-12, 13, p1.shape)
+    p1 = np.clip(p1, 0, [w - 1, h - 1]).astype(np.int64)
+    ref = oracle.refine_matches(d11, d21, p1, 3, 5)
+    (got,) = mb.refine_matches(_t(d11, dev), _t(d21, dev), _t(p1, dev), 3, 5)
     np.testing.assert_array_equal(got.cpu().numpy(), ref)
 
 

@@ -1,4 +1,6 @@
-"""Graph-timed refine_matches / iter_proj at 384x512 on a synthetic pair (tools only)."""
+"""Graph-timed refine_matches at 384x512 on a synthetic pair (tools only); M3S_LIB_PATH
+selects an A/B build of the library.
+Usage: [COHERENT=1] python tools/match_bench.py [batch] [jitter_px] [dilation_max]"""
 import ctypes
 import os
 import sys
@@ -15,9 +17,19 @@ h, w, F = 384, 512, 24
 n = h * w
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 J = int(sys.argv[2]) if len(sys.argv) > 2 else 4   # match jitter amplitude (px); 0 = smooth
+DMAX = int(sys.argv[3]) if len(sys.argv) > 3 else 5  # dilation levels
 g = torch.Generator(device=dev).manual_seed(0)
 D11 = torch.nn.functional.normalize(torch.randn(B, h, w, F, device=dev, generator=g), dim=-1).half()
 D21 = torch.nn.functional.normalize(torch.randn(B, n, F, device=dev, generator=g), dim=-1).half()
+if os.environ.get("COHERENT"):
+    # trained-network-like descriptors: a spatially smooth field (9 x 9 box filter of noise),
+    # each query's descriptor its true match's plus noise — the coarse-to-fine search then
+    # moves a tile's matches coherently toward the identity instead of scattering them
+    f = torch.randn(B, F, h, w, device=dev, generator=g)
+    f = torch.nn.functional.avg_pool2d(f, 9, stride=1, padding=4, count_include_pad=False)
+    D11 = torch.nn.functional.normalize(f.permute(0, 2, 3, 1), dim=-1).half().contiguous()
+    D21 = torch.nn.functional.normalize(D11.reshape(B, n, F).float() + 0.05 * torch.randn(
+        B, n, F, device=dev, generator=g), dim=-1).half().contiguous()
 # matches near the identity (as after iter_proj on consecutive frames): local windows overlap
 yy, xx = torch.meshgrid(torch.arange(h, device=dev), torch.arange(w, device=dev), indexing="ij")
 jit = torch.randint(-J, J + 1, (B, 2, h, w), device=dev, generator=g) + (3 if J == 0 else 0)
@@ -28,7 +40,7 @@ out = torch.empty_like(p1)
 
 def refine():
     _lib.check(lib.m3s_refine_matches(_lib.ptr(D11), _lib.ptr(D21), _lib.ptr(p1), _lib.ptr(out), B,
-                                      h, w, n, F, 3, 5, _lib.stream(dev)), "refine")
+                                      h, w, n, F, 3, DMAX, _lib.stream(dev)), "refine")
 
 
 def graph_us(fn, rep=20):
@@ -52,27 +64,8 @@ def graph_us(fn, rep=20):
     return e0.elapsed_time(e1) * 1e3 / rep
 
 
-D11p = torch.empty((B, 3, n, 8), dtype=torch.float16, device=dev)
-out2 = torch.empty_like(p1)
-
-
-def planar():
-    _lib.check(lib.m3s_desc_planar(_lib.ptr(D11), _lib.ptr(D11p), B, n, _lib.stream(dev)), "pl")
-
-
-def refine_planar():
-    _lib.check(lib.m3s_refine_matches_planar(_lib.ptr(D11p), _lib.ptr(D21), _lib.ptr(p1),
-                                             _lib.ptr(out2), B, h, w, 3, 5, _lib.stream(dev)),
-               "refine_planar")
-
-
-tag = os.environ.get("M3S_REFINE_KERNEL", "r3")
+lib_tag = os.path.basename(os.environ.get("M3S_LIB_PATH", "") or "product") + (
+    " coherent" if os.environ.get("COHERENT") else " random")
 us = graph_us(refine)
-print(f"refine_matches 384x512 r3 d5 b={B} jitter={J} {tag}: {us:.1f} us ({us / B:.1f} us per pair)", flush=True)
-us = graph_us(planar)
-print(f"desc_planar 384x512 b={B}: {us:.1f} us", flush=True)
-us = graph_us(refine_planar)
-print(f"refine_matches_planar 384x512 r3 d5 b={B} jitter={J}: {us:.1f} us ({us / B:.1f} us per pair)",
-      flush=True)
-torch.cuda.synchronize()
-print("planar == rows:", bool(torch.equal(out, out2)), flush=True)
+print(f"refine_matches 384x512 r3 d{DMAX} b={B} jitter={J} [{lib_tag}]: {us:.1f} us "
+      f"({us / B:.1f} us per pair)", flush=True)
