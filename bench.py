@@ -20,6 +20,10 @@ whole configs[2] sequence); a shorter K is also followed by an untimed-in-the-he
 200-frame pass ("c3_sequence_200").
 Multi-GPU: tracking is sequential per sequence → one independent replica per rank
 ("replicas only"); value = frames of all ranks / max rank time.
+`python bench.py --gpus N` (WORLD_SIZE unset) starts `python -m torch.distributed.run
+--nproc-per-node N --master-addr 127.0.0.1 ...` over this file as a child process before
+any GPU call and exits with its status; under an external launcher --gpus must equal
+WORLD_SIZE.
 
 Also measured at every N (field "keyframe_graph", configs[3]): 16 keyframes,
 64 pairs re-inferred symmetrically (4 directed decodes + 8 heads each) and matched both ways,
@@ -359,13 +363,15 @@ def step_pmc():
     (tools/step_prof.py under rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU
     GRBM_GUI_ACTIVE, summarised by tools/step_pmc_report.py; counters cannot be read from
     inside the timed run).  None if absent."""
-    path = os.path.join(ROOT, "profiles", "r03_step_pmc.json")
-    if not os.path.exists(path):
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_step_pmc.json")))
+    if not found:
         return None
+    path = found[-1]                        # the newest round's pass
     d = dict(json.load(open(path)))
     if isinstance(d.get("traced"), dict):   # the per-kernel table stays in the profile file
         d["traced"] = {k: v for k, v in d["traced"].items() if k != "kernels"}
-    d["source"] = "profiles/r03_step_pmc.json"
+    d["source"] = "profiles/" + os.path.basename(path)
     return d
 
 
@@ -954,7 +960,11 @@ def main():
                                    ("" if args.no_split_heads else
                                     "; MASt3R DPT heads on a side stream"),
                        "h": H, "w": W, "models": "MonST3R ViT-L/B dpt + MASt3R ViT-L/B catmlp+dpt",
-                       "parallelism": f"replicas{world}"},
+                       "parallelism": f"replicas{world}",
+                       # tuning / A-B overrides the library and the model read (tools only):
+                       # a stray one changes the timed schedule, so it is printed with it
+                       "env_overrides": {k: v for k, v in sorted(os.environ.items())
+                                         if k.startswith("M3S_")}},
             "sequence": seq_rep,
             "pair_inference_ms": pair_ms,
             "roofline": roofline_entry(tl, roof, pmc, mfma, ms),

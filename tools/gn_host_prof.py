@@ -1,8 +1,8 @@
 """Diagnostic: where the host time of the backend GN goes.  Runs the bench's keyframe-graph
 leg (configs[3], one step) and profiles its final ShardedFactorGraph._solve_sharded('rays')
 call with cProfile (torch ops that synchronise show up as their own entries), then times the
-same call three more times.
-Usage: python tools/gn_host_prof.py"""
+same call three more times.  GN_DUMP=path saves the call's inputs (tools/gn_stamps.py).
+Usage: [GN_DUMP=path] python tools/gn_host_prof.py"""
 import cProfile
 import os
 import pstats
@@ -25,6 +25,15 @@ calls = []
 
 def wrapped(self, mode):
     calls.append(1)             # the bench calls it once, after its timed graph steps
+    if os.environ.get("GN_DUMP"):   # the call's inputs, for tools/gn_stamps.py GN_INPUTS=...
+        uniq = self.get_unique_kf_idx()
+        Xs, T_WCs, Cs = self.get_poses_points(uniq)
+        torch.save({"Twc": T_WCs[:, 0, :].contiguous(), "Xs": Xs.contiguous(),
+                    "Cs": Cs.contiguous(), "ii": torch.cat((self.ii, self.jj)),
+                    "jj": torch.cat((self.jj, self.ii)),
+                    "idx": torch.cat((self.idx_ii2jj, self.idx_jj2ii)),
+                    "valid": torch.cat((self.valid_match_j, self.valid_match_i)),
+                    "Q": torch.cat((self.Q_ii2jj, self.Q_jj2ii))}, os.environ["GN_DUMP"])
     torch.cuda.synchronize(dev)
     pr = cProfile.Profile()
     pr.enable()

@@ -3,7 +3,7 @@ two-way edges, 384 x 512 points) — wall time per iteration of mast3r_slam_back
 gauss_newton_rays, and, with the debug library (make -C monst3r-slam_amd/csrc gn_stamps),
 the LDS solve's phase timeline per iteration: per-edge blocks, assembly, Cholesky,
 triangular solves, retraction / convergence (µs, thread 0, s_memrealtime).
-Usage: python tools/gn_stamps.py"""
+Usage: [SCATTER=1] python tools/gn_stamps.py   (SCATTER: shifted, jittered match indices)"""
 import ctypes
 import os
 import sys
@@ -21,9 +21,23 @@ dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
 ITERS = 10
 g = syn.keyframe_graph(P=16, h=384, w=512, seed=5, pairs=64, two_way=True)
+if os.environ.get("SCATTER"):  # match indices as a moving camera's: shifted, jittered
+    rng = np.random.default_rng(1)
+    h, w = 384, 512
+    yy, xx = np.divmod(np.arange(h * w), w)
+    for e in range(g["idx"].shape[0]):
+        dx, dy = rng.integers(-40, 41, 2)
+        u = np.clip(xx + dx + rng.integers(-3, 4, h * w), 0, w - 1)
+        v = np.clip(yy + dy + rng.integers(-3, 4, h * w), 0, h - 1)
+        g["idx"][e] = v * w + u
 host = {k: torch.from_numpy(np.ascontiguousarray(g[k])) for k in
         ("Twc", "Xs", "Cs", "ii", "jj", "idx", "valid", "Q")}
 dv = {k: v.to(dev) for k, v in host.items()}
+if os.environ.get("GN_INPUTS"):  # the bench's keyframe-graph GN call (tools/gn_host_prof.py)
+    dv = {k: v.to(dev) for k, v in torch.load(os.environ["GN_INPUTS"]).items()}
+    dv["valid"] = dv["valid"].reshape(dv["idx"].shape[0], -1, 1)
+    dv["Q"] = dv["Q"].reshape(dv["idx"].shape[0], -1, 1)
+    print({k: (tuple(v.shape), str(v.dtype)) for k, v in dv.items()}, flush=True)
 
 
 def run():
