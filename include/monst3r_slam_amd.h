@@ -111,9 +111,11 @@ int m3s_pixel_to_lin(const int64_t* d_p1, int64_t* d_idx, int64_t b, int64_t n, 
  * the step is zero (reference :142-150) and M3S_ERR_NOT_PD is reported through
  * *h_status_out after the call completes (it is written by a final D2H copy; the call
  * synchronises `stream` only when h_status_out != NULL).
- * workspace: d_workspace of m3s_gn_workspace_bytes(P, E) bytes (device).
+ * workspace: d_workspace of m3s_gn_workspace_bytes(P, E, N) bytes (device); it includes a
+ * packed copy of the inputs (16-B (X, C) records, 32-bit match indices: 16 P N + 4 E N B).
+ * N < 2^31.
  * ------------------------------------------------------------------------- */
-size_t m3s_gn_workspace_bytes(int64_t num_poses, int64_t num_edges);
+size_t m3s_gn_workspace_bytes(int64_t num_poses, int64_t num_edges, int64_t num_points);
 
 /* Replaces mast3r_slam_backends.gauss_newton_rays (gn.cpp:28-50 → gn_kernels.cu:1140-1228). */
 int m3s_gauss_newton_rays(float* d_Twc, const float* d_Xs, const float* d_Cs,
@@ -157,7 +159,9 @@ int m3s_gn_force_global_solve(int on);
  *                                    (28 of Σ w J'J'ᵀ + 7 of Σ w e J')
  *   (caller) all-gather the rows into d_G_all [E_total][35] in global edge order
  *   m3s_gn_solve_step              → assemble + fp64 Cholesky + retract + convergence flag
- * m3s_gn_sharded_begin once before (ranks of all E_total edges, flags, dx = 0);
+ * m3s_gn_sharded_begin once before (ranks of all E_total edges, flags, dx = 0); the first
+ * edge pass after it packs Xs / Cs / idx / valid into the workspace, later ones (until the
+ * next begin) read that copy — the points and matches are fixed during a solve;
  * m3s_gn_sharded_status after (synchronises; status as h_status_out of the calls above,
  * iterations taken).  The split count S follows E_total, so every edge's sums — and the
  * poses — are bit-identical to the unsharded call's.  After convergence the kernels exit

@@ -174,15 +174,25 @@ __device__ __forceinline__ void point_acc(float* acc, bool vm, int64_t ind, cons
 
 template <int MODE>
 __global__ __launch_bounds__(kEdgeThreads) void gn_edge_kernel(
-    const float* __restrict__ Twc, const float* __restrict__ Xs, const float* __restrict__ Cs,
-    const float* __restrict__ K, const int* __restrict__ rank_ii,
-    const int* __restrict__ rank_jj, const int64_t* __restrict__ idx_ii2jj,
-    const uint8_t* __restrict__ valid_match, const float* __restrict__ Q,
-    float* __restrict__ partial, const int* __restrict__ flags, int64_t num_points, int S,
-    GnParams prm, const int* __restrict__ edge_ids) {
+    const float* __restrict__ Twc, const float4* __restrict__ XC, const float* __restrict__ K,
+    const int* __restrict__ rank_ii, const int* __restrict__ rank_jj,
+    const int* __restrict__ MI, const float* __restrict__ Q,
+    float* __restrict__ partial, int* __restrict__ flags, int64_t num_points, int S,
+    GnParams prm, const int* __restrict__ edge_ids, const int* __restrict__ order, int rows) {
   if (flags[0]) return;  // converged in an earlier iteration
-  const int e = blockIdx.x;     // row of this rank's edge data (idx / valid / Q / partial)
-  const int s = blockIdx.y;
+  // 1-D grid of rows x S blocks, dispatched round-robin over the 8 XCDs: block -> position v
+  // in (row in `order`, split) sequence so that each XCD takes a contiguous run of the rows
+  // sorted by pose i — its L2 then holds few keyframes' pointmaps for the scattered Xi / Ci
+  // gathers instead of every keyframe's.  Same per-block work and partial slot either way.
+  int e, s;
+  {
+    const int total = rows * S, lin = blockIdx.x, xcd = lin & 7, loc = lin >> 3;
+    const int tq = total >> 3, tr = total & 7;
+    const int v = xcd < tr ? xcd * (tq + 1) + loc : tr * (tq + 1) + (xcd - tr) * tq + loc;
+    const int pos = v / S;
+    s = v - pos * S;
+    e = order[pos];             // row of this rank's edge data (idx / valid / Q / partial)
+  }
   const int ge = edge_ids ? edge_ids[e] : e;   // the edge's id in the whole graph
   const int ix = rank_ii[ge], jx = rank_jj[ge];
   const float* Ti = Twc + 8 * ix;
@@ -204,49 +214,37 @@ __global__ __launch_bounds__(kEdgeThreads) void gn_edge_kernel(
   const int64_t chunk = (num_points + S - 1) / S;
   const int64_t k0 = (int64_t)s * chunk;
   const int64_t k1 = min(num_points, k0 + chunk);
-  const float* Xi_base = Xs + (int64_t)ix * num_points * 3;
-  const float* Xj_base = Xs + (int64_t)jx * num_points * 3;
-  const float* Ci_base = Cs + (int64_t)ix * num_points;
-  const float* Cj_base = Cs + (int64_t)jx * num_points;
+  const float4* XCi = XC + (int64_t)ix * num_points;  // (X, C) records (gn_pack_kernel)
+  const float4* XCj = XC + (int64_t)jx * num_points;
   const int64_t eoff = (int64_t)e * num_points;
 
-  // U points per thread per trip: their independent loads (valid, idx, Q, Xj, Cj) issue back
-  // to back, then their gathers at the match index (Xi, Ci), then the arithmetic — two
-  // memory round trips per U points instead of per point.  Lanes past k1 load point k1 - 1
-  // and accumulate it as invalid (weight 0).
+  // U points per thread per trip: their independent loads (match, Q, record j) issue back to
+  // back, then their gathers of record i at the match index, then the arithmetic — two
+  // memory round trips per U points instead of per point, one 16-B gather per point.
+  // Lanes past k1 load point k1 - 1 and accumulate it as invalid (weight 0).
   constexpr int U = 4;
   for (int64_t kb = k0 + threadIdx.x; kb < k1; kb += U * kEdgeThreads) {
-    int64_t kk[U];
-    uint8_t vmb[U];
-    int64_t raw[U];
-    float xj[U][3], qv[U], cjv[U], xi[U][3], civ[U];
+    int mi[U];
+    float qv[U];
+    float4 rj[U], ri[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      kk[u] = min(kb + (int64_t)u * kEdgeThreads, k1 - 1);
-      vmb[u] = valid_match[eoff + kk[u]];
-      raw[u] = idx_ii2jj[eoff + kk[u]];
-      xj[u][0] = Xj_base[3 * kk[u]];
-      xj[u][1] = Xj_base[3 * kk[u] + 1];
-      xj[u][2] = Xj_base[3 * kk[u] + 2];
-      qv[u] = Q[eoff + kk[u]];
-      cjv[u] = Cj_base[kk[u]];
+      const int64_t k = min(kb + (int64_t)u * kEdgeThreads, k1 - 1);
+      mi[u] = MI[eoff + k];
+      qv[u] = Q[eoff + k];
+      rj[u] = XCj[k];
     }
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int64_t ind = vmb[u] ? raw[u] : 0;
-      raw[u] = ind;
-      xi[u][0] = Xi_base[3 * ind];
-      xi[u][1] = Xi_base[3 * ind + 1];
-      xi[u][2] = Xi_base[3 * ind + 2];
-      civ[u] = Ci_base[ind];
-    }
+    for (int u = 0; u < U; u++) ri[u] = XCi[mi[u] >= 0 ? mi[u] : 0];
 #pragma unroll
     for (int u = 0; u < U; u++) {  // unconditional (a branch would sink the loads into it)
       const bool in = kb + (int64_t)u * kEdgeThreads < k1;
-      point_acc<MODE>(acc, in && vmb[u] != 0, raw[u], xi[u], civ[u], xj[u], qv[u], cjv[u], tij,
-                      qij, sij, prm, fx, fy, cx, cy);
+      const float xi[3] = {ri[u].x, ri[u].y, ri[u].z}, xj[3] = {rj[u].x, rj[u].y, rj[u].z};
+      point_acc<MODE>(acc, in && mi[u] >= 0, mi[u] >= 0 ? mi[u] : 0, xi, ri[u].w, xj, qv[u],
+                      rj[u].w, tij, qij, sij, prm, fx, fy, cx, cy);
     }
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) flags[4] = 1;  // the records are packed (below)
 
   // workgroup reduction: wave butterfly, then 4 waves through LDS
   __shared__ float red[kEdgeThreads / M3S_WAVE][kAcc];
@@ -263,6 +261,44 @@ __global__ __launch_bounds__(kEdgeThreads) void gn_edge_kernel(
     for (int wv = 1; wv < kEdgeThreads / M3S_WAVE; wv++) v += red[wv][threadIdx.x];
     partial[((int64_t)e * S + s) * kAcc + threadIdx.x] = v;
   }
+}
+
+// The rows of an edge pass sorted by the rank of pose i (counting sort in LDS, one
+// workgroup; the order within a pose is immaterial: each row's partials are its own).
+__global__ __launch_bounds__(kSolveThreads) void gn_order_kernel(
+    const int* __restrict__ rank_ii, const int* __restrict__ edge_ids, int rows, int P,
+    int* __restrict__ order) {
+  extern __shared__ int cnt[];  // [P + 1]
+  for (int p = threadIdx.x; p <= P; p += blockDim.x) cnt[p] = 0;
+  __syncthreads();
+  for (int r = threadIdx.x; r < rows; r += blockDim.x)
+    atomicAdd(&cnt[rank_ii[edge_ids ? edge_ids[r] : r] + 1], 1);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int p = 1; p <= P; p++) cnt[p] += cnt[p - 1];
+  __syncthreads();
+  for (int r = threadIdx.x; r < rows; r += blockDim.x)
+    order[atomicAdd(&cnt[rank_ii[edge_ids ? edge_ids[r] : r]], 1)] = r;
+}
+
+// The edge pass's inputs repacked once per solve (flags[4] = 0; the first edge pass sets
+// it): XC f32x4 [P][N] = (X, C) of every point — one 16-B gather per matched point instead
+// of a 12-B and a 4-B one — and MI i32 [rows][N] = the match index where valid, -1 where not
+// (the reference's `valid ? idx : 0` with the flag folded in; 4 B streamed instead of 9).
+__global__ __launch_bounds__(256) void gn_pack_kernel(const float* __restrict__ Xs,
+                                                      const float* __restrict__ Cs,
+                                                      const int64_t* __restrict__ idx,
+                                                      const uint8_t* __restrict__ valid,
+                                                      int64_t n_pts, int64_t n_match,
+                                                      float4* __restrict__ XC,
+                                                      int* __restrict__ MI,
+                                                      const int* __restrict__ flags) {
+  if (flags[4]) return;  // packed by an earlier edge pass of this solve
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pts; i += stride)
+    XC[i] = make_float4(Xs[3 * i], Xs[3 * i + 1], Xs[3 * i + 2], Cs[i]);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_match; i += stride)
+    MI[i] = valid[i] ? (int)idx[i] : -1;
 }
 
 // ranks of ii/jj in sorted unique(ii ∪ jj) (gn_kernels.cu:161-170, torch::_unique +
@@ -917,8 +953,8 @@ int choose_splits(int64_t E, int64_t N) {
 }
 
 struct Layout {
-  size_t flags, rank_ii, rank_jj, partial, A, b, G, EB, blk_start, blk_list, vec_start, vec_list,
-      total;
+  size_t flags, rank_ii, rank_jj, order, xc, mi, partial, A, b, G, EB, blk_start, blk_list,
+      vec_start, vec_list, total;
 };
 
 // the LDS solve's regions (EB, contribution lists) appended at `off`
@@ -938,7 +974,7 @@ size_t lds_regions(L& l, size_t off, int64_t P, int64_t E) {
   return off;
 }
 
-Layout make_layout(int64_t P, int64_t E, int S) {
+Layout make_layout(int64_t P, int64_t E, int S, int64_t N) {
   Layout L;
   const int64_t n = 7 * (P > 1 ? P - 1 : 0);
   size_t off = 0;
@@ -948,6 +984,12 @@ Layout make_layout(int64_t P, int64_t E, int S) {
   off = align_up(off + 4 * E, 256);
   L.rank_jj = off;
   off = align_up(off + 4 * E, 256);
+  L.order = off;
+  off = align_up(off + 4 * E, 256);
+  L.xc = off;
+  off = align_up(off + 16 * P * N, 256);
+  L.mi = off;
+  off = align_up(off + 4 * E * N, 256);
   L.partial = off;
   off = align_up(off + 4 * E * S * kAcc, 256);
   L.A = off;
@@ -993,10 +1035,10 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
   if (!d_Twc || !d_Xs || !d_Cs || !d_ii || !d_jj || !d_idx || !d_valid || !d_Q || !d_ws)
     return M3S_ERR_INVALID_ARG;
   if (MODE == MODE_CALIB && !d_K) return M3S_ERR_INVALID_ARG;
-  if (E > 65535 || 7 * P > 46000) return M3S_ERR_TOO_LARGE;
+  if (E > 65535 || 7 * P > 46000 || N >= (1ll << 31)) return M3S_ERR_TOO_LARGE;
   hipStream_t st = m3s_stream(stream);
   const int S = choose_splits(E, N);
-  const Layout L = make_layout(P, E, S);
+  const Layout L = make_layout(P, E, S, N);
   char* ws = reinterpret_cast<char*>(d_ws);
   int* flags = reinterpret_cast<int*>(ws + L.flags);
   int* rii = reinterpret_cast<int*>(ws + L.rank_ii);
@@ -1010,6 +1052,15 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
   hipLaunchKernelGGL(gn_rank_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_ii, d_jj, (int)E, rii,
                      rjj, flags);
   M3S_LAUNCH_CHECK();
+  int* order = reinterpret_cast<int*>(ws + L.order);
+  hipLaunchKernelGGL(gn_order_kernel, dim3(1), dim3(kSolveThreads), sizeof(int) * (P + 1), st,
+                     rii, nullptr, (int)E, (int)P, order);
+  M3S_LAUNCH_CHECK();
+  float4* XC = reinterpret_cast<float4*>(ws + L.xc);
+  int* MI = reinterpret_cast<int*>(ws + L.mi);
+  hipLaunchKernelGGL(gn_pack_kernel, dim3(2048), dim3(256), 0, st, d_Xs, d_Cs, d_idx, d_valid,
+                     P * N, E * N, XC, MI, flags);
+  M3S_LAUNCH_CHECK();
   const bool lds = use_lds_solve(P);
   if (lds) {
     const int st_l = launch_lists(ws, L, rii, rjj, E, P, st);
@@ -1017,9 +1068,9 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
   }
   if (P > 1) {
     for (int it = 0; it < max_iter; it++) {
-      hipLaunchKernelGGL(gn_edge_kernel<MODE>, dim3((unsigned)E, (unsigned)S),
-                         dim3(kEdgeThreads), 0, st, d_Twc, d_Xs, d_Cs, d_K, rii, rjj, d_idx,
-                         d_valid, d_Q, partial, flags, N, S, prm, nullptr);
+      hipLaunchKernelGGL(gn_edge_kernel<MODE>, dim3((unsigned)(E * S)), dim3(kEdgeThreads), 0,
+                         st, d_Twc, XC, d_K, rii, rjj, MI, d_Q, partial, flags, N, S, prm,
+                         nullptr, order, (int)E);
       M3S_LAUNCH_CHECK();
       if (lds)
         hipLaunchKernelGGL(gn_solve_lds_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_Twc,
@@ -1047,8 +1098,8 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
 // edges, the dense system.  S comes from E_total, so every edge's partials — hence its G
 // row — are those of the unsharded m3s_gauss_newton_* call, bit for bit.
 struct ShardLayout {
-  size_t flags, rank_ii, rank_jj, partial, A, b, EB, blk_start, blk_list, vec_start, vec_list,
-      total;
+  size_t flags, rank_ii, rank_jj, order, xc, mi, partial, A, b, EB, blk_start, blk_list,
+      vec_start, vec_list, total;
   int S;
 };
 
@@ -1063,6 +1114,12 @@ ShardLayout make_shard_layout(int64_t P, int64_t E_total, int64_t E_local, int64
   off = align_up(off + 4 * E_total, 256);
   L.rank_jj = off;
   off = align_up(off + 4 * E_total, 256);
+  L.order = off;
+  off = align_up(off + 4 * (E_local > 0 ? E_local : 1), 256);
+  L.xc = off;
+  off = align_up(off + 16 * P * N, 256);
+  L.mi = off;
+  off = align_up(off + 4 * (E_local > 0 ? E_local : 1) * N, 256);
   L.partial = off;
   off = align_up(off + 4 * (E_local > 0 ? E_local : 1) * L.S * kAcc, 256);
   L.A = off;
@@ -1074,8 +1131,8 @@ ShardLayout make_shard_layout(int64_t P, int64_t E_total, int64_t E_local, int64
 }
 
 bool shard_sizes_ok(int64_t P, int64_t N, int64_t E_total, int64_t E_local) {
-  return P >= 1 && N >= 1 && E_total >= 1 && E_local >= 0 && E_local <= E_total &&
-         E_total <= 65535 && 7 * P <= 46000;
+  return P >= 1 && N >= 1 && N < (1ll << 31) && E_total >= 1 && E_local >= 0 &&
+         E_local <= E_total && E_total <= 65535 && 7 * P <= 46000;
 }
 
 template <int MODE>
@@ -1090,14 +1147,23 @@ int shard_edge_pass(const float* d_Twc, const float* d_Xs, const float* d_Cs, co
   if (MODE == MODE_CALIB && !d_K) return M3S_ERR_INVALID_ARG;
   const ShardLayout L = make_shard_layout(P, E_total, E_local, N);
   char* ws = reinterpret_cast<char*>(d_ws);
-  const int* flags = reinterpret_cast<const int*>(ws + L.flags);
+  int* flags = reinterpret_cast<int*>(ws + L.flags);
   float* partial = reinterpret_cast<float*>(ws + L.partial);
   hipStream_t st = m3s_stream(stream);
-  hipLaunchKernelGGL(gn_edge_kernel<MODE>, dim3((unsigned)E_local, (unsigned)L.S),
-                     dim3(kEdgeThreads), 0, st, d_Twc, d_Xs, d_Cs, d_K,
+  float4* XC = reinterpret_cast<float4*>(ws + L.xc);
+  int* MI = reinterpret_cast<int*>(ws + L.mi);
+  hipLaunchKernelGGL(gn_pack_kernel, dim3(2048), dim3(256), 0, st, d_Xs, d_Cs, d_idx, d_valid,
+                     P * N, E_local * N, XC, MI, flags);
+  M3S_LAUNCH_CHECK();
+  int* order = reinterpret_cast<int*>(ws + L.order);
+  hipLaunchKernelGGL(gn_order_kernel, dim3(1), dim3(kSolveThreads), sizeof(int) * (P + 1), st,
                      reinterpret_cast<const int*>(ws + L.rank_ii),
-                     reinterpret_cast<const int*>(ws + L.rank_jj), d_idx, d_valid, d_Q, partial,
-                     flags, N, L.S, prm, reinterpret_cast<const int*>(d_edge_ids));
+                     reinterpret_cast<const int*>(d_edge_ids), (int)E_local, (int)P, order);
+  M3S_LAUNCH_CHECK();
+  hipLaunchKernelGGL(gn_edge_kernel<MODE>, dim3((unsigned)(E_local * L.S)), dim3(kEdgeThreads),
+                     0, st, d_Twc, XC, d_K, reinterpret_cast<const int*>(ws + L.rank_ii),
+                     reinterpret_cast<const int*>(ws + L.rank_jj), MI, d_Q, partial, flags, N,
+                     L.S, prm, reinterpret_cast<const int*>(d_edge_ids), order, (int)E_local);
   M3S_LAUNCH_CHECK();
   hipLaunchKernelGGL(gn_reduce_kernel, dim3(m3s_div_up(E_local * kAcc, 256)), dim3(256), 0, st,
                      partial, d_G, flags, (int)E_local, L.S);
@@ -1227,11 +1293,11 @@ extern "C" int m3s_gn_sharded_status(const void* d_ws, int64_t num_poses, int* h
   return M3S_OK;
 }
 
-extern "C" size_t m3s_gn_workspace_bytes(int64_t num_poses, int64_t num_edges) {
-  if (num_poses < 1 || num_edges < 1) return 256;
-  // worst-case S for any N
-  const int S = choose_splits(num_edges, (int64_t)1 << 40);
-  return make_layout(num_poses, num_edges, S).total;
+extern "C" size_t m3s_gn_workspace_bytes(int64_t num_poses, int64_t num_edges,
+                                         int64_t num_points) {
+  if (num_poses < 1 || num_edges < 1 || num_points < 1) return 256;
+  return make_layout(num_poses, num_edges, choose_splits(num_edges, num_points), num_points)
+      .total;
 }
 
 extern "C" int m3s_gauss_newton_rays(float* d_Twc, const float* d_Xs, const float* d_Cs,

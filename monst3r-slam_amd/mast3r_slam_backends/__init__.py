@@ -79,7 +79,7 @@ def _gn_common(Twc, Xs, Cs, ii, jj, idx_ii2jj, valid_match, Q):
     E = ii.shape[0]
     dev = Twc.device
     dx = torch.zeros((max(P - 1, 0), 7), dtype=torch.float32, device=dev)
-    nbytes = _lib.load().m3s_gn_workspace_bytes(P, E)
+    nbytes = _lib.load().m3s_gn_workspace_bytes(P, E, N)
     ws = torch.empty((nbytes,), dtype=torch.uint8, device=dev)
     return P, N, E, dx, ws
 

@@ -34,7 +34,7 @@ SIGNATURES = {
     "m3s_match_prep": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P]),
     "m3s_match_occlusion": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _P]),
     "m3s_pixel_to_lin": (_I, [_P, _P, _I64, _I64, _I64, _P]),
-    "m3s_gn_workspace_bytes": (_SZ, [_I64, _I64]),
+    "m3s_gn_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
     "m3s_gauss_newton_rays": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _F, _F,
                                    _F, _I, _F, _P, _P, _P, _P]),
     "m3s_gauss_newton_calib": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I, _I,

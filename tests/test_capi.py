@@ -47,7 +47,7 @@ def test_invalid_args_rejected_without_device():
     assert lib.m3s_refine_matches(None, None, None, None, 1, 8, 8, 64, 24, 3, 5, None) == -1
     assert lib.m3s_iter_proj(None, None, None, None, None, 0, 8, 8, 0, 10, 1e-8, 1e-6,
                              None) == 0
-    assert lib.m3s_gn_workspace_bytes(10, 20) > 0
+    assert lib.m3s_gn_workspace_bytes(10, 20, 100) > 16 * 10 * 100 + 4 * 20 * 100
 
 
 def test_dropin_module_surface():
