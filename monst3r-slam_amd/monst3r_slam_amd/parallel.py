@@ -347,7 +347,12 @@ class ShardedFactorGraph(FactorGraph):
         Xs, Cs = Xs.contiguous(), Cs.contiguous()
         ii = torch.cat((self.ii, self.jj)).contiguous()
         jj = torch.cat((self.jj, self.ii)).contiguous()
-        ids = self.local_edge_ids().contiguous()
+        # the edge → rank map on the host once (one small copy) — the slab layout below is
+        # host arithmetic, not a device bincount / nonzero per rank (each a sync)
+        owner_h = self.owner.cpu().long()
+        E = self.ii.numel()
+        mine = torch.nonzero(owner_h == rank).flatten()
+        ids = torch.cat([mine, mine + E]).to(torch.int32).to(self.device).contiguous()
         idx = torch.cat((self.idx_ii2jj, self.idx_jj2ii)).contiguous()
         valid = torch.cat((self.valid_match_j, self.valid_match_i)).contiguous()
         Q = torch.cat((self.Q_ii2jj, self.Q_jj2ii)).contiguous()
@@ -360,19 +365,19 @@ class ShardedFactorGraph(FactorGraph):
                          device=dev)
         dx = torch.zeros((max(P - 1, 1), 7), dtype=torch.float32, device=dev)
         # the per-edge rows all-gather as equal-size padded slabs; where each rank's rows go
-        counts = torch.bincount(self.owner.long(), minlength=world).tolist()
+        counts = torch.bincount(owner_h, minlength=world).tolist()
         pad = max(1, 2 * max(counts))
         G_loc = torch.zeros((pad, 35), dtype=torch.float64, device=dev)
         G_all = torch.zeros((E2, 35), dtype=torch.float64, device=dev)
-        E = self.ii.numel()
         slot = []                                  # gathered row → global two-way edge id
         for r_ in range(world):
-            loc = torch.nonzero(self.owner == r_).flatten()
+            loc = torch.nonzero(owner_h == r_).flatten()
             slot.append(torch.cat([loc, loc + E, torch.full((pad - 2 * loc.numel(),), -1,
-                                                           dtype=loc.dtype, device=dev)]))
+                                                           dtype=loc.dtype)]))
         slot = torch.cat(slot)
-        take = torch.nonzero(slot >= 0).flatten()    # index lists, built once: no per-
-        dst = slot.index_select(0, take)              # iteration mask (a host sync)
+        take_h = torch.nonzero(slot >= 0).flatten()  # index lists, built once: no per-
+        take = take_h.to(dev)                         # iteration mask (a host sync)
+        dst = slot.index_select(0, take_h).to(dev)
         _lib.check(lib.m3s_gn_sharded_begin(ptr(ii), ptr(jj), P, N, E2, El, ptr(dx), ptr(ws), s),
                    "gn_sharded_begin")
         loop_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
