@@ -820,61 +820,85 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
   __syncthreads();
   M3S_GS(2)
 
-  // 3) right-looking Cholesky in LDS, one barrier per column.  Each thread forms L[i][k] =
-  //    A[i][k] / piv and L[j][k] on the fly for its entries (i, j) of the trailing triangle
-  //    (the same products as gn_solve_kernel's scaled column); L[., k] goes to the unused
-  //    upper triangle (L[i][k] = sA[k n + i]) so that no one overwrites column k while it is
-  //    being read.  The next pivot's 1 / sqrt(d) is formed by the thread that finishes
-  //    A[k+1][k+1] (its row has one column: done long before the longest rows) and read from
-  //    sR after the barrier.
-  __shared__ int s_fail[2];  // pivot k's test in s_fail[k & 1]: written in step k - 1,
-  bool fail = false;         // read after its barrier, never while it is being read
-  if (tid == 0) {
-    const double d = sA[0];
-    s_fail[0] = !(d > 0.0);
-    s_fail[1] = 0;
-    sR[0] = 1.0 / sqrt(d);
-  }
+  // 3) blocked right-looking Cholesky in LDS, one 7-column panel per pose, two barriers per
+  //    panel (instead of one per column).  Wave 0 factors the panel with its rows in
+  //    registers (row c0 + lane + 64 t; the pivot row and L[j][k] of the panel's rows come
+  //    from lanes 0..6 by v_readlane), then every thread applies the panel to its entries
+  //    (i, j) of the trailing triangle, the seven updates in column order.  Each entry
+  //    receives the unblocked algorithm's operations in the same order (A[i][j] -= L[i][k]
+  //    L[j][k], k increasing; L[i][k] = A[i][k] · (1 / √A[k][k])), so the factor — and the
+  //    poses — are bit-identical to gn_solve_kernel's.  L[., k] goes to the unused upper
+  //    triangle (L[i][k] = sA[k n + i]), 1 / L[k][k] to sR[k].
+  auto bcast = [](double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+  };
+  __shared__ int s_fail;
+  bool fail = false;
+  if (tid == 0) s_fail = 0;
   __syncthreads();
-  {
-    // thread (row i = k + 1 + ri, column group cg): columns j = k + 1 + cg, + 8, ... <= i.
-    // (Measured against two alternatives at P = 16: all of a thread's reads issued before
-    // its writes, 16-deep unrolled, 110 us; row pairs (ra, m - 1 - ra) balanced over 16
-    // column groups, 105 us; this plain loop is LDS-issue-bound at fewer instructions.)
-    const int ri = tid >> 3, cg = tid & 7;  // 128 rows x 8 column groups (n - k - 1 <= 125)
-    for (int k = 0; k < n; k++) {
-      if (s_fail[k & 1]) {  // uniform: every thread leaves at the same k
-        fail = true;
-        break;
+  for (int c0 = 0; c0 < n; c0 += 7) {
+    if (wv == 0) {
+      const int i0 = c0 + lane, i1 = c0 + 64 + lane;  // n - c0 <= 126 rows
+      double a0[7], a1[7];
+#pragma unroll
+      for (int c = 0; c < 7; c++) {
+        a0[c] = i0 < n ? sA[i0 * n + c0 + c] : 0.0;
+        a1[c] = i1 < n ? sA[i1 * n + c0 + c] : 0.0;
       }
-      const double rpiv = sR[k];
-      const int i = k + 1 + ri;
-      if (i < n) {
-        const double li = sA[i * n + k] * rpiv;
-        for (int j = k + 1 + cg; j <= i; j += 8) sA[i * n + j] -= li * (sA[j * n + k] * rpiv);
-        if (cg == 0) {
-          sA[k * n + i] = li;
-          if (ri == 0) {  // row k + 1's only column: A[k+1][k+1] is final, the next pivot
-            const double d = sA[i * n + i];
-            s_fail[i & 1] = !(d > 0.0);
-            sR[i] = 1.0 / sqrt(d);
-          }
+      bool f = false;
+#pragma unroll
+      for (int c = 0; c < 7; c++) {
+        const int k = c0 + c;
+        const double d = bcast(a0[c], c);             // A[k][k]: row k is lane c
+        if (!(d > 0.0)) {
+          f = true;
+          break;
+        }
+        const double rpiv = 1.0 / sqrt(d);
+        const double l0 = a0[c] * rpiv, l1 = a1[c] * rpiv;
+        if (i0 > k && i0 < n) sA[k * n + i0] = l0;
+        if (i1 > k && i1 < n) sA[k * n + i1] = l1;
+        if (lane == 0) sR[k] = rpiv;
+#pragma unroll
+        for (int c2 = c + 1; c2 < 7; c2++) {
+          const double lj = bcast(l0, c2);            // L[c0 + c2][k]
+          if (i0 >= c0 + c2) a0[c2] -= l0 * lj;
+          if (i1 >= c0 + c2) a1[c2] -= l1 * lj;
         }
       }
-      __syncthreads();
+      if (lane == 0 && f) s_fail = 1;
     }
+    __syncthreads();
+    if (s_fail) {  // uniform: read after the barrier by every thread
+      fail = true;
+      break;
+    }
+    const int t0 = c0 + 7;
+    if (t0 < n) {  // thread (row t0 + ri, column group cg): columns t0 + cg, + 8, ... <= row
+      const int ri = tid >> 3, cg = tid & 7;
+      const int i = t0 + ri;
+      if (i < n) {
+        double li[7];
+#pragma unroll
+        for (int c = 0; c < 7; c++) li[c] = sA[(c0 + c) * n + i];
+        for (int j = t0 + cg; j <= i; j += 8) {
+          double a = sA[i * n + j];
+#pragma unroll
+          for (int c = 0; c < 7; c++) a -= li[c] * sA[(c0 + c) * n + j];
+          sA[i * n + j] = a;
+        }
+      }
+    }
+    __syncthreads();
   }
 
   M3S_GS(3)
   // 4) L y = b, Lᵀ x = y by wave 0, rows i = lane + 64 t in registers (t < 2: n <= 128);
   //    the solved unknown goes to every lane by v_readlane (the owner lane is uniform)
   if (wv == 0 && !fail) {
-    auto bcast = [](double v, int l) {
-      const uint64_t u = __builtin_bit_cast(uint64_t, v);
-      const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, l);
-      const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
-      return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
-    };
     double x0 = lane < n ? sb[lane] : 0.0, x1 = lane + 64 < n ? sb[lane + 64] : 0.0;
     for (int j = 0; j < n; j++) {
       const int owner = j & 63;
