@@ -89,6 +89,24 @@ def test_gn_lds_solve_equals_global_solve(dev, P):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+def test_gn_invalid_matches_ignore_their_index(dev):
+    """The edge pass packs the match index with the validity folded in (-1 where invalid,
+    `gn_pack_kernel`): an invalid match's index is never read, whatever it holds — the
+    reference's `valid ? idx : 0`.  Garbage indices (negative, past N) under invalid
+    matches give the same poses, bit for bit, as zeros there."""
+    import mast3r_slam_backends as mb
+    g = syn.keyframe_graph(P=6, h=24, w=32, seed=31)
+    outs = []
+    for fill in (0, -7, 10 ** 9):
+        Twc, Xs, Cs, ii, jj, idx, valid, Q = _gn_case(g, dev)
+        idx = torch.where(valid[..., 0], idx, torch.full_like(idx, fill))
+        (dx,) = mb.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx.contiguous(), valid, Q, 0.003,
+                                     10.0, 0.0, 1.5, 4, 1e-8)
+        outs.append((Twc.cpu(), dx.cpu()))
+    for t, d in outs[1:]:
+        assert torch.equal(t, outs[0][0]) and torch.equal(d, outs[0][1])
+
+
 def test_gn_points_parity(oracle, dev):
     import mast3r_slam_backends as mb
     g = syn.keyframe_graph(P=4, h=48, w=64, seed=3)
