@@ -586,92 +586,41 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_kernel(
 // The system is small (P = 16 keyframes: n = 105, 88 KB of f64), so it lives in LDS for
 // the whole solve instead of in global memory, and the per-edge serial assembly loop of
 // gn_solve_kernel (four barriers and global read-modify-writes per edge) becomes:
-//  * per edge, in parallel over the workgroup's 16 waves: the f64 reduction of its S
-//    partials (or its all-gathered G row), M (apply_Sim3_adj_inv of pose i), A = M G Mᵀ and
-//    v = M v' — the same operations in the same order as gn_solve_kernel — written to EB;
-//  * assembly by ownership: each matrix entry is owned by one thread, which adds the
-//    contributions of the edges touching its 7x7 block in edge order (per-block lists built
-//    once per solve by gn_lists_kernel) — the same additions in the same order as the serial
-//    loop, so the system, and everything after it, is bit-identical;
-//  * right-looking Cholesky in LDS (one barrier per phase), the two triangular solves by
-//    one wave with the right-hand side in registers (no barriers), retraction and the
+//  * M of every pose once (apply_Sim3_adj_inv, f64), then per edge, in parallel over the
+//    workgroup's 16 waves: the f64 reduction of its S partials (or its all-gathered G row;
+//    the partials of four edges in flight at once), A = M G Mᵀ and v = M v' — the same
+//    operations in the same order as gn_solve_kernel — written to EB;
+//  * assembly by block row: wave w owns the system rows of pose w (+ 16, ...), walks the
+//    edges in order, takes those touching its pose by ballot and applies their blocks
+//    (Hii += A, Hij -= A, Hji -= A, Hjj += A; b_i -= v, b_j += v) — each entry's lane adds
+//    the same contributions in the same order as the serial loop, so the system, and
+//    everything after it, is bit-identical;
+//  * blocked right-looking Cholesky in LDS (two barriers per 7-column panel), the two
+//    triangular solves by one wave with the right-hand side in registers (no barriers,
+//    each panel's operands read ahead of its dependent chain), retraction and the
 //    convergence test as before.
 constexpr int kLdsN = 126;            // P <= 19
 constexpr int kEB = 56;               // per edge: A (49) then v (7), f64
 
-// Contribution lists of a solve (edges touching each 7x7 block, in the serial loop's
-// order).  blk_start [(P-1)^2 + 1], blk_list [4E] (e << 2 | kind; kind 0: +A (Hii), 1: -A
-// (Hij), 2: -A (Hji), 3: +A (Hjj)); vec_start [P], vec_list [2E] (e << 1 | 0: -v at pose i,
-// 1: +v at pose j).  Indices are those of the system (pose rank - 1; rank 0 is fixed).
-__global__ __launch_bounds__(kSolveThreads) void gn_lists_kernel(
-    const int* __restrict__ rank_ii, const int* __restrict__ rank_jj, int E, int P,
-    int* __restrict__ blk_start, int* __restrict__ blk_list, int* __restrict__ vec_start,
-    int* __restrict__ vec_list) {
-  const int np = P - 1, nb = np * np;
-  __shared__ int cnt[kLdsN / 7 * kLdsN / 7 + 1];
-  __shared__ int vcnt[kLdsN / 7 + 1];
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-    const int bi = b / np, bj = b % np;
-    int c = 0;
-    for (int e = 0; e < E; e++) {
-      const int oi = rank_ii[e] - 1, oj = rank_jj[e] - 1;
-      c += (oi >= 0 && bi == oi && bj == oi) + (oi >= 0 && oj >= 0 && bi == oi && bj == oj) +
-           (oi >= 0 && oj >= 0 && bi == oj && bj == oi) + (oj >= 0 && bi == oj && bj == oj);
-    }
-    cnt[b] = c;
-  }
-  for (int p = threadIdx.x; p < np; p += blockDim.x) {
-    int c = 0;
-    for (int e = 0; e < E; e++) c += (rank_ii[e] - 1 == p) + (rank_jj[e] - 1 == p);
-    vcnt[p] = c;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {  // exclusive scans (<= 324 + 18 entries)
-    int a = 0;
-    for (int b = 0; b < nb; b++) {
-      blk_start[b] = a;
-      a += cnt[b];
-    }
-    blk_start[nb] = a;
-    a = 0;
-    for (int p = 0; p < np; p++) {
-      vec_start[p] = a;
-      a += vcnt[p];
-    }
-    vec_start[np] = a;
-  }
-  __syncthreads();
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-    const int bi = b / np, bj = b % np;
-    int w = blk_start[b];
-    for (int e = 0; e < E; e++) {
-      const int oi = rank_ii[e] - 1, oj = rank_jj[e] - 1;
-      if (oi >= 0 && bi == oi && bj == oi) blk_list[w++] = e << 2 | 0;
-      if (oi >= 0 && oj >= 0 && bi == oi && bj == oj) blk_list[w++] = e << 2 | 1;
-      if (oi >= 0 && oj >= 0 && bi == oj && bj == oi) blk_list[w++] = e << 2 | 2;
-      if (oj >= 0 && bi == oj && bj == oj) blk_list[w++] = e << 2 | 3;
-    }
-  }
-  for (int p = threadIdx.x; p < np; p += blockDim.x) {
-    int w = vec_start[p];
-    for (int e = 0; e < E; e++) {
-      if (rank_ii[e] - 1 == p) vec_list[w++] = e << 1 | 0;
-      if (rank_jj[e] - 1 == p) vec_list[w++] = e << 1 | 1;
-    }
-  }
-}
-
 // LDS written by some lanes of a wave, then read by others of the same wave: wait for the
-// writes and keep the compiler from moving accesses across (wave-scope fence)
+// writes and keep the compiler from moving accesses across (wave-scope fence on LDS only —
+// a fence over all address spaces also waits for the wave's global stores)
 __device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
 }
 
-struct LdsLists {
-  const int *blk_start, *blk_list, *vec_start, *vec_list;
-};
+// keep a value in registers at this point: loads issued ahead of a dependent chain are not
+// sunk by the compiler into the conditional updates that use them
+__device__ __forceinline__ void pin_vgpr(double& v) { asm volatile("" : "+v"(v)); }
+
+__device__ __forceinline__ double bcast_f64(double v, int l) {  // v of lane l, l uniform
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
 
 #ifdef M3S_GN_STAMPS
 // debug build (tools/gn_stamps.py): thread 0 of the LDS solve, s_memrealtime (100 MHz) at
@@ -686,49 +635,28 @@ __device__ long long g_gn_stamps[16 * 8];
 
 __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
     float* __restrict__ Twc, const float* __restrict__ partial, const int* __restrict__ rank_ii,
-    double* __restrict__ EB, LdsLists lists, float* __restrict__ dx_out,
+    const int* __restrict__ rank_jj, double* __restrict__ EB, float* __restrict__ dx_out,
     int* __restrict__ flags, int E, int S, int P, float delta_thresh,
     const double* __restrict__ G_in) {
   if (flags[0]) return;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar edge indexing
   const int n = 7 * (P - 1);
   const int nt = blockDim.x;
   M3S_GS(0)
   constexpr int NW = kSolveThreads / 64;
   __shared__ double sA[kLdsN * kLdsN];
   __shared__ double sb[kLdsN];
-  __shared__ double sW[NW][4][49];      // per wave: M, G, T (A reuses G), v' / v
+  __shared__ double sW[NW][3][49];      // per wave: G, T, v'
   __shared__ double sR[kLdsN];          // 1 / L[k][k]
   __shared__ float s_red[NW];
 
-  // 1) per edge (wave w: edges w, w + NW, ...): G → M, T = M G, A = T Mᵀ, v = M v'
-  double (*M)[7] = reinterpret_cast<double(*)[7]>(sW[wv][0]);
-  double (*Gm)[7] = reinterpret_cast<double(*)[7]>(sW[wv][1]);
-  double (*T)[7] = reinterpret_cast<double(*)[7]>(sW[wv][2]);
-  double* vp = sW[wv][3];
-  for (int e = wv; e < E; e += NW) {
-    const int ix = rank_ii[e];
-    // the edge's 35 sums (the f64 reduction of gn_solve_kernel step 1, same order)
-    double g = 0.0;
-    if (lane < kAcc) {
-      if (G_in) {
-        g = G_in[e * kAcc + lane];
-      } else {
-        for (int s = 0; s < S; s++) g += (double)partial[((int64_t)e * S + s) * kAcc + lane];
-      }
-    }
-    // lanes 0..27: the packed upper triangle → symmetric G; 28..34: v'
-    if (lane < 28) {
-      int r = 0;
-      while ((r + 1) * (r + 2) / 2 <= lane) r++;
-      const int c = lane - r * (r + 1) / 2;
-      Gm[r][c] = g;
-      Gm[c][r] = g;
-    } else if (lane < kAcc) {
-      vp[lane - 28] = g;
-    }
+  // 1a) M of every pose (column `lane` = M applied to the unit vector e_lane), into sA,
+  //     which is free until the assembly
+  double* sM = sA;  // [P][7][7], P * 49 <= kLdsN^2
+  for (int p = wv; p < P; p += NW) {
     if (lane < 7) {
-      const float* Ti = Twc + 8 * ix;
+      const float* Ti = Twc + 8 * p;
       const double t[3] = {Ti[0], Ti[1], Ti[2]};
       const double q[4] = {Ti[3], Ti[4], Ti[5], Ti[6]};
       const double s = Ti[7];
@@ -736,86 +664,150 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
       X[lane] = 1.0;
       double Y[7];
       m3s_adj_inv_apply<double>(t, q, s, X, Y);
-      for (int r = 0; r < 7; r++) M[r][lane] = Y[r];
+      for (int r = 0; r < 7; r++) sM[p * 49 + r * 7 + lane] = Y[r];
     }
-    wave_lds_sync();                             // this wave's scratch writes visible
-    double* out = EB + (int64_t)e * kEB;
-    if (lane < 49) {  // T = M G
-      const int r = lane / 7, c = lane % 7;
-      double v = 0.0;
-      for (int k = 0; k < 7; k++) v += M[r][k] * Gm[k][c];
-      T[r][c] = v;
+  }
+  __syncthreads();
+  M3S_GS(6)
+
+  // 1b) per edge (wave w: edges w, w + NW, ...): the 35 sums (the f64 reduction of
+  //     gn_solve_kernel step 1, same order), T = M G, A = T Mᵀ, v = M v'
+  double (*Gm)[7] = reinterpret_cast<double(*)[7]>(sW[wv][0]);
+  double (*T)[7] = reinterpret_cast<double(*)[7]>(sW[wv][1]);
+  double* vp = sW[wv][2];
+  constexpr int CE = 4, CS = 8;  // edges per batch; partials per edge in flight
+  for (int k0 = 0; wv + NW * k0 < E; k0 += CE) {
+    double g[CE];
+    int ri[CE];
+#pragma unroll
+    for (int u = 0; u < CE; u++) {
+      g[u] = 0.0;
+      ri[u] = __builtin_amdgcn_readfirstlane(rank_ii[min(wv + NW * (k0 + u), E - 1)]);
     }
-    double vj = 0.0;
-    if (lane >= 56 && lane < 63) {  // vj = M v'
-      const int r = lane - 56;
-      for (int k = 0; k < 7; k++) vj += M[r][k] * vp[k];
+    if (G_in) {
+#pragma unroll
+      for (int u = 0; u < CE; u++) {
+        const int e = wv + NW * (k0 + u);
+        if (lane < kAcc && e < E) g[u] = G_in[e * kAcc + lane];
+      }
+    } else {
+      // unconditional loads (indices clamped into range; what they fetch beyond the edge's
+      // partials is not added): guarded loads became one branch and memory wait each
+      const int lc = lane < kAcc ? lane : kAcc - 1;
+      for (int s0 = 0; s0 < S; s0 += CS) {
+        float pv[CE][CS];
+#pragma unroll
+        for (int u = 0; u < CE; u++) {
+          const int e = min(wv + NW * (k0 + u), E - 1);
+#pragma unroll
+          for (int t = 0; t < CS; t++)
+            pv[u][t] = partial[((int64_t)e * S + min(s0 + t, S - 1)) * kAcc + lc];
+        }
+#pragma unroll
+        for (int u = 0; u < CE; u++)
+#pragma unroll
+          for (int t = 0; t < CS; t++)
+            if (s0 + t < S) g[u] += (double)pv[u][t];
+      }
     }
-    wave_lds_sync();
-    if (lane < 49) {  // A = T Mᵀ
-      const int r = lane / 7, c = lane % 7;
-      double v = 0.0;
-      for (int k = 0; k < 7; k++) v += T[r][k] * M[c][k];
-      out[lane] = v;
-    } else if (lane >= 56 && lane < 63) {
-      out[49 + lane - 56] = vj;
+#pragma unroll
+    for (int u = 0; u < CE; u++) {
+      const int e = wv + NW * (k0 + u);
+      if (e >= E) break;
+      const double* M = sM + 49 * ri[u];
+      // lanes 0..27: the packed upper triangle → symmetric G; 28..34: v'
+      if (lane < 28) {
+        int r = 0;
+        while ((r + 1) * (r + 2) / 2 <= lane) r++;
+        const int c = lane - r * (r + 1) / 2;
+        Gm[r][c] = g[u];
+        Gm[c][r] = g[u];
+      } else if (lane < kAcc) {
+        vp[lane - 28] = g[u];
+      }
+      wave_lds_sync();                           // this wave's scratch writes visible
+      double* out = EB + (int64_t)e * kEB;
+      if (lane < 49) {  // T = M G
+        const int r = lane / 7, c = lane % 7;
+        double v = 0.0;
+        for (int k = 0; k < 7; k++) v += M[r * 7 + k] * Gm[k][c];
+        T[r][c] = v;
+      }
+      double vj = 0.0;
+      if (lane >= 56 && lane < 63) {  // vj = M v'
+        const int r = lane - 56;
+        for (int k = 0; k < 7; k++) vj += M[r * 7 + k] * vp[k];
+      }
+      wave_lds_sync();
+      if (lane < 49) {  // A = T Mᵀ
+        const int r = lane / 7, c = lane % 7;
+        double v = 0.0;
+        for (int k = 0; k < 7; k++) v += T[r][k] * M[c * 7 + k];
+        out[lane] = v;
+      } else if (lane >= 56 && lane < 63) {
+        out[49 + lane - 56] = vj;
+      }
+      wave_lds_sync();                           // scratch reused by the next edge
     }
-    wave_lds_sync();                             // scratch reused by the next edge
+    if (k0 == 0) { M3S_GS(7) }
   }
   __threadfence_block();
   __syncthreads();
   M3S_GS(1)
 
-  // 2) assembly by ownership, contributions in the serial loop's order; each owner fetches
-  //    its contribution list 8 entries at a time (codes, then the 8 EB values, then the
-  //    additions in order): two memory round trips per 8 contributions, not per one — a
-  //    diagonal block collects one contribution per edge at its pose (~16 at P = 16)
-  constexpr int CH = 8;
+  // 2) assembly by block row (see above): lane (r, c) < 49 owns entry (7 bi + r, 7 bj + c)
+  //    of every block of the row, lanes 49..55 b[7 bi + r]; up to 8 touching edges' EB rows
+  //    fetched per round trip, applied in edge order
   const int np = P - 1;
-  for (int idx = tid; idx < n * n; idx += nt) {
-    const int row = idx / n, col = idx - row * n;
-    const int bi = row / 7, r = row - 7 * bi, bj = col / 7, c = col - 7 * bj;
-    const int b = bi * np + bj;
-    const int k0 = lists.blk_start[b], k1 = lists.blk_start[b + 1];
-    double a = 0.0;
-    for (int kb = k0; kb < k1; kb += CH) {
-      int code[CH];
-      double v[CH];
+  for (int bi = wv; bi < np; bi += NW) {
+    double* rowA = sA + 7 * bi * n;
+    for (int x = lane; x < 7 * n; x += 64) rowA[x] = 0.0;
+    if (lane < 7) sb[7 * bi + lane] = 0.0;
+    wave_lds_sync();
+    double* ent = lane < 49 ? rowA + (lane / 7) * n + lane % 7 : nullptr;
+    for (int kb = 0; kb < E; kb += 64) {
+      const int e_l = kb + lane;
+      const int oi_l = e_l < E ? rank_ii[e_l] - 1 : -2;
+      const int oj_l = e_l < E ? rank_jj[e_l] - 1 : -2;
+      uint64_t mask = __ballot(oi_l == bi || oj_l == bi);
+      while (mask) {
+        constexpr int CB = 8;
+        int eu[CB], oiu[CB], oju[CB];
+        double v[CB];
 #pragma unroll
-      for (int u = 0; u < CH; u++) code[u] = kb + u < k1 ? lists.blk_list[kb + u] : 0;
+        for (int u = 0; u < CB; u++) {
+          eu[u] = -1;
+          if (mask) {
+            const int bit = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            eu[u] = kb + bit;
+            oiu[u] = __builtin_amdgcn_readlane(oi_l, bit);
+            oju[u] = __builtin_amdgcn_readlane(oj_l, bit);
+          }
+        }
 #pragma unroll
-      for (int u = 0; u < CH; u++)
-        v[u] = kb + u < k1 ? EB[(int64_t)(code[u] >> 2) * kEB + r * 7 + c] : 0.0;
+        for (int u = 0; u < CB; u++)  // unconditional (clamped) loads, all in flight
+          v[u] = EB[(int64_t)max(eu[u], 0) * kEB + min(lane, kEB - 1)];
 #pragma unroll
-      for (int u = 0; u < CH; u++) {
-        if (kb + u >= k1) break;
-        const int kind = code[u] & 3;
-        if (kind == 0 || kind == 3) a += v[u];
-        else a -= v[u];
+        for (int u = 0; u < CB; u++) {
+          if (eu[u] < 0) break;
+          const int oi = oiu[u], oj = oju[u];
+          if (lane < 49) {
+            if (oi == bi) {
+              ent[7 * oi] += v[u];                 // Hii += A
+              if (oj >= 0) ent[7 * oj] -= v[u];    // Hij -= A
+            }
+            if (oj == bi) {
+              if (oi >= 0) ent[7 * oi] -= v[u];    // Hji -= A
+              ent[7 * oj] += v[u];                 // Hjj += A
+            }
+          } else if (lane < kEB) {
+            if (oi == bi) sb[7 * bi + lane - 49] -= v[u];
+            if (oj == bi) sb[7 * bi + lane - 49] += v[u];
+          }
+        }
       }
     }
-    sA[idx] = a;
-  }
-  for (int row = tid; row < n; row += nt) {
-    const int p = row / 7, r = row - 7 * p;
-    const int k0 = lists.vec_start[p], k1 = lists.vec_start[p + 1];
-    double bv = 0.0;
-    for (int kb = k0; kb < k1; kb += CH) {
-      int code[CH];
-      double v[CH];
-#pragma unroll
-      for (int u = 0; u < CH; u++) code[u] = kb + u < k1 ? lists.vec_list[kb + u] : 0;
-#pragma unroll
-      for (int u = 0; u < CH; u++)
-        v[u] = kb + u < k1 ? EB[(int64_t)(code[u] >> 1) * kEB + 49 + r] : 0.0;
-#pragma unroll
-      for (int u = 0; u < CH; u++) {
-        if (kb + u >= k1) break;
-        if (code[u] & 1) bv += v[u];
-        else bv -= v[u];
-      }
-    }
-    sb[row] = bv;
   }
   __syncthreads();
   M3S_GS(2)
@@ -824,17 +816,11 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
   //    panel (instead of one per column).  Wave 0 factors the panel with its rows in
   //    registers (row c0 + lane + 64 t; the pivot row and L[j][k] of the panel's rows come
   //    from lanes 0..6 by v_readlane), then every thread applies the panel to its entries
-  //    (i, j) of the trailing triangle, the seven updates in column order.  Each entry
-  //    receives the unblocked algorithm's operations in the same order (A[i][j] -= L[i][k]
-  //    L[j][k], k increasing; L[i][k] = A[i][k] · (1 / √A[k][k])), so the factor — and the
-  //    poses — are bit-identical to gn_solve_kernel's.  L[., k] goes to the unused upper
-  //    triangle (L[i][k] = sA[k n + i]), 1 / L[k][k] to sR[k].
-  auto bcast = [](double v, int l) {
-    const uint64_t u = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, l);
-    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
-    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
-  };
+  //    (i, j) of the trailing triangle, the seven updates in column order, two entries at a
+  //    time.  Each entry receives the unblocked algorithm's operations in the same order
+  //    (A[i][j] -= L[i][k] L[j][k], k increasing; L[i][k] = A[i][k] · (1 / √A[k][k])), so
+  //    the factor — and the poses — are bit-identical to gn_solve_kernel's.  L[., k] goes
+  //    to the unused upper triangle (L[i][k] = sA[k n + i]), 1 / L[k][k] to sR[k].
   __shared__ int s_fail;
   bool fail = false;
   if (tid == 0) s_fail = 0;
@@ -852,7 +838,7 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
 #pragma unroll
       for (int c = 0; c < 7; c++) {
         const int k = c0 + c;
-        const double d = bcast(a0[c], c);             // A[k][k]: row k is lane c
+        const double d = bcast_f64(a0[c], c);         // A[k][k]: row k is lane c
         if (!(d > 0.0)) {
           f = true;
           break;
@@ -864,7 +850,7 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
         if (lane == 0) sR[k] = rpiv;
 #pragma unroll
         for (int c2 = c + 1; c2 < 7; c2++) {
-          const double lj = bcast(l0, c2);            // L[c0 + c2][k]
+          const double lj = bcast_f64(l0, c2);        // L[c0 + c2][k]
           if (i0 >= c0 + c2) a0[c2] -= l0 * lj;
           if (i1 >= c0 + c2) a1[c2] -= l1 * lj;
         }
@@ -884,7 +870,24 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
         double li[7];
 #pragma unroll
         for (int c = 0; c < 7; c++) li[c] = sA[(c0 + c) * n + i];
-        for (int j = t0 + cg; j <= i; j += 8) {
+        int j = t0 + cg;
+        for (; j + 8 <= i; j += 16) {  // entries j and j + 8: two independent chains
+          double a = sA[i * n + j], a8 = sA[i * n + j + 8];
+          double lj[7], lj8[7];
+#pragma unroll
+          for (int c = 0; c < 7; c++) {
+            lj[c] = sA[(c0 + c) * n + j];
+            lj8[c] = sA[(c0 + c) * n + j + 8];
+          }
+#pragma unroll
+          for (int c = 0; c < 7; c++) {
+            a -= li[c] * lj[c];
+            a8 -= li[c] * lj8[c];
+          }
+          sA[i * n + j] = a;
+          sA[i * n + j + 8] = a8;
+        }
+        if (j <= i) {
           double a = sA[i * n + j];
 #pragma unroll
           for (int c = 0; c < 7; c++) a -= li[c] * sA[(c0 + c) * n + j];
@@ -897,32 +900,109 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
 
   M3S_GS(3)
   // 4) L y = b, Lᵀ x = y by wave 0, rows i = lane + 64 t in registers (t < 2: n <= 128);
-  //    the solved unknown goes to every lane by v_readlane (the owner lane is uniform)
+  //    the solved unknown goes to every lane by v_readlane (the owner lane is uniform).  The
+  //    unknowns of rows < 64 and >= 64 are swept by separate loops, so the owner's register
+  //    is known at compile time (a select between the two was on every step's dependent
+  //    chain), and each group of 8 steps reads its columns of L and 1 / L[j][j] (clamped,
+  //    unconditional LDS loads; masked lanes do not use them) ahead of its chain; the masked
+  //    updates are selects, so the compiler does not sink those loads into branches.
   if (wv == 0 && !fail) {
+    constexpr int G8 = 8;
+    const int lc = min(lane, n - 1), lc1 = min(lane + 64, n - 1), n0 = min(n, 64);
     double x0 = lane < n ? sb[lane] : 0.0, x1 = lane + 64 < n ? sb[lane + 64] : 0.0;
-    for (int j = 0; j < n; j++) {
-      const int owner = j & 63;
-      const double c0 = lane > j && lane < n ? sA[j * n + lane] : 0.0;
-      const double c1 = lane + 64 > j && lane + 64 < n ? sA[j * n + lane + 64] : 0.0;
-      const double yj = bcast((j < 64 ? x0 : x1) * sR[j], owner);
-      if (lane == owner) {
-        if (j < 64) x0 = yj;
-        else x1 = yj;
+    for (int jb = 0; jb < n0; jb += G8) {       // forward, unknowns j < 64 (x0 of lane j)
+      double c0[G8], c1[G8], rr[G8];
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = min(jb + u, n - 1);
+        c0[u] = sA[j * n + lc];
+        c1[u] = sA[j * n + lc1];
+        rr[u] = sR[j];
       }
-      if (lane > j && lane < n) x0 -= c0 * yj;
-      if (lane + 64 > j && lane + 64 < n) x1 -= c1 * yj;
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        pin_vgpr(c0[u]);
+        pin_vgpr(c1[u]);
+        pin_vgpr(rr[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = jb + u;
+        if (j >= n0) break;
+        const double yj = bcast_f64(x0 * rr[u], j);
+        if (lane == j) x0 = yj;
+        x0 = lane > j && lane < n ? x0 - c0[u] * yj : x0;
+        x1 = lane + 64 < n ? x1 - c1[u] * yj : x1;
+      }
     }
-    for (int j = n - 1; j >= 0; j--) {
-      const int owner = j & 63;
-      const double c0 = lane < j ? sA[lane * n + j] : 0.0;
-      const double c1 = lane + 64 < j ? sA[(lane + 64) * n + j] : 0.0;
-      const double xj = bcast((j < 64 ? x0 : x1) * sR[j], owner);
-      if (lane == owner) {
-        if (j < 64) x0 = xj;
-        else x1 = xj;
+    for (int jb = 64; jb < n; jb += G8) {       // forward, unknowns j >= 64 (x1 of lane j - 64)
+      double c1[G8], rr[G8];
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = min(jb + u, n - 1);
+        c1[u] = sA[j * n + lc1];
+        rr[u] = sR[j];
       }
-      if (lane < j) x0 -= c0 * xj;
-      if (lane + 64 < j) x1 -= c1 * xj;
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        pin_vgpr(c1[u]);
+        pin_vgpr(rr[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = jb + u;
+        if (j >= n) break;
+        const double yj = bcast_f64(x1 * rr[u], j - 64);
+        if (lane == j - 64) x1 = yj;
+        x1 = lane + 64 > j && lane + 64 < n ? x1 - c1[u] * yj : x1;
+      }
+    }
+    for (int jt = n - 1; jt >= 64; jt -= G8) {  // backward, unknowns j >= 64
+      double c0[G8], c1[G8], rr[G8];
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = max(jt - u, 0);
+        c0[u] = sA[lc * n + j];
+        c1[u] = sA[lc1 * n + j];
+        rr[u] = sR[j];
+      }
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        pin_vgpr(c0[u]);
+        pin_vgpr(c1[u]);
+        pin_vgpr(rr[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = jt - u;
+        if (j < 64) break;
+        const double xj = bcast_f64(x1 * rr[u], j - 64);
+        if (lane == j - 64) x1 = xj;
+        x0 = lane < j ? x0 - c0[u] * xj : x0;
+        x1 = lane + 64 < j ? x1 - c1[u] * xj : x1;
+      }
+    }
+    for (int jt = n0 - 1; jt >= 0; jt -= G8) {  // backward, unknowns j < 64
+      double c0[G8], rr[G8];
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = max(jt - u, 0);
+        c0[u] = sA[lc * n + j];
+        rr[u] = sR[j];
+      }
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        pin_vgpr(c0[u]);
+        pin_vgpr(rr[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = jt - u;
+        if (j < 0) break;
+        const double xj = bcast_f64(x0 * rr[u], j);
+        if (lane == j) x0 = xj;
+        x0 = lane < j ? x0 - c0[u] * xj : x0;
+      }
     }
     if (lane < n) sb[lane] = x0;
     if (lane + 64 < n) sb[lane + 64] = x1;
@@ -977,25 +1057,14 @@ int choose_splits(int64_t E, int64_t N) {
 }
 
 struct Layout {
-  size_t flags, rank_ii, rank_jj, order, xc, mi, partial, A, b, G, EB, blk_start, blk_list,
-      vec_start, vec_list, total;
+  size_t flags, rank_ii, rank_jj, order, xc, mi, partial, A, b, G, EB, total;
 };
 
-// the LDS solve's regions (EB, contribution lists) appended at `off`
+// the LDS solve's per-edge blocks (EB) appended at `off`
 template <class L>
-size_t lds_regions(L& l, size_t off, int64_t P, int64_t E) {
-  const int64_t np = P > 1 ? P - 1 : 0;
+size_t lds_regions(L& l, size_t off, int64_t E) {
   l.EB = off;
-  off = align_up(off + 8 * kEB * E, 256);
-  l.blk_start = off;
-  off = align_up(off + 4 * (np * np + 1), 256);
-  l.blk_list = off;
-  off = align_up(off + 4 * 4 * E, 256);
-  l.vec_start = off;
-  off = align_up(off + 4 * (np + 1), 256);
-  l.vec_list = off;
-  off = align_up(off + 4 * 2 * E, 256);
-  return off;
+  return align_up(off + 8 * kEB * E, 256);
 }
 
 Layout make_layout(int64_t P, int64_t E, int S, int64_t N) {
@@ -1022,32 +1091,12 @@ Layout make_layout(int64_t P, int64_t E, int S, int64_t N) {
   off = align_up(off + 8 * n, 256);
   L.G = off;
   off = align_up(off + 8 * E * kAcc, 256);
-  L.total = lds_regions(L, off, P, E);
+  L.total = lds_regions(L, off, E);
   return L;
 }
 
 bool g_force_global_solve = false;   // m3s_gn_force_global_solve (diagnostic)
 bool use_lds_solve(int64_t P) { return P > 1 && 7 * (P - 1) <= kLdsN && !g_force_global_solve; }
-
-template <class L>
-LdsLists lds_lists(char* ws, const L& l) {
-  return LdsLists{reinterpret_cast<const int*>(ws + l.blk_start),
-                  reinterpret_cast<const int*>(ws + l.blk_list),
-                  reinterpret_cast<const int*>(ws + l.vec_start),
-                  reinterpret_cast<const int*>(ws + l.vec_list)};
-}
-
-template <class L>
-int launch_lists(char* ws, const L& l, const int* rii, const int* rjj, int64_t E, int64_t P,
-                 hipStream_t st) {
-  hipLaunchKernelGGL(gn_lists_kernel, dim3(1), dim3(kSolveThreads), 0, st, rii, rjj, (int)E,
-                     (int)P, reinterpret_cast<int*>(ws + l.blk_start),
-                     reinterpret_cast<int*>(ws + l.blk_list),
-                     reinterpret_cast<int*>(ws + l.vec_start),
-                     reinterpret_cast<int*>(ws + l.vec_list));
-  M3S_LAUNCH_CHECK();
-  return M3S_OK;
-}
 
 template <int MODE>
 int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
@@ -1086,10 +1135,6 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
                      P * N, E * N, XC, MI, flags);
   M3S_LAUNCH_CHECK();
   const bool lds = use_lds_solve(P);
-  if (lds) {
-    const int st_l = launch_lists(ws, L, rii, rjj, E, P, st);
-    if (st_l != M3S_OK) return st_l;
-  }
   if (P > 1) {
     for (int it = 0; it < max_iter; it++) {
       hipLaunchKernelGGL(gn_edge_kernel<MODE>, dim3((unsigned)(E * S)), dim3(kEdgeThreads), 0,
@@ -1098,8 +1143,8 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
       M3S_LAUNCH_CHECK();
       if (lds)
         hipLaunchKernelGGL(gn_solve_lds_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_Twc,
-                           partial, rii, reinterpret_cast<double*>(ws + L.EB), lds_lists(ws, L),
-                           d_dx, flags, (int)E, S, (int)P, delta_thresh, nullptr);
+                           partial, rii, rjj, reinterpret_cast<double*>(ws + L.EB), d_dx,
+                           flags, (int)E, S, (int)P, delta_thresh, nullptr);
       else
         hipLaunchKernelGGL(gn_solve_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_Twc, partial,
                            rii, rjj, A, b, G, d_dx, flags, (int)E, S, (int)P, delta_thresh,
@@ -1122,8 +1167,7 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
 // edges, the dense system.  S comes from E_total, so every edge's partials — hence its G
 // row — are those of the unsharded m3s_gauss_newton_* call, bit for bit.
 struct ShardLayout {
-  size_t flags, rank_ii, rank_jj, order, xc, mi, partial, A, b, EB, blk_start, blk_list,
-      vec_start, vec_list, total;
+  size_t flags, rank_ii, rank_jj, order, xc, mi, partial, A, b, EB, total;
   int S;
 };
 
@@ -1150,7 +1194,7 @@ ShardLayout make_shard_layout(int64_t P, int64_t E_total, int64_t E_local, int64
   off = align_up(off + 8 * n * n, 256);
   L.b = off;
   off = align_up(off + 8 * (n > 0 ? n : 1), 256);
-  L.total = lds_regions(L, off, P, E_total);
+  L.total = lds_regions(L, off, E_total);
   return L;
 }
 
@@ -1232,9 +1276,6 @@ extern "C" int m3s_gn_sharded_begin(const int64_t* d_ii, const int64_t* d_jj, in
                      reinterpret_cast<int*>(ws + L.rank_ii), reinterpret_cast<int*>(ws + L.rank_jj),
                      reinterpret_cast<int*>(ws + L.flags));
   M3S_LAUNCH_CHECK();
-  if (use_lds_solve(P))
-    return launch_lists(ws, L, reinterpret_cast<const int*>(ws + L.rank_ii),
-                        reinterpret_cast<const int*>(ws + L.rank_jj), E, P, st);
   return M3S_OK;
 }
 
@@ -1288,7 +1329,8 @@ extern "C" int m3s_gn_solve_step(float* d_Twc, const double* d_G, int64_t num_po
   if (use_lds_solve(P)) {
     hipLaunchKernelGGL(gn_solve_lds_kernel, dim3(1), dim3(kSolveThreads), 0, m3s_stream(stream),
                        d_Twc, nullptr, reinterpret_cast<const int*>(ws + L.rank_ii),
-                       reinterpret_cast<double*>(ws + L.EB), lds_lists(ws, L), d_dx,
+                       reinterpret_cast<const int*>(ws + L.rank_jj),
+                       reinterpret_cast<double*>(ws + L.EB), d_dx,
                        reinterpret_cast<int*>(ws + L.flags), (int)E, L.S, (int)P, delta_thresh,
                        d_G);
     M3S_LAUNCH_CHECK();

@@ -92,4 +92,6 @@ for dbg_path in paths:
         d = np.diff(st[it, :6])
         print(f"  iteration {it}: " + " ".join(f"{n} {v:7.2f}" for n, v in zip(names, d))
               + f" | solve kernel {st[it, 5] - st[it, 0]:7.2f} us"
-              + f" | to next solve {st[it + 1, 0] - st[it, 5]:7.2f}", flush=True)
+              + f" | to next solve {st[it + 1, 0] - st[it, 5]:7.2f}"
+              + (f" | M of poses {st[it, 6] - st[it, 0]:6.2f}, first edge batch "
+                 f"{st[it, 7] - st[it, 6]:6.2f}" if st[it, 7] > 0 else ""), flush=True)
