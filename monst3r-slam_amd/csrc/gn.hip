@@ -647,9 +647,25 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
   constexpr int NW = kSolveThreads / 64;
   __shared__ double sA[kLdsN * kLdsN];
   __shared__ double sb[kLdsN];
-  __shared__ double sW[NW][3][49];      // per wave: G, T, v'
   __shared__ double sR[kLdsN];          // 1 / L[k][k]
   __shared__ float s_red[NW];
+
+  constexpr int CE = 4, CS = 8;  // edges per batch; partials per edge in flight
+  // unconditional loads (indices clamped into range; what they fetch beyond the edge's
+  // partials is not added): guarded loads became one branch and memory wait each.  The
+  // next batch's first partials are requested before this batch's edges are processed.
+  const int lc = lane < kAcc ? lane : kAcc - 1;
+  float pv[CE][CS];
+  auto load_partials = [&](int k0, int s0) {
+#pragma unroll
+    for (int u = 0; u < CE; u++) {
+      const int e = min(wv + NW * (k0 + u), E - 1);
+#pragma unroll
+      for (int t = 0; t < CS; t++)
+        pv[u][t] = partial[((int64_t)e * S + min(s0 + t, S - 1)) * kAcc + lc];
+    }
+  };
+  if (!G_in && wv < E) load_partials(0, 0);  // in flight during 1a
 
   // 1a) M of every pose (column `lane` = M applied to the unit vector e_lane), into sA,
   //     which is free until the assembly
@@ -672,17 +688,22 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
 
   // 1b) per edge (wave w: edges w, w + NW, ...): the 35 sums (the f64 reduction of
   //     gn_solve_kernel step 1, same order), T = M G, A = T Mᵀ, v = M v'
-  double (*Gm)[7] = reinterpret_cast<double(*)[7]>(sW[wv][0]);
-  double (*T)[7] = reinterpret_cast<double(*)[7]>(sW[wv][1]);
-  double* vp = sW[wv][2];
-  constexpr int CE = 4, CS = 8;  // edges per batch; partials per edge in flight
+  // per-wave scratch for two edges at a time, in sA past the poses' M: edge h's G at
+  // 147 h, T at 147 h + 49, v' at 147 h + 98
+  double* scr = sA + 1024 + wv * 294;  // P * 49 <= 1024; 1024 + 16 * 294 <= kLdsN^2
+  const bool tl = lane < 49, vl = lane >= 56 && lane < 63;  // T / A lanes; v lanes
+  const int r_l = tl ? lane / 7 : lane - 56, c_l = tl ? lane % 7 : 0;
+  // pose ranks of this wave's edges k0 .. k0 + 63 (its k-th edge is wv + NW k), one per lane,
+  // taken by v_readlane: no memory wait inside the loop (it would also wait for the prefetch)
+  int rank_l = 0;
   for (int k0 = 0; wv + NW * k0 < E; k0 += CE) {
+    if ((k0 & 63) == 0) rank_l = rank_ii[min(wv + NW * (k0 + lane), E - 1)];
     double g[CE];
     int ri[CE];
 #pragma unroll
     for (int u = 0; u < CE; u++) {
       g[u] = 0.0;
-      ri[u] = __builtin_amdgcn_readfirstlane(rank_ii[min(wv + NW * (k0 + u), E - 1)]);
+      ri[u] = __builtin_amdgcn_readlane(rank_l, (k0 & 63) + u);
     }
     if (G_in) {
 #pragma unroll
@@ -691,63 +712,69 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
         if (lane < kAcc && e < E) g[u] = G_in[e * kAcc + lane];
       }
     } else {
-      // unconditional loads (indices clamped into range; what they fetch beyond the edge's
-      // partials is not added): guarded loads became one branch and memory wait each
-      const int lc = lane < kAcc ? lane : kAcc - 1;
-      for (int s0 = 0; s0 < S; s0 += CS) {
-        float pv[CE][CS];
-#pragma unroll
-        for (int u = 0; u < CE; u++) {
-          const int e = min(wv + NW * (k0 + u), E - 1);
-#pragma unroll
-          for (int t = 0; t < CS; t++)
-            pv[u][t] = partial[((int64_t)e * S + min(s0 + t, S - 1)) * kAcc + lc];
-        }
+      for (int s0 = 0;;) {
 #pragma unroll
         for (int u = 0; u < CE; u++)
 #pragma unroll
           for (int t = 0; t < CS; t++)
             if (s0 + t < S) g[u] += (double)pv[u][t];
+        s0 += CS;
+        if (s0 >= S) break;
+        load_partials(k0, s0);
       }
+      if (wv + NW * (k0 + CE) < E) load_partials(k0 + CE, 0);
     }
+    // two edges per step, so the two dependent chains (T = M G, then A = T Mᵀ) of one
+    // overlap the other's; v = M v' runs on lanes 56..62 in the same instructions as T
 #pragma unroll
-    for (int u = 0; u < CE; u++) {
-      const int e = wv + NW * (k0 + u);
-      if (e >= E) break;
-      const double* M = sM + 49 * ri[u];
-      // lanes 0..27: the packed upper triangle → symmetric G; 28..34: v'
-      if (lane < 28) {
-        int r = 0;
-        while ((r + 1) * (r + 2) / 2 <= lane) r++;
-        const int c = lane - r * (r + 1) / 2;
-        Gm[r][c] = g[u];
-        Gm[c][r] = g[u];
-      } else if (lane < kAcc) {
-        vp[lane - 28] = g[u];
+    for (int u = 0; u < CE; u += 2) {
+      const int e0 = wv + NW * (k0 + u);
+      if (e0 >= E) break;
+      const bool two = e0 + NW < E;  // edge 1 is computed regardless, stored only if real
+#pragma unroll
+      for (int h = 0; h < 2; h++) {  // lanes 0..27: packed upper triangle → symmetric G
+        double* G = scr + 147 * h;
+        if (lane < 28) {
+          int r = 0;
+          while ((r + 1) * (r + 2) / 2 <= lane) r++;
+          const int c = lane - r * (r + 1) / 2;
+          G[r * 7 + c] = g[u + h];
+          G[c * 7 + r] = g[u + h];
+        } else if (lane < kAcc) {
+          G[98 + lane - 28] = g[u + h];  // v'
+        }
       }
       wave_lds_sync();                           // this wave's scratch writes visible
-      double* out = EB + (int64_t)e * kEB;
-      if (lane < 49) {  // T = M G
-        const int r = lane / 7, c = lane % 7;
-        double v = 0.0;
-        for (int k = 0; k < 7; k++) v += M[r * 7 + k] * Gm[k][c];
-        T[r][c] = v;
-      }
-      double vj = 0.0;
-      if (lane >= 56 && lane < 63) {  // vj = M v'
-        const int r = lane - 56;
-        for (int k = 0; k < 7; k++) vj += M[r * 7 + k] * vp[k];
+      const double* M0 = sM + 49 * ri[u];
+      const double* M1 = sM + 49 * ri[u + 1];
+      double v0 = 0.0, v1 = 0.0;
+      if (tl || vl) {  // T = M G (lanes < 49), v = M v' (lanes 56..62)
+        const int bo = tl ? c_l : 98, bs = tl ? 7 : 1;
+        for (int k = 0; k < 7; k++) {
+          v0 += M0[r_l * 7 + k] * scr[bo + k * bs];
+          v1 += M1[r_l * 7 + k] * scr[147 + bo + k * bs];
+        }
+        if (tl) {
+          scr[49 + lane] = v0;
+          scr[147 + 49 + lane] = v1;
+        }
       }
       wave_lds_sync();
-      if (lane < 49) {  // A = T Mᵀ
-        const int r = lane / 7, c = lane % 7;
-        double v = 0.0;
-        for (int k = 0; k < 7; k++) v += T[r][k] * M[c * 7 + k];
-        out[lane] = v;
-      } else if (lane >= 56 && lane < 63) {
-        out[49 + lane - 56] = vj;
+      double* out0 = EB + (int64_t)e0 * kEB;
+      double* out1 = EB + (int64_t)(e0 + NW) * kEB;
+      if (tl) {  // A = T Mᵀ
+        double a0 = 0.0, a1 = 0.0;
+        for (int k = 0; k < 7; k++) {
+          a0 += scr[49 + r_l * 7 + k] * M0[c_l * 7 + k];
+          a1 += scr[147 + 49 + r_l * 7 + k] * M1[c_l * 7 + k];
+        }
+        out0[lane] = a0;
+        if (two) out1[lane] = a1;
+      } else if (vl) {
+        out0[49 + lane - 56] = v0;
+        if (two) out1[49 + lane - 56] = v1;
       }
-      wave_lds_sync();                           // scratch reused by the next edge
+      wave_lds_sync();                           // scratch reused by the next pair
     }
     if (k0 == 0) { M3S_GS(7) }
   }
@@ -812,65 +839,83 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
   __syncthreads();
   M3S_GS(2)
 
-  // 3) blocked right-looking Cholesky in LDS, one 7-column panel per pose, two barriers per
-  //    panel (instead of one per column).  Wave 0 factors the panel with its rows in
-  //    registers (row c0 + lane + 64 t; the pivot row and L[j][k] of the panel's rows come
-  //    from lanes 0..6 by v_readlane), then every thread applies the panel to its entries
-  //    (i, j) of the trailing triangle, the seven updates in column order, two entries at a
-  //    time.  Each entry receives the unblocked algorithm's operations in the same order
-  //    (A[i][j] -= L[i][k] L[j][k], k increasing; L[i][k] = A[i][k] · (1 / √A[k][k])), so
-  //    the factor — and the poses — are bit-identical to gn_solve_kernel's.  L[., k] goes
-  //    to the unused upper triangle (L[i][k] = sA[k n + i]), 1 / L[k][k] to sR[k].
+  // 3) blocked right-looking Cholesky in LDS with look-ahead, one 7-column panel per pose.
+  //    Wave 0 factors a panel with its rows in registers (row c0 + lane + 64 t; the pivot
+  //    row and L[j][k] of the panel's rows come from lanes 0..6 by v_readlane).  Panel p's
+  //    update of the trailing triangle is split: first the seven columns of panel p + 1 (all
+  //    threads, one entry each), then — while wave 0 already factors panel p + 1 — waves
+  //    1..15 apply panel p to the columns right of it, two entries per step.  Each entry
+  //    still receives the unblocked algorithm's operations in the same order (A[i][j] -=
+  //    L[i][k] L[j][k], k increasing; L[i][k] = A[i][k] · (1 / √A[k][k])), so the factor —
+  //    and the poses — are bit-identical to gn_solve_kernel's.  L[., k] goes to the unused
+  //    upper triangle (L[i][k] = sA[k n + i]), which neither update touches, 1 / L[k][k] to
+  //    sR[k].  The panel factor (its 1 / √d chain) is the critical path; the wide update
+  //    runs beside it.
   __shared__ int s_fail;
   bool fail = false;
   if (tid == 0) s_fail = 0;
+  auto factor_panel = [&](int c0) {  // wave 0
+    const int i0 = c0 + lane, i1 = c0 + 64 + lane;  // n - c0 <= 126 rows
+    double a0[7], a1[7];
+#pragma unroll
+    for (int c = 0; c < 7; c++) {
+      a0[c] = i0 < n ? sA[i0 * n + c0 + c] : 0.0;
+      a1[c] = i1 < n ? sA[i1 * n + c0 + c] : 0.0;
+    }
+    bool f = false;
+#pragma unroll
+    for (int c = 0; c < 7; c++) {
+      const int k = c0 + c;
+      const double d = bcast_f64(a0[c], c);         // A[k][k]: row k is lane c
+      if (!(d > 0.0)) {
+        f = true;
+        break;
+      }
+      const double rpiv = 1.0 / sqrt(d);
+      const double l0 = a0[c] * rpiv, l1 = a1[c] * rpiv;
+      if (i0 > k && i0 < n) sA[k * n + i0] = l0;
+      if (i1 > k && i1 < n) sA[k * n + i1] = l1;
+      if (lane == 0) sR[k] = rpiv;
+#pragma unroll
+      for (int c2 = c + 1; c2 < 7; c2++) {
+        const double lj = bcast_f64(l0, c2);        // L[c0 + c2][k]
+        if (i0 >= c0 + c2) a0[c2] -= l0 * lj;
+        if (i1 >= c0 + c2) a1[c2] -= l1 * lj;
+      }
+    }
+    if (lane == 0 && f) s_fail = 1;
+  };
+  if (wv == 0) factor_panel(0);
   __syncthreads();
   for (int c0 = 0; c0 < n; c0 += 7) {
-    if (wv == 0) {
-      const int i0 = c0 + lane, i1 = c0 + 64 + lane;  // n - c0 <= 126 rows
-      double a0[7], a1[7];
-#pragma unroll
-      for (int c = 0; c < 7; c++) {
-        a0[c] = i0 < n ? sA[i0 * n + c0 + c] : 0.0;
-        a1[c] = i1 < n ? sA[i1 * n + c0 + c] : 0.0;
-      }
-      bool f = false;
-#pragma unroll
-      for (int c = 0; c < 7; c++) {
-        const int k = c0 + c;
-        const double d = bcast_f64(a0[c], c);         // A[k][k]: row k is lane c
-        if (!(d > 0.0)) {
-          f = true;
-          break;
-        }
-        const double rpiv = 1.0 / sqrt(d);
-        const double l0 = a0[c] * rpiv, l1 = a1[c] * rpiv;
-        if (i0 > k && i0 < n) sA[k * n + i0] = l0;
-        if (i1 > k && i1 < n) sA[k * n + i1] = l1;
-        if (lane == 0) sR[k] = rpiv;
-#pragma unroll
-        for (int c2 = c + 1; c2 < 7; c2++) {
-          const double lj = bcast_f64(l0, c2);        // L[c0 + c2][k]
-          if (i0 >= c0 + c2) a0[c2] -= l0 * lj;
-          if (i1 >= c0 + c2) a1[c2] -= l1 * lj;
-        }
-      }
-      if (lane == 0 && f) s_fail = 1;
-    }
-    __syncthreads();
     if (s_fail) {  // uniform: read after the barrier by every thread
       fail = true;
       break;
     }
     const int t0 = c0 + 7;
-    if (t0 < n) {  // thread (row t0 + ri, column group cg): columns t0 + cg, + 8, ... <= row
-      const int ri = tid >> 3, cg = tid & 7;
-      const int i = t0 + ri;
+    if (t0 >= n) break;
+    {  // panel p applied to panel p + 1's columns: entry (t0 + ri, t0 + cj), cj <= ri
+      const int ri = tid / 7, cj = tid - 7 * ri;
+      const int i = t0 + ri, j = t0 + cj;
+      if (i < n && j <= i) {
+        double a = sA[i * n + j];
+#pragma unroll
+        for (int c = 0; c < 7; c++) a -= sA[(c0 + c) * n + i] * sA[(c0 + c) * n + j];
+        sA[i * n + j] = a;
+      }
+    }
+    __syncthreads();
+    if (wv == 0) {
+      factor_panel(t0);
+    } else {  // panel p applied to columns t0 + 7 .. i of row i = t0 + 7 + ri
+      const int t1 = t0 + 7;
+      const int ri = (tid - 64) >> 3, cg = tid & 7;
+      const int i = t1 + ri;
       if (i < n) {
         double li[7];
 #pragma unroll
         for (int c = 0; c < 7; c++) li[c] = sA[(c0 + c) * n + i];
-        int j = t0 + cg;
+        int j = t1 + cg;
         for (; j + 8 <= i; j += 16) {  // entries j and j + 8: two independent chains
           double a = sA[i * n + j], a8 = sA[i * n + j + 8];
           double lj[7], lj8[7];
