@@ -39,7 +39,7 @@ def test_gn_rays_parity(oracle, dev, P, h, w, iters):
 
 @pytest.mark.parametrize("P", [2, 19, 20, 24])
 def test_gn_rays_solve_paths(oracle, dev, P):
-    """The fp64 solve runs LDS-resident (system assembled by per-block contribution lists,
+    """The fp64 solve runs LDS-resident (system assembled by block row in edge order,
     Cholesky in LDS, one-wave triangular solves) while n = 7(P - 1) <= 126 and in global
     memory beyond: both paths, at the LDS capacity edge (P = 19, n = 126) and past it, vs
     the oracle's dense Cholesky."""
@@ -69,8 +69,8 @@ def test_gn_rays_solve_paths(oracle, dev, P):
 
 @pytest.mark.parametrize("P", [2, 16, 19])
 def test_gn_lds_solve_equals_global_solve(dev, P):
-    """The LDS-resident solve (per-block contribution lists, LDS Cholesky, one-wave
-    triangular solves) performs the global-memory solve's operations in the same order:
+    """The LDS-resident solve (block-row assembly in edge order, look-ahead LDS Cholesky,
+    one-wave triangular solves) performs the global-memory solve's operations in the same order:
     poses and steps bit-identical."""
     import mast3r_slam_backends as mb
     from monst3r_slam_amd import _lib
@@ -87,6 +87,38 @@ def test_gn_lds_solve_equals_global_solve(dev, P):
             _lib.load().m3s_gn_force_global_solve(0)
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_gn_lds_solve_equals_global_solve_many_edges(dev):
+    """Past 1,024 edges (64 per wave of the LDS solve: the per-wave pose-rank registers are
+    refilled, the assembly's ballot walks 18 chunks of 64 edges) the LDS solve still performs
+    the global solve's operations in the same order: 1,120 two-way edges (the 28 pairs of 8
+    keyframes, each 20 times with its own validity and Q), poses and steps bit-identical."""
+    import mast3r_slam_backends as mb
+    from monst3r_slam_amd import _lib
+    g = syn.keyframe_graph(P=8, h=8, w=16, seed=77, pairs=28, two_way=True)
+    rng = np.random.default_rng(5)
+    reps = 20
+    g = dict(g)
+    for k in ("ii", "jj", "idx"):
+        g[k] = np.concatenate([g[k]] * reps)
+    E, N = g["idx"].shape
+    assert E == 1120
+    g["valid"] = rng.uniform(size=(E, N, 1)) < 0.9
+    g["Q"] = (1.0 + np.exp(rng.normal(1.0, 0.5, size=(E, N, 1)))).astype(np.float32)
+    outs = []
+    for force in (0, 1):
+        _lib.load().m3s_gn_force_global_solve(force)
+        try:
+            Twc, Xs, Cs, ii, jj, idx, valid, Q = _gn_case(g, dev)
+            (dx,) = mb.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.003, 10.0, 0.0,
+                                         1.5, 3, 1e-8)
+            outs.append((Twc.cpu(), dx.cpu()))
+        finally:
+            _lib.load().m3s_gn_force_global_solve(0)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert torch.isfinite(outs[0][0]).all() and outs[0][1].abs().sum() > 0
 
 
 def test_gn_invalid_matches_ignore_their_index(dev):
