@@ -368,13 +368,15 @@ class ShardedFactorGraph(FactorGraph):
         counts = torch.bincount(owner_h, minlength=world).tolist()
         pad = max(1, 2 * max(counts))
         G_loc = torch.zeros((pad, 35), dtype=torch.float64, device=dev)
-        G_all = torch.zeros((E2, 35), dtype=torch.float64, device=dev)
+        G_all = torch.zeros((E2, 35), dtype=torch.float64, device=dev) if world > 1 else None
         slot = []                                  # gathered row → global two-way edge id
         for r_ in range(world):
             loc = torch.nonzero(owner_h == r_).flatten()
             slot.append(torch.cat([loc, loc + E, torch.full((pad - 2 * loc.numel(),), -1,
                                                            dtype=loc.dtype)]))
         slot = torch.cat(slot)
+        if world == 1:  # slot is the identity over the 2E two-way rows (pad == 2E)
+            assert pad == E2 and torch.equal(slot, torch.arange(E2))
         take_h = torch.nonzero(slot >= 0).flatten()  # index lists, built once: no per-
         take = take_h.to(dev)                         # iteration mask (a host sync)
         dst = slot.index_select(0, take_h).to(dev)
@@ -396,10 +398,13 @@ class ShardedFactorGraph(FactorGraph):
                     float(c["depth_eps"]), float(c["sigma_pixel"]), float(c["sigma_depth"]),
                     float(c["C_conf"]), float(c["Q_conf"]), ptr(G_loc), ptr(ws), s)
             _lib.check(st, "gn_edge_pass")
-            gathered = (_all_gather_fixed(G_loc, self.group) if world > 1 else G_loc).reshape(
-                world * pad, 35)
-            G_all.index_copy_(0, dst, gathered.index_select(0, take))
-            _lib.check(lib.m3s_gn_solve_step(ptr(pose), ptr(G_all), P, N, E2, El,
+            if world > 1:
+                gathered = _all_gather_fixed(G_loc, self.group).reshape(world * pad, 35)
+                G_all.index_copy_(0, dst, gathered.index_select(0, take))
+                G_use = G_all
+            else:  # one rank holds every edge: its slab is already in two-way edge order
+                G_use = G_loc
+            _lib.check(lib.m3s_gn_solve_step(ptr(pose), ptr(G_use), P, N, E2, El,
                                              float(c["delta_norm"]), ptr(dx), ptr(ws), s),
                        "gn_solve_step")
         loop_ev[1].record()

@@ -101,3 +101,22 @@ def test_sharded_gn_equals_unsharded(dev, world, mode, parity_log):
         assert 1 <= iters <= 10
     parity_log(f"sharded_gn_{mode}_world{world}", pose_maxabs_vs_unsharded=0.0,
                iterations=int(res[0][2]), bar="bit-identical")
+
+
+@pytest.mark.parametrize("mode", ["rays", "calib"])
+def test_sharded_solver_one_rank_equals_unsharded(dev, mode):
+    """The sharded solver on one rank (the bench's one-GPU keyframe-graph leg calls
+    _solve_sharded directly): the rank's slab of per-edge sums is already in two-way edge
+    order and goes to the solve as is (no gather / permutation) — poses bit-identical to the
+    unsharded solve."""
+    from monst3r_slam_amd import parallel as Pm
+    from monst3r_slam_amd.global_opt import FactorGraph
+    sc = _scene()
+    g, frames = _graph(FactorGraph, dev, sc)
+    (g.solve_GN_rays if mode == "rays" else g.solve_GN_calib)()
+    ref = frames.T_WC[:P].cpu().numpy()
+    g1, frames1 = _graph(Pm.ShardedFactorGraph, dev, sc, owner=[0] * PAIRS, rank=0)
+    g1._solve_sharded(mode)
+    torch.cuda.synchronize()
+    assert np.array_equal(frames1.T_WC[:P].cpu().numpy(), ref)
+    assert 1 <= g1.gn_iterations <= 10
