@@ -1090,10 +1090,19 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// E x S ~ 768 workgroups of 4 waves = 3 waves on each of the 1024 SIMDs, the rays kernel's
-// occupancy at 146 VGPRs: the edge pass runs in one round, with no tail
+// E x S ~ 3072 workgroups: four rounds of the 768 that fit the chip at once (3 waves per
+// SIMD at the rays kernel's 126 VGPRs).  The 1-D grid gives each XCD a contiguous run of the
+// edges sorted by pose i and dispatches it in order, so with four rounds an XCD works on
+// about half of one keyframe's edges at a time and the scattered gathers of its (X, C)
+// records (3.1 MB at 384 x 512) stay in its 4 MB L2; one round (768) had two keyframes'
+// records in flight per XCD.  Measured per GN iteration at P = 16, E = 128 (debug builds,
+// tools/gn_stamps.py, profiles/r04_gn_split_sweep.txt): random matches 376 → 294 µs, shifted
+// 285 → 278, identity 273 → 271; 4608 / 6144 are slower again.
+#ifndef M3S_GN_SPLIT_TARGET
+#define M3S_GN_SPLIT_TARGET 3072
+#endif
 int choose_splits(int64_t E, int64_t N) {
-  int64_t S = (768 + E - 1) / E;
+  int64_t S = (M3S_GN_SPLIT_TARGET + E - 1) / E;
   const int64_t max_by_points = (N + 1023) / 1024;  // >= ~1024 points per workgroup
   if (S > max_by_points) S = max_by_points;
   if (S < 1) S = 1;

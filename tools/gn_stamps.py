@@ -3,7 +3,8 @@ two-way edges, 384 x 512 points) — wall time per iteration of mast3r_slam_back
 gauss_newton_rays, and, with the debug library (make -C monst3r-slam_amd/csrc gn_stamps),
 the LDS solve's phase timeline per iteration: per-edge blocks, assembly, Cholesky,
 triangular solves, retraction / convergence (µs, thread 0, s_memrealtime).
-Usage: [SCATTER=1] python tools/gn_stamps.py   (SCATTER: shifted, jittered match indices)"""
+Usage: [SCATTER=1|2] python tools/gn_stamps.py   (SCATTER=1: shifted, jittered match
+indices; 2: uniformly random ones)"""
 import ctypes
 import os
 import sys
@@ -21,7 +22,10 @@ dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
 ITERS = 10
 g = syn.keyframe_graph(P=16, h=384, w=512, seed=5, pairs=64, two_way=True)
-if os.environ.get("SCATTER"):  # match indices as a moving camera's: shifted, jittered
+if os.environ.get("SCATTER") == "2":  # uniformly random match indices (the bench leg's
+    rng = np.random.default_rng(1)         # random-weight descriptors scatter ~90 % of them)
+    g["idx"] = rng.integers(0, g["idx"].shape[1], g["idx"].shape).astype(np.int64)
+elif os.environ.get("SCATTER"):  # match indices as a moving camera's: shifted, jittered
     rng = np.random.default_rng(1)
     h, w = 384, 512
     yy, xx = np.divmod(np.arange(h * w), w)
