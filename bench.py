@@ -224,10 +224,11 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
     buf = torch.empty((cap, 64, 2), dtype=torch.int64, device=dev)
 
     def cap_tl(k):
-        loop.step(k)                      # warm / allocate outside the timeline
-        torch.cuda.synchronize(dev)
+        from monst3r_slam_amd.capture import capture_graph, check_topology
+        # warm / allocate outside the timeline's slot range, with the step's fork / join
+        # structure and width checked before the capture (TopologyError, not a crash)
+        check_topology(lambda: loop.step(k), dev)
         n0 = int(lib.m3s_timeline_count())
-        from monst3r_slam_amd.capture import capture_graph
         g = capture_graph(lambda: loop.step(k), dev, warmup=False)
         return g, n0, int(lib.m3s_timeline_count())
 
@@ -841,16 +842,13 @@ def sequence_report(loop, seq, steps):
 def launch_ranks(n, argv):
     """`--gpus N` with no launcher around this process: start N ranks of this same script
     under torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1, RCCL between
-    them), wait for them and exit with their status.  Only torch.cuda.device_count() is
-    called first (it does not initialise the GPU), and N above it is an error, never a
-    silent fallback to fewer ranks.  Rank 0 prints the one JSON line."""
+    them), wait for them and exit with their status.  This parent makes no HIP call at all
+    (not even a device count, which can bring the runtime up): each rank checks its
+    LOCAL_RANK against the GPUs it sees and exits non-zero past them (`check_local_rank`),
+    and torch.distributed.run propagates that failure — N above the visible GPUs is an
+    error, never a silent fallback to fewer ranks.  Rank 0 prints the one JSON line."""
     import socket
     import subprocess
-    if "--launcher-selftest" not in argv:
-        avail = torch.cuda.device_count()
-        if n > avail:
-            sys.stderr.write(f"bench.py --gpus {n}: only {avail} GPU(s) visible\n")
-            sys.exit(2)
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
@@ -860,6 +858,18 @@ def launch_ranks(n, argv):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL on this host
     sys.exit(subprocess.call(cmd, env=env))
+
+
+def check_local_rank(local_rank, world):
+    """A launched rank's own check, before any other GPU or collective call: its LOCAL_RANK
+    must name a visible GPU.  `M3S_BENCH_DEVICES_STUB` replaces the device count (the CPU
+    test of the too-many-ranks exit)."""
+    stub = os.environ.get("M3S_BENCH_DEVICES_STUB")
+    avail = int(stub) if stub is not None else torch.cuda.device_count()
+    if local_rank >= avail:
+        sys.stderr.write(f"bench.py --gpus {world}: rank with LOCAL_RANK={local_rank} but only "
+                         f"{avail} GPU(s) visible\n")
+        sys.exit(2)
 
 
 def launcher_selftest(world, rank):
@@ -884,10 +894,13 @@ def main():
         sys.stderr.write(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}\n")
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.launcher_selftest:
+        if "M3S_BENCH_DEVICES_STUB" in os.environ:
+            check_local_rank(local_rank, world)
         launcher_selftest(world, rank)
         return
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    check_local_rank(local_rank, world)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)

@@ -267,7 +267,10 @@ __global__ __launch_bounds__(kEdgeThreads) void gn_edge_kernel(
 // workgroup; the order within a pose is immaterial: each row's partials are its own).
 __global__ __launch_bounds__(kSolveThreads) void gn_order_kernel(
     const int* __restrict__ rank_ii, const int* __restrict__ edge_ids, int rows, int P,
-    int* __restrict__ order) {
+    int* __restrict__ order, const int* __restrict__ flags) {
+  // |unique(ii, jj)| != P (gn_rank_kernel set flags[0]): ranks may reach past the P + 1
+  // counters, and every later kernel of the solve returns early anyway
+  if (flags[0]) return;
   extern __shared__ int cnt[];  // [P + 1]
   for (int p = threadIdx.x; p <= P; p += blockDim.x) cnt[p] = 0;
   __syncthreads();
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(kSolveThreads) void gn_rank_kernel(const int64_t* _
                                                                const int64_t* __restrict__ jj,
                                                                int E, int* __restrict__ rank_ii,
                                                                int* __restrict__ rank_jj,
-                                                               int* __restrict__ flags) {
+                                                               int* __restrict__ flags, int P) {
   constexpr int kWords = (1 << 17) / 32;
   const int M = 2 * E;  // E <= 65535
   __shared__ unsigned bits[kWords];
@@ -358,7 +361,10 @@ __global__ __launch_bounds__(kSolveThreads) void gn_rank_kernel(const int64_t* _
       if (p < E) rank_ii[p] = rank;
       else rank_jj[p - E] = rank;
     }
-    if (threadIdx.x == 0) flags[2] = s_unique;
+    if (threadIdx.x == 0) {
+      flags[2] = s_unique;
+      if (s_unique != P) flags[0] = 1;  // invalid graph: no kernel of the solve runs (status)
+    }
     return;
   }
   // wide id range: first occurrences (reusing the bitmap over positions), then count below
@@ -389,7 +395,10 @@ __global__ __launch_bounds__(kSolveThreads) void gn_rank_kernel(const int64_t* _
     if (p < E) rank_ii[p] = rank;
     else rank_jj[p - E] = rank;
   }
-  if (threadIdx.x == 0) flags[2] = s_unique;
+  if (threadIdx.x == 0) {
+    flags[2] = s_unique;
+    if (s_unique != P) flags[0] = 1;
+  }
 }
 
 // The S partials of each of this rank's E edges → G [E][kAcc] f64, in the solve kernel's
@@ -1177,11 +1186,11 @@ int run_gn(float* d_Twc, const float* d_Xs, const float* d_Cs, const float* d_K,
   M3S_HIP_CHECK(hipMemsetAsync(flags, 0, 64, st));
   if (P > 1) M3S_HIP_CHECK(hipMemsetAsync(d_dx, 0, sizeof(float) * 7 * (P - 1), st));
   hipLaunchKernelGGL(gn_rank_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_ii, d_jj, (int)E, rii,
-                     rjj, flags);
+                     rjj, flags, (int)P);
   M3S_LAUNCH_CHECK();
   int* order = reinterpret_cast<int*>(ws + L.order);
   hipLaunchKernelGGL(gn_order_kernel, dim3(1), dim3(kSolveThreads), sizeof(int) * (P + 1), st,
-                     rii, nullptr, (int)E, (int)P, order);
+                     rii, nullptr, (int)E, (int)P, order, flags);
   M3S_LAUNCH_CHECK();
   float4* XC = reinterpret_cast<float4*>(ws + L.xc);
   int* MI = reinterpret_cast<int*>(ws + L.mi);
@@ -1280,7 +1289,8 @@ int shard_edge_pass(const float* d_Twc, const float* d_Xs, const float* d_Cs, co
   int* order = reinterpret_cast<int*>(ws + L.order);
   hipLaunchKernelGGL(gn_order_kernel, dim3(1), dim3(kSolveThreads), sizeof(int) * (P + 1), st,
                      reinterpret_cast<const int*>(ws + L.rank_ii),
-                     reinterpret_cast<const int*>(d_edge_ids), (int)E_local, (int)P, order);
+                     reinterpret_cast<const int*>(d_edge_ids), (int)E_local, (int)P, order,
+                     flags);
   M3S_LAUNCH_CHECK();
   hipLaunchKernelGGL(gn_edge_kernel<MODE>, dim3((unsigned)(E_local * L.S)), dim3(kEdgeThreads),
                      0, st, d_Twc, XC, d_K, reinterpret_cast<const int*>(ws + L.rank_ii),
@@ -1328,7 +1338,7 @@ extern "C" int m3s_gn_sharded_begin(const int64_t* d_ii, const int64_t* d_jj, in
   if (P > 1) M3S_HIP_CHECK(hipMemsetAsync(d_dx, 0, sizeof(float) * 7 * (P - 1), st));
   hipLaunchKernelGGL(gn_rank_kernel, dim3(1), dim3(kSolveThreads), 0, st, d_ii, d_jj, (int)E,
                      reinterpret_cast<int*>(ws + L.rank_ii), reinterpret_cast<int*>(ws + L.rank_jj),
-                     reinterpret_cast<int*>(ws + L.flags));
+                     reinterpret_cast<int*>(ws + L.flags), (int)P);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }

@@ -162,6 +162,26 @@ def _join_all(topo: CaptureTopology, s: torch.cuda.Stream):
             s.wait_stream(other)
 
 
+def check_topology(fn, dev, check: bool = True):
+    """Run fn once eagerly on a fresh stream under CaptureTopology and raise TopologyError on
+    a malformed fork / join structure or a capture wider than the hardware queues allow —
+    the pre-capture check of `capture_graph(warmup=True)`, for callers that warm up
+    separately (bench.step_timeline) and then capture with warmup=False.  A width violation
+    found only DURING a capture cannot be kept from capture_end (torch's graph context always
+    ends the capture), so a capture without this eager pass in front is unchecked for width."""
+    s = torch.cuda.Stream(dev)
+    cur = torch.cuda.current_stream(dev)
+    s.wait_stream(cur)
+    topo = CaptureTopology(s)
+    with topo, torch.cuda.stream(s):
+        fn()
+    cur.wait_stream(s)
+    torch.cuda.synchronize(dev)
+    if check:
+        topo.check()
+    return topo
+
+
 def capture_graph(fn, dev, warmup: bool = True, check: bool = True):
     """Capture fn into a torch.cuda.CUDAGraph on a fresh stream, its stream topology checked.
 
@@ -171,17 +191,9 @@ def capture_graph(fn, dev, warmup: bool = True, check: bool = True):
     itself is traced again; should it differ and fail, every participating stream is joined
     into the capture stream before capture_end and the error is raised after it.
     Returns the graph (attribute m3s_streams: the streams that took part)."""
-    s = torch.cuda.Stream(dev)
-    cur = torch.cuda.current_stream(dev)
     if warmup:
-        s.wait_stream(cur)
-        topo = CaptureTopology(s)
-        with topo, torch.cuda.stream(s):
-            fn()
-        cur.wait_stream(s)
-        torch.cuda.synchronize(dev)
-        if check:
-            topo.check()
+        check_topology(fn, dev, check)
+    s = torch.cuda.Stream(dev)
     g = torch.cuda.CUDAGraph()
     topo = CaptureTopology(s)
     bad = None

@@ -36,3 +36,24 @@ def test_world_size_must_match_gpus():
     r = _run(["--gpus", "2", "--launcher-selftest"], {"WORLD_SIZE": "1", "RANK": "0"})
     assert r.returncode == 2
     assert "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_more_ranks_than_gpus_exits_nonzero():
+    """The launching parent makes no HIP call; each rank compares its LOCAL_RANK with its own
+    device count (stubbed to 1 here) and the one past it exits 2, which torch.distributed.run
+    propagates as a failed job — never a silent run on fewer ranks."""
+    r = _run(["--gpus", "2", "--launcher-selftest"], {"M3S_BENCH_DEVICES_STUB": "1"})
+    assert r.returncode != 0
+    assert "LOCAL_RANK=1 but only 1 GPU(s) visible" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_launcher_parent_makes_no_device_call():
+    """`launch_ranks` (bench.py) must not touch torch.cuda / HIP before starting the ranks."""
+    import ast
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    fn = next(n for n in ast.walk(ast.parse(src))
+              if isinstance(n, ast.FunctionDef) and n.name == "launch_ranks")
+    body = ast.get_source_segment(src, fn)
+    doc = ast.get_docstring(fn) or ""
+    assert "torch.cuda" not in body.replace(doc, "")

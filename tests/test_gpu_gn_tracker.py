@@ -181,6 +181,32 @@ def test_gn_global_ids_and_not_pd(oracle, dev):
     assert torch.count_nonzero(dx) == 0
 
 
+@pytest.mark.parametrize("extra", [1, 2])
+def test_gn_more_unique_ids_than_poses_is_rejected_cleanly(oracle, dev, extra):
+    """|unique(ii, jj)| > P (the reference's size check, gn_kernels.cu:1160-1170): ranks then
+    reach past the P poses, so no kernel of the solve may run — the call raises, Twc is left
+    untouched (no out-of-bounds pose / counter / partial access on the way), and a valid call
+    on the same device afterwards still matches the oracle."""
+    import mast3r_slam_backends as mb
+    g = syn.keyframe_graph(P=4, h=24, w=32, seed=12)
+    Twc, Xs, Cs, ii, jj, idx, valid, Q = _gn_case(g, dev)
+    bad_ii = ii.clone()
+    for t in range(extra):
+        bad_ii[t] = 50 + t          # keyframe ids no pose exists for
+    before = Twc.clone()
+    with pytest.raises(RuntimeError, match="unique keyframes"):
+        mb.gauss_newton_rays(Twc, Xs, Cs, bad_ii, jj, idx, valid, Q, 0.003, 10.0, 0.0, 1.5, 5,
+                             1e-8)
+    torch.cuda.synchronize()
+    assert torch.equal(Twc, before)
+    Twc_ref = g["Twc"].copy()
+    oracle.gauss_newton("rays", Twc_ref, g["Xs"], g["Cs"], g["ii"], g["jj"], g["idx"],
+                        g["valid"], g["Q"], sig0=0.003, sig1=10.0, C_thresh=0.0, Q_thresh=1.5,
+                        max_iter=3, delta_thresh=1e-8)
+    mb.gauss_newton_rays(Twc, Xs, Cs, ii, jj, idx, valid, Q, 0.003, 10.0, 0.0, 1.5, 3, 1e-8)
+    np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=POSE_TOL, rtol=0)
+
+
 @pytest.mark.parametrize("stride", [3, 70001])
 def test_gn_global_ids_parity(oracle, dev, stride):
     # stride 3: ids within a 2^17 range (bitmap ranks); 70001: wider (the O(M^2) fallback)
