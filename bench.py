@@ -206,6 +206,67 @@ def _union_ticks(iv):
     return tot
 
 
+def _union_np(s, e):
+    """Total length of the union of intervals [s, e) (numpy, vectorised)."""
+    import numpy as np
+    if len(s) == 0:
+        return 0.0
+    o = np.argsort(s, kind="stable")
+    s, e = s[o], e[o]
+    ce = np.maximum.accumulate(e)
+    new = np.ones(len(s), bool)
+    new[1:] = s[1:] > ce[:-1]
+    seg = np.cumsum(new) - 1
+    seg_s = s[new]
+    seg_e = np.zeros(int(seg[-1]) + 1, dtype=e.dtype)
+    np.maximum.at(seg_e, seg, e)
+    return float((seg_e - seg_s).sum())
+
+
+def _cu_occupancy(blog, bcnt, slot, graphs, kinds):
+    """Which CUs hold a GEMM / attention block, over the replayed steps of the last round
+    (the block log, common.h M3sTlEnd: per block its start / end and HW_ID / XCC_ID): per
+    step, the fraction of CU-time (256 CUs x the step's stamped span) during which a CU
+    holds at least one block, and the same per launch kind — the split between "CUs idle"
+    and "CUs busy at a low MFMA rate" that the step's 0.2 of peak hides."""
+    import numpy as np
+    nb = min(int(bcnt[0]), blog.shape[0])
+    if nb == 0:
+        return None
+    lg = blog[:nb].cpu().numpy()
+    sl = (lg[:, 2] - slot.data_ptr()) // (132 * 8)
+    kd = kinds[np.clip(sl, 0, len(kinds) - 1)]
+    hw, xcc = lg[:, 3] & 0xFFFFFFFF, (lg[:, 3] >> 32) & 0xF
+    # gfx9 HW_ID: CU_ID [11:8], SH_ID [12], SE_ID [15:13]; one CU = (XCC, SE, SH, CU)
+    cu = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xF)
+    ucu, cu_ix = np.unique(cu, return_inverse=True)
+    steps = []
+    for i, (g, a, b) in enumerate(graphs):
+        if i == 0:
+            continue
+        sel = (sl >= a) & (sl < b)
+        if not sel.any():
+            continue
+        t0, t1 = lg[sel, 0].min(), lg[sel, 1].max()
+        span = float(t1 - t0)
+        off = (cu_ix.astype(np.int64) * int(4 * span + 10))   # CUs' intervals never overlap
+        row = {"span_ms": span * 1e-5}
+        for name, mk in (("any", sel), ("gemm", sel & np.isin(kd, (1, 3))),
+                         ("attn", sel & (kd == 2))):
+            row[name] = _union_np((lg[mk, 0] - t0 + off[mk]).astype(np.int64),
+                                  (lg[mk, 1] - t0 + off[mk]).astype(np.int64)) / (256.0 * span)
+        steps.append(row)
+    if not steps:
+        return None
+    return {"cus_seen": int(len(ucu)), "blocks_logged": nb, "steps": len(steps),
+            "busy_frac_any": float(np.median([r["any"] for r in steps])),
+            "busy_frac_gemm": float(np.median([r["gemm"] for r in steps])),
+            "busy_frac_attn": float(np.median([r["attn"] for r in steps])),
+            "note": "fraction of the 256 CUs x stamped step span during which a CU holds at "
+                    "least one GEMM (or attention) block (block log of common.h M3sTlEnd, "
+                    "median over the replayed steps of the last round)"}
+
+
 def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
     """The captured C3 step timed launch by launch AS IT RUNS (no tracer): `pairs` pairs of
     the two parity graphs are captured again with the library's step timeline armed
@@ -221,7 +282,16 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
     from monst3r_slam_amd import _lib
     lib, P = _lib.load(), _lib.ptr
     cap = 8192
-    buf = torch.empty((cap, 64, 2), dtype=torch.int64, device=dev)
+    slot = torch.empty((cap, 132), dtype=torch.int64, device=dev)   # M3S_TL_SLOT u64 per slot
+    buf = slot[:, :128].view(cap, 64, 2)
+    # block log (common.h M3sTlEnd): one record per block of every instrumented launch
+    nlog = 1 << 21
+    blog = torch.zeros((nlog, 4), dtype=torch.int64, device=dev)
+    bcnt = torch.zeros(2, dtype=torch.int32, device=dev)
+    slot[:, 128] = 0
+    slot[:, 129] = bcnt.data_ptr()
+    slot[:, 130] = nlog
+    slot[:, 131] = 0
 
     def cap_tl(k):
         from monst3r_slam_amd.capture import capture_graph, check_topology
@@ -251,9 +321,13 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
     rows = []
     keep = None
     st = torch.cuda.current_stream(dev)
+    occ = None
     for rd in range(rounds):
         buf[..., 0] = -1                  # UINT64_MAX: atomic-min target
         buf[..., 1] = 0
+        last = rd == rounds - 1           # the last round also logs every block
+        slot[:, 128] = blog.data_ptr() if last else 0
+        bcnt.zero_()
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(graphs) + 1)]
         evs[0].record(st)
         for i, (g, _, _) in enumerate(graphs):
@@ -292,11 +366,14 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
             rows.append(row)
             if rd == rounds - 1 and i == len(graphs) - 2:
                 keep = (t.copy(), k.copy(), fl.copy(), dims[a:b].copy(), step_ms)
+        if last:
+            occ = _cu_occupancy(blog, bcnt, slot, graphs, kinds)
 
     def med(f):
         return float(np.median([f(r) for r in rows]))
 
     res = {"replays": len(rows), "step_ms": med(lambda r: r["step_ms"]),
+           "cu_occupancy": occ,
            "span_ms": med(lambda r: r["span_ms"]),
            "gemm_or_attn_union_ms": med(lambda r: r["busy_union_ms"])}
     for name in ("gemm", "attn"):
@@ -408,7 +485,8 @@ def roofline_entry(tl, roof, pmc, mfma, step_ms):
              avg_launch_us=g["avg_launch_us"], tflops_per_launch_avg=g["tflops_per_launch_avg"],
              attention=tl["attn"], timeline_step_ms=tl["step_ms"],
              timeline_vs_timed_step=tl["step_ms"] / step_ms,
-             gemm_or_attn_union_ms=tl["gemm_or_attn_union_ms"])
+             gemm_or_attn_union_ms=tl["gemm_or_attn_union_ms"],
+             cu_occupancy=tl.get("cu_occupancy"))
     e["algorithmic_bytes_per_step"] = g["algorithmic_bytes"]
     e["algorithmic_bytes_rule"] = ("floor: every GEMM reads A and B and writes C once, bf16 "
                                    "((M·K + N·K + M·N)·batch·2 B per launch, step_timeline dims; "

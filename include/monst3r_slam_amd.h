@@ -45,10 +45,13 @@ int m3s_device_count(void);
 /* Step timeline (diagnostic; bench.py step_timeline).  m3s_timeline_set(d_buf, capacity)
  * arms it: every GEMM (m3s_vit_gemm) and attention (m3s_vit_attention) launch issued
  * afterwards — eager or captured into a graph — takes the next of `capacity` slots of
- * d_buf (u64 [capacity][64][2]: per slot 64 pairs {earliest block start, latest wave end}
+ * d_buf (u64 [capacity][132]: per slot 64 pairs {earliest block start, latest wave end}
  * in s_memrealtime ticks of 100 MHz, block b stamping pair b % 64; the launch spans
  * [min of the starts, max of the ends]; the caller fills every pair with {UINT64_MAX, 0}
- * before a run).  A null d_buf
+ * before a run; then a 4-u64 header {block-log buffer or 0, pointer to its u32 record
+ * counter, capacity in records, 0}: when set, the first wave of every block appends
+ * {start, end, slot address, HW_ID | XCC_ID << 32} (4 u64) at the counter — the busy
+ * intervals of every CU).  A null d_buf
  * disarms it (later launches carry no slot).  m3s_timeline_count() = slots taken since the
  * last set; m3s_timeline_meta() copies their kinds (1 GEMM, 2 attention, 3 implicit 3x3
  * conv GEMM), algorithmic

@@ -38,7 +38,7 @@ unsigned long long* m3s_timeline_take(int kind, double flops, int64_t d0, int64_
   g_tl_kind.push_back(kind);
   g_tl_flops.push_back(flops);
   g_tl_dims.insert(g_tl_dims.end(), {d0, d1, d2, d3});
-  return g_tl + 2 * M3S_TL_SUB_HOST * (int64_t)g_tl_n++;
+  return g_tl + (2 * M3S_TL_SUB_HOST + 4) * (int64_t)g_tl_n++;   // M3S_TL_SLOT u64 per slot
 }
 
 extern "C" int m3s_timeline_set(void* d_buf, int capacity) {

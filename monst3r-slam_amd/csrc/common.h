@@ -49,8 +49,13 @@ __device__ __forceinline__ double m3s_wave_sum_d(double v) {
 // atomics in series and stretched the step 1.4x.  The slot pointer travels in the kernel
 // arguments, so a captured graph keeps its launches' slots; with no buffer set the pointer
 // is null and the kernels only test it.
+// A slot is M3S_TL_SLOT u64: the M3S_TL_SUB pairs, then a header the host fills before a
+// replay — [0] a block-log buffer or 0, [1] its u32 record counter, [2] its capacity in
+// records — through which the first wave of every block appends one 32-B record {start,
+// end, slot address, HW_ID | XCC_ID << 32} (bench.step_timeline: which CUs are busy when).
 enum { M3S_TL_GEMM = 1, M3S_TL_ATTN = 2, M3S_TL_CONV = 3 };  // CONV: implicit 3x3 GEMM
 #define M3S_TL_SUB 64
+#define M3S_TL_SLOT (2 * M3S_TL_SUB + 4)
 unsigned long long* m3s_timeline_take(int kind, double flops, int64_t d0, int64_t d1, int64_t d2,
                                         int64_t d3);  // capi.cpp; null when off
 
@@ -63,8 +68,28 @@ __device__ __forceinline__ void m3s_tl_begin(unsigned long long* tl) {
 }
 struct M3sTlEnd {  // stamps the wave's end on every return path
   unsigned long long* p;
+  unsigned long long t0;
+  __device__ __forceinline__ M3sTlEnd(unsigned long long* slot)
+      : p(slot), t0(slot ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull) {}
   __device__ __forceinline__ ~M3sTlEnd() {
-    if (p && (threadIdx.x & 63) == 0)
-      atomicMax(m3s_tl_pair(p) + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (p && (threadIdx.x & 63) == 0) {
+      const unsigned long long now = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+      atomicMax(m3s_tl_pair(p) + 1, now);
+      unsigned long long* log =
+          threadIdx.x == 0 ? reinterpret_cast<unsigned long long*>(p[2 * M3S_TL_SUB]) : nullptr;
+      if (log) {
+        unsigned* cnt = reinterpret_cast<unsigned*>(p[2 * M3S_TL_SUB + 1]);
+        const unsigned i = atomicAdd(cnt, 1u);
+        if (i < (unsigned)p[2 * M3S_TL_SUB + 2]) {
+          unsigned hw, xcc;
+          asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+          asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+          ulonglong2* r = reinterpret_cast<ulonglong2*>(log + 4 * (size_t)i);
+          r[0] = make_ulonglong2(t0, now);
+          r[1] = make_ulonglong2(reinterpret_cast<unsigned long long>(p),
+                                 (unsigned long long)hw | ((unsigned long long)xcc << 32));
+        }
+      }
+    }
   }
 };

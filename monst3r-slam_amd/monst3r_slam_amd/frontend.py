@@ -258,6 +258,10 @@ class FramePipeline:
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
             self.encode_side(img_next, k)
-        res = self.tr.track(img_cur, T_WCf_init, feat_i=self.feat[k % 2])
+        self.tr.model.head_aux = self.side   # DPT heads' off-chain branches (model._head_aux)
+        try:
+            res = self.tr.track(img_cur, T_WCf_init, feat_i=self.feat[k % 2])
+        finally:
+            self.tr.model.head_aux = None
         main.wait_stream(self.side)
         return res

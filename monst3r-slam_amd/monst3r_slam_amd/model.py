@@ -458,6 +458,7 @@ class PairModel:
         self._wbase = 0       # first head-weight stack of that set
         self._wm = 4
         self._ev_heads = None
+        self.head_aux = None  # stream for the DPT heads' off-chain branches (_head_aux)
 
     def set_fp8(self, on=True):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
@@ -487,6 +488,19 @@ class PairModel:
         main = torch.cuda.current_stream(self.dev)
         self.side[k].wait_stream(main)
         return torch.cuda.stream(self.side[k])
+
+    def _head_aux(self):
+        """Stream for the DPT head set's off-chain work (`_dpt`): the caller's `head_aux`
+        (FramePipeline hands its prefetch stream, idle once the step's encoder part is
+        issued, so the captured step keeps its three streams), else side stream 1; None —
+        everything on the current stream — for the split MASt3R set (already a side
+        chain) or M3S_HEAD_AUX=0."""
+        mode = os.environ.get("M3S_HEAD_AUX", "1")   # A/B: 0 = none, side1 = side stream 1
+        if self._tag == "mast3r" or mode == "0":
+            return None
+        if mode == "side1" or self.head_aux is None:
+            return self.side[1]
+        return self.head_aux
 
     def _event(self):
         if self.serial:
@@ -865,35 +879,43 @@ class PairModel:
         return hout, wout
 
     def _rcu(self, x, k, u, b, h, w, out, addend_res=None):
-        """ResidualConvUnit: out = conv2(relu(conv1(relu(x)))) + (x or addend_res)."""
+        """ResidualConvUnit: out = conv2(relu(conv1(relu(x)))) + (x or addend_res).  The
+        conv1 scratch is per unit (RCU1 runs on the aux stream beside RCU2 of the same
+        resolution)."""
         F = self.a.feature_dim
-        t = self._buf(("rcu_t", h, w), (b, h, w, F), BF16)
+        t = self._buf(("rcu_t", u, h, w), (b, h, w, F), BF16)
         self._conv3(x, f"r{k}_u{u}c1_w", t, b, h, w, F, F, bias_key=f"r{k}_u{u}c1_b",
                     flags=_lib.PRO_RELU)
         self._conv3(t, f"r{k}_u{u}c2_w", out, b, h, w, F, F, bias_key=f"r{k}_u{u}c2_b",
                     R=addend_res if addend_res is not None else x,
                     flags=_lib.PRO_RELU | _lib.EPI_RES_BF16)
 
-    def _fusion(self, k, path, skip, b, h, w, next_hw, next_skip, out):
-        """FeatureFusionBlock (dpt_block.py:185-218) at resolution (h, w):
-        s = path + RCU1(skip) (skip None for refinenet4); s = RCU2(s);
-        out = up2(out_conv(s)) (+ next_skip)  — out_conv commuted before the upsample.
-        With a skip, `path` already holds path + skip (the previous level's upsample added
-        it), which is exactly RCU1's residual addend."""
+    def _fusion(self, k, s1, b, h, w, next_hw, next_u, out, ev_u=None):
+        """FeatureFusionBlock (dpt_block.py:185-218) at resolution (h, w), from its input
+        s1 = path + RCU1(skip) (refinenet4: the path alone): s = RCU2(s1);
+        out = up2(out_conv(s)) + next_u — out_conv commuted before the upsample, and the
+        next level's `+ RCU1(skip)` (next_u, computed off this chain: `_rcu1_skip`, ready
+        at event ev_u) added by the upsample, so `out` is the next level's s1."""
         o, H = self.ops, self._hw
         F = self.a.feature_dim
-        s1 = self._buf(("fus_s1", h, w), (b, h, w, F), BF16)
-        if skip is not None:
-            self._rcu(skip, k, 1, b, h, w, s1, addend_res=path)   # conv(..) + (path + skip)
-        else:
-            s1 = path
         s2 = self._buf(("fus_s2", h, w), (b, h, w, F), BF16)
         self._rcu(s1, k, 2, b, h, w, s2)
         oc = self._buf(("fus_oc", h, w), (b, h, w, F), BF16)
         o.gemm(s2, H(f"r{k}_out_w"), oc, h * w, F, F, b, sA=h * w * F, sB=F * F, sC=h * w * F,
                bias=H(f"r{k}_out_b"), sBias=F, wmod=self._wm)
         oh, ow = next_hw
-        o.up2(oc, out, b, h, w, F, oh, ow, add=next_skip)
+        if ev_u is not None:
+            torch.cuda.current_stream(self.dev).wait_event(ev_u)
+        o.up2(oc, out, b, h, w, F, oh, ow, add=next_u)
+
+    def _rcu1_skip(self, k, skip, b, h, w):
+        """refinenet k's RCU1 on its skip (layer_rn output): u = conv2(relu(conv1(relu(skip))))
+        + skip.  It depends on the skip alone, so it runs beside the refinenet chain
+        (`_dpt`); the chain's upsample adds it: path + RCU1(skip) is the fusion's s1."""
+        F = self.a.feature_dim
+        u = self._buf(("fus_u", h, w), (b, h, w, F), BF16)
+        self._rcu(skip, k, 1, b, h, w, u)
+        return u
 
     def _local_features(self, hooks, G, S, E, D, H, W):
         """MASt3R local features (z = 2, 3 of each pair): cat(enc, dec_last) → MLP → pixel
@@ -1049,26 +1071,35 @@ class PairModel:
         F = a.feature_dim
         g3h, g3w = (gh + 1) // 2, (gw + 1) // 2
         R = self._rn_bufs(gh, gw, Z)
-        # act_postprocess + layer_rn (3x3, no bias → F channels): branches 1-3 on side
-        # stream 0, branch 0 (the largest) on the current stream (one stream when serial)
-        with self._on(0):
-            for k in (1, 2, 3):
-                self._ap_branch(k, hooks, gh, gw, Z, R)
-            ev_ap = self._event()
-        self._ap_branch(0, hooks, gh, gw, Z, R)
-        self._wait(ev_ap)
-        # refinenets: path_k = up2(out_conv(RCU2(path_{k+1} + RCU1(R_k)))) with the next
-        # level's skip pre-added by the upsample (consumed as RCU1's residual addend)
+        # The refinenet chain needs the act_postprocess / layer_rn outputs one level at a
+        # time (R[3] first, R[0] last), and each level's RCU1 depends on its skip R[k-1]
+        # alone: branch 3 opens the chain; branches 2, 1, 0, each followed by its level's
+        # RCU1 (u3, u2, u1), run in that order on the aux stream (`head_aux`: the chain's
+        # own stream is the tracking-critical one) and are joined by event at the upsample
+        # that adds them — 11 of the chain's ~36 launches leave it.
+        aux = self._head_aux()
+        h_of = {3: (gh, gw), 2: (2 * gh, 2 * gw), 1: (4 * gh, 4 * gw)}
+        u, ev_u = {}, {}
+        main = torch.cuda.current_stream(self.dev)
+        if aux is not None:
+            aux.wait_stream(main)
+        with (torch.cuda.stream(aux) if aux is not None else _Nullctx()):
+            for lvl, br in ((3, 2), (2, 1), (1, 0)):
+                self._ap_branch(br, hooks, gh, gw, Z, R)
+                u[lvl] = self._rcu1_skip(lvl, R[br], Z, *h_of[lvl])
+                if aux is not None:
+                    ev_u[lvl] = torch.cuda.Event()
+                    ev_u[lvl].record(aux)
+        self._ap_branch(3, hooks, gh, gw, Z, R)
+        # refinenets: s1_k = path_k + RCU1_k(R_{k-1}); path_{k-1} = up2(out_conv(RCU2(s1_k)))
         p4 = self._buf("path4", (Z, gh, gw, F), BF16)
-        # (each level's upsample also adds the next level's skip: p_k = path_k + R_{k-1},
-        # the `path + skip` that refinenet_{k-1}'s RCU1 residual takes)
-        self._fusion(4, R[3], None, Z, g3h, g3w, (gh, gw), R[2], p4)
+        self._fusion(4, R[3], Z, g3h, g3w, (gh, gw), u[3], p4, ev_u.get(3))
         p3 = self._buf("path3", (Z, 2 * gh, 2 * gw, F), BF16)
-        self._fusion(3, p4, R[2], Z, gh, gw, (2 * gh, 2 * gw), R[1], p3)
+        self._fusion(3, p4, Z, gh, gw, (2 * gh, 2 * gw), u[2], p3, ev_u.get(2))
         p2 = self._buf("path2", (Z, 4 * gh, 4 * gw, F), BF16)
-        self._fusion(2, p3, R[1], Z, 2 * gh, 2 * gw, (4 * gh, 4 * gw), R[0], p2)
+        self._fusion(2, p3, Z, 2 * gh, 2 * gw, (4 * gh, 4 * gw), u[1], p2, ev_u.get(1))
         p1 = self._buf("path1", (Z, 8 * gh, 8 * gw, F), BF16)
-        self._fusion(1, p2, R[0], Z, 4 * gh, 4 * gw, (8 * gh, 8 * gw), None, p1)
+        self._fusion(1, p2, Z, 4 * gh, 4 * gw, (8 * gh, 8 * gw), None, p1)
         # head: conv3x3 F→F/2 @ (H/2, W/2), up2, conv3x3 → last_dim + ReLU, 1x1 → 4 + post
         h2, w2 = 8 * gh, 8 * gw
         hd0 = self._buf("head0", (Z, h2, w2, F // 2), BF16)

@@ -274,7 +274,14 @@ class SequenceLoop:
                                         pipe.group > 1 else 1)
                         self._gathered.record(pipe.side)
                     pipe.encode_side(self.img_next, k)
-                out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i, split_heads=split)
+                # the DPT heads' off-chain branches follow this step's encoder part on the
+                # prefetch stream (the step keeps its three streams)
+                m.head_aux = pipe.side
+                try:
+                    out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i,
+                                 split_heads=split)
+                finally:
+                    m.head_aux = None
             else:
                 self.gather(self.img_cur, 0)
                 out = m.pair(self.img_cur, feat_j=tr.kf.feat, split_heads=split)

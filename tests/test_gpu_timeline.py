@@ -23,9 +23,18 @@ def test_timeline_records_every_launch(dev):
     m.pair(img, feat_j=feat_k)          # allocate outside the timeline
     torch.cuda.synchronize()
     cap = 2048
-    buf = torch.empty((cap, 64, 2), dtype=torch.int64, device=dev)
+    slot = torch.empty((cap, 132), dtype=torch.int64, device=dev)   # M3S_TL_SLOT u64 per slot
+    buf = slot[:, :128].view(cap, 64, 2)
     buf[..., 0] = -1
     buf[..., 1] = 0
+    # block log: one 4-u64 record per block {start, end, slot address, HW_ID | XCC_ID << 32}
+    nlog = 1 << 16
+    blog = torch.zeros((nlog, 4), dtype=torch.int64, device=dev)
+    bcnt = torch.zeros(2, dtype=torch.int32, device=dev)
+    slot[:, 128] = blog.data_ptr()
+    slot[:, 129] = bcnt.data_ptr()
+    slot[:, 130] = nlog
+    slot[:, 131] = 0
     m.ops.record = []
     _lib.check(lib.m3s_timeline_set(P(buf), cap), "timeline_set")
     try:
@@ -59,3 +68,17 @@ def test_timeline_records_every_launch(dev):
     st = np.where(tb[..., 0] > 0, tb[..., 0], np.iinfo(np.int64).max).min(1)
     en = tb[..., 1].max(1)
     assert (en > 0).all() and (st < en).all()
+    # the block log: every block of every launch recorded once, inside its launch's span,
+    # on a CU the hardware ids name (XCC 0-7)
+    nb = int(bcnt[0])
+    assert 0 < nb <= nlog
+    lg = blog[:nb].cpu().numpy()
+    base = slot.data_ptr()
+    sl = (lg[:, 2] - base) // (132 * 8)
+    assert ((lg[:, 2] - base) % (132 * 8) == 0).all() and (sl >= 0).all() and (sl < n).all()
+    assert (lg[:, 0] <= lg[:, 1]).all()
+    assert (lg[:, 0] >= st[sl]).all() and (lg[:, 1] <= en[sl]).all()
+    xcc = (lg[:, 3] >> 32) & 0xF
+    assert xcc.max() <= 7
+    assert set(np.unique(sl)) == set(range(n))      # no launch without a block record
+
