@@ -236,6 +236,9 @@ def _cu_occupancy(blog, bcnt, slot, graphs, kinds):
     lg = blog[:nb].cpu().numpy()
     sl = (lg[:, 2] - slot.data_ptr()) // (132 * 8)
     kd = kinds[np.clip(sl, 0, len(kinds) - 1)]
+    if os.environ.get("M3S_BLOCKLOG_OUT"):   # raw log for offline analysis (tools)
+        np.savez_compressed(os.environ["M3S_BLOCKLOG_OUT"], log=lg, slot=sl, kind=kd,
+                            graphs=np.array([(a, b) for _, a, b in graphs]))
     hw, xcc = lg[:, 3] & 0xFFFFFFFF, (lg[:, 3] >> 32) & 0xF
     # gfx9 HW_ID: CU_ID [11:8], SH_ID [12], SE_ID [15:13]; one CU = (XCC, SE, SH, CU)
     cu = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 0xF)
@@ -528,27 +531,75 @@ def graph_pairs(n_kf=16, n_pairs=64):
     return ii, jj
 
 
+def retrieval_graph_pairs(feats, n_pairs=64, k=3, min_thresh=5e-3, device="cuda", db=None):
+    """The backend's graph construction (main_monster_slam.py:109-130) replayed over
+    keyframes 0, 1, ... in order: keyframe idx is paired with the previous keyframe and the
+    retrieval database's top-k hits above min_thresh (RetrievalDatabase.update(frame,
+    add_after_query=True, k, min_thresh), retrieval_database.py:43-72; k / min_thresh of
+    config/base.yaml:59-61), duplicates and idx itself dropped, edges (kf, idx) as
+    factor_graph.add_factors(kf_idx, frame_idx); stops after the keyframe whose edges reach
+    n_pairs.  feats: per-keyframe encoder features [1, S, E] bf16; db: a database to
+    empty and reuse (else a fresh one, seeded weights).  Returns ii, jj, retrieval (per
+    edge: True unless it is the consecutive edge), keyframes used."""
+    from monst3r_slam_amd.retrieval import RetrievalDatabase, synthetic_retrieval_weights
+    if db is None:
+        db = RetrievalDatabase(synthetic_retrieval_weights(seed=0), device=device,
+                               image_capacity=len(feats) + 1)
+    db.reset()
+    ii, jj, lc = [], [], []
+    for idx in range(len(feats)):
+        kf_idx = [idx - 1] if idx > 0 else []
+        kf_idx += db.update(feats[idx], add_after_query=True, k=k, min_thresh=min_thresh)
+        for j in sorted(set(kf_idx) - {idx}):
+            ii.append(j)
+            jj.append(idx)
+            lc.append(j != idx - 1)
+        if len(ii) >= n_pairs:
+            return ii, jj, lc, idx + 1
+    return ii, jj, lc, len(feats)
+
+
 def keyframe_graph_bench(model, dev, world, steps, warmup=1):
-    """configs[3]: sharded 64-pair symmetric re-inference + matching + GN over 16 keyframes."""
+    """configs[3]: sharded ~64-pair symmetric re-inference + matching + GN over the keyframe
+    graph the reference's backend builds: consecutive keyframes plus the retrieval
+    database's loop-closure candidates (retrieval_graph_pairs, inside the timed step)."""
     import numpy as np
     from monst3r_slam_amd import global_opt as GO
     from monst3r_slam_amd import parallel as P
     from monst3r_slam_amd import synthetic as syn
-    n_kf = 16
-    ii, jj = graph_pairs(n_kf, 64)
-    sc = syn.keyframe_graph(P=n_kf, h=H, w=W, seed=3)
+    kf_max = 24
+    sc = syn.keyframe_graph(P=kf_max, h=H, w=W, seed=3)
     g = torch.Generator(device=dev).manual_seed(7)     # same images on every rank
-    imgs = torch.rand(n_kf, 1, 3, H, W, device=dev, generator=g) * 2 - 1
-    frames = GO.Keyframes(H, W, buffer=n_kf, device=dev)
-    frames.img[:n_kf] = imgs
-    frames.X[:n_kf] = torch.from_numpy(sc["Xs"]).to(dev)
-    frames.C[:n_kf] = torch.from_numpy(sc["Cs"]).to(dev)
-    frames.set_counts(range(n_kf), N=1)
-    frames.img_true_shape[:n_kf] = torch.tensor([[H, W]], dtype=torch.int32, device=dev)
-    frames.n_size = n_kf
-    T0 = torch.from_numpy(sc["Twc"]).to(dev).reshape(n_kf, 1, 8)
-    h = _Bound(model)
+    imgs = torch.rand(kf_max, 1, 3, H, W, device=dev, generator=g) * 2 - 1
+    frames = GO.Keyframes(H, W, buffer=kf_max, device=dev)
+    frames.img[:kf_max] = imgs
+    frames.X[:kf_max] = torch.from_numpy(sc["Xs"]).to(dev)
+    frames.C[:kf_max] = torch.from_numpy(sc["Cs"]).to(dev)
+    frames.set_counts(range(kf_max), N=1)
+    frames.img_true_shape[:kf_max] = torch.tensor([[H, W]], dtype=torch.int32, device=dev)
+    frames.n_size = kf_max
     group = None
+    # the graph: encoder features of the keyframes, then the backend's retrieval-driven
+    # construction (replicated on every rank: same all-gathered features, deterministic
+    # kernels → the same pair list everywhere)
+    # (the encoder's tiles depend on the batch size, so the features of n keyframes encoded
+    # together are the ones the timed step reproduces: iterate to the fixed point)
+    from monst3r_slam_amd.retrieval import RetrievalDatabase, synthetic_retrieval_weights
+    db = RetrievalDatabase(synthetic_retrieval_weights(seed=0), device=dev,
+                           image_capacity=kf_max + 1)
+    n_kf, prev = kf_max, None
+    for _ in range(4):
+        P.shard_keyframe_features(frames, range(n_kf), model.encode, group)
+        ii, jj, lc, n_new = retrieval_graph_pairs([frames.feat[i] for i in range(n_kf)], 64,
+                                                  device=dev, db=db)
+        if (ii, jj, n_new) == prev:
+            break
+        prev, n_kf = (ii, jj, n_new), n_new
+    else:
+        raise RuntimeError("keyframe graph: the retrieval pair list does not settle")
+    frames.n_size = n_kf
+    T0 = torch.from_numpy(sc["Twc"][:n_kf]).to(dev).reshape(n_kf, 1, 8)
+    h = _Bound(model)
     # stand-in geometry, as in the C3 leg: the networks run on every pair (their cost is the
     # measured work) but random weights regress no geometry, so the symmetric decode's
     # pointmaps are overwritten with the scene's (Xii, Xji = T_i^-1 T_j X_j, Xjj, Xij),
@@ -578,6 +629,11 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
         P.shard_keyframe_features(frames, range(n_kf), model.encode, group)
         # the newest keyframe's pointmap, fused on the tracking rank, reaches every rank
         P.all_gather_keyframes(frames, [n_kf - 1], [0], group)
+        # the backend's graph construction: retrieval over the keyframes' features
+        pairs = retrieval_graph_pairs([frames.feat[i] for i in range(n_kf)], 64, device=dev,
+                                      db=db)
+        if pairs[:2] != (ii, jj):
+            raise RuntimeError("keyframe graph: retrieval returned another pair list")
         graph = P.ShardedFactorGraph(h, h, frames, device=dev, group=group)
         graph.add_factors(ii, jj, min_match_frac=0.0)
         graph.solve_GN_rays()
@@ -617,8 +673,12 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
         el = float(t.item())
     n = H * W
     del np
-    return {"workload": "configs[3]: 16 keyframes, 64 pairs symmetric re-inference (MonST3R+"
-                        "MASt3R, 4 decodes + 8 heads each) + 128 directed matches + GN rays",
+    return {"workload": f"configs[3]: {n_kf} keyframes, {len(ii)} pairs from the backend's "
+                        "graph construction (previous keyframe + RetrievalDatabase.update "
+                        "top-3 hits, main_monster_slam.py:109-130, inside the timed step) "
+                        "symmetric re-inference (MonST3R+MASt3R, 4 decodes + 8 heads each) + "
+                        f"{2 * len(ii)} directed matches + GN rays",
+            "pairs": len(ii), "pairs_from_retrieval": int(sum(lc)), "keyframes": n_kf,
             "pairs_per_s": len(ii) * steps / el, "ms_per_graph": el / steps * 1e3,
             "steps": steps, "edges_accepted": int(graph.ii.numel()),
             "pointmaps": "scene geometry stand-in over the network outputs (the decode runs)",

@@ -397,6 +397,14 @@ class PackedWeights:
 # ---------------------------------------------------------------------------------------
 # model runner
 # ---------------------------------------------------------------------------------------
+def _exp_hot_weights(part):
+    """DIAGNOSTIC ONLY (wrong outputs; tools / sweeps): M3S_EXP_HOT_WEIGHTS = enc | dec |
+    both makes every block of that stack read block 0's weights, so they stay cache-
+    resident across the step — how much of the step waits on streaming the weights."""
+    v = os.environ.get("M3S_EXP_HOT_WEIGHTS", "")
+    return v == part or v == "both"
+
+
 def _tile_knob(env, names, default):
     """GEMM tile hints {projection: (TileCfg, split-K)} from an experiment knob: "cfg:splits"
     for every projection, "name=cfg:splits,..." for some (the others: per-shape table),
@@ -495,7 +503,10 @@ class PairModel:
         issued, so the captured step keeps its three streams), else side stream 1; None —
         everything on the current stream — for the split MASt3R set (already a side
         chain) or M3S_HEAD_AUX=0."""
-        mode = os.environ.get("M3S_HEAD_AUX", "1")   # A/B: 0 = none, side1 = side stream 1
+        # default: the chain's own stream.  M3S_HEAD_AUX=1: the caller's stream (the step's
+        # prefetch stream: that captured step segfaulted at graph replay, round 5), side1:
+        # side stream 1 (a fourth captured stream: 232.6 vs 231.4 frames/s, noise)
+        mode = os.environ.get("M3S_HEAD_AUX", "0")
         if self._tag == "mast3r" or mode == "0":
             return None
         if mode == "side1" or self.head_aux is None:
@@ -607,16 +618,18 @@ class PairModel:
         rt = self.rope_tab(gh, gw)
         P, P8 = W.enc, W.enc8
         if fold:
+            hot = _exp_hot_weights("enc")
             for i in range(lo, hi):
-                o.gemm(xb, P["qkv_wf"][i], qkv, M, 3 * E, E, bias=P["qkv_c2"][i],
-                       rope=(rt, 2 * E, S), ln_fold=(st, P["qkv_c1"][i], 0), tile=tiles.get("qkv"))
+                j = 0 if hot else i
+                o.gemm(xb, P["qkv_wf"][j], qkv, M, 3 * E, E, bias=P["qkv_c2"][j],
+                       rope=(rt, 2 * E, S), ln_fold=(st, P["qkv_c1"][j], 0), tile=tiles.get("qkv"))
                 o.attn(qkv, 3 * E, S * 3 * E, qkv[:, E:], qkv[:, 2 * E:], 3 * E, S * 3 * E, att,
                        E, S * E, B, a.enc_heads, S, S)
-                o.gemm(att, P["proj_w"][i], x, M, E, E, bias=P["proj_b"][i], R=x,
+                o.gemm(att, P["proj_w"][j], x, M, E, E, bias=P["proj_b"][j], R=x,
                        tile=tiles.get("proj"), **R32S)
-                o.gemm(xb, P["fc1_wf"][i], hid, M, a.mlp_ratio * E, E, bias=P["fc1_c2"][i],
-                       flags=_lib.EPI_GELU, ln_fold=(st, P["fc1_c1"][i], 0), tile=tiles.get("fc1"))
-                o.gemm(hid, P["fc2_w"][i], x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][i], R=x,
+                o.gemm(xb, P["fc1_wf"][j], hid, M, a.mlp_ratio * E, E, bias=P["fc1_c2"][j],
+                       flags=_lib.EPI_GELU, ln_fold=(st, P["fc1_c1"][j], 0), tile=tiles.get("fc1"))
+                o.gemm(hid, P["fc2_w"][j], x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][j], R=x,
                        tile=tiles.get("fc2"), **R32S)
                 yield i
         for i in (range(lo, hi) if not fold else ()):
@@ -820,8 +833,9 @@ class PairModel:
         # tile hints (M3S_DEC_TILE experiment knob, as M3S_ENC_TILE; default: the table)
         tl = _tile_knob("M3S_DEC_TILE", ("qkv", "proj", "q", "cproj", "fc1", "fc2"),
                         self.dec_tiles if part is None else self.dec_tiles_split).get
+        hot = _exp_hot_weights("dec")
         for i in range(a.dec_depth):
-            P = W.dec[i]
+            P = W.dec[0 if hot else i]
             if sl is not None:
                 P = {k: v[sl] for k, v in P.items()}
             R32S = dict(R=x, sR=S * D, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32,

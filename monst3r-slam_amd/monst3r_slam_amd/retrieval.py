@@ -90,6 +90,14 @@ class RetrievalDatabase:
         self.img_start = torch.zeros(self._img_cap + 1, dtype=torch.int32, device=dev)
         self.n_entries = 0
 
+    def reset(self):
+        """Empty the database (no keyframes indexed), keeping the weights and workspaces —
+        a fresh load_retriever() without re-uploading the codebook."""
+        self.kf_counter = 0
+        self.kf_ids = []
+        self.n_entries = 0
+        self.img_start.zero_()
+
     # ---- retrieval_database.py:25-41 ------------------------------------------------------
     def prep_features(self, backbone_feat):
         """[1,S,E] (bf16 or f32) -> top-nfeat whitened local features [1,nfeat,H] f32."""

@@ -25,6 +25,7 @@ from __future__ import annotations
 import math
 
 import numpy as np
+
 import torch
 
 from . import _lib
@@ -266,14 +267,20 @@ class SequenceLoop:
                 feat_i = pipe.slot(k)
                 # group g: only part 0 of a group encode reads the images
                 gathers = k % pipe.group == 0
-                pipe.side.wait_stream(main)
-                with torch.cuda.stream(pipe.side):
-                    if gathers:   # group g: the frames g .. 2g-1 after the tracked one
-                        for j in range(pipe.group):
-                            self.gather(self.img_next[j:j + 1], pipe.group + j if
-                                        pipe.group > 1 else 1)
-                        self._gathered.record(pipe.side)
-                    pipe.encode_side(self.img_next, k)
+
+                def prefetch():
+                    pipe.side.wait_stream(main)
+                    with torch.cuda.stream(pipe.side):
+                        if gathers:   # group g: the frames g .. 2g-1 after the tracked one
+                            for j in range(pipe.group):
+                                self.gather(self.img_next[j:j + 1], pipe.group + j if
+                                            pipe.group > 1 else 1)
+                            self._gathered.record(pipe.side)
+                        pipe.encode_side(self.img_next, k)
+                # (issued before the pair: the encoder fills the decoder phase.  Started once
+                # the decoders are issued instead, into the head phase's idle CUs: 196 vs
+                # 231.5 frames/s, round 5 — the head phase cannot absorb it)
+                prefetch()
                 # the DPT heads' off-chain branches follow this step's encoder part on the
                 # prefetch stream (the step keeps its three streams)
                 m.head_aux = pipe.side

@@ -91,7 +91,13 @@ def test_factor_graph_add_factors_c4_vs_oracle(dev, scene, monkeypatch, parity_l
     h = bench._Bound(m)
     frames = _keyframes(dev, scene, m.a.enc_dim)
     P.shard_keyframe_features(frames, range(NKF), m.encode, None)
-    ii, jj = bench.graph_pairs(NKF, NPAIRS)
+    # the pair list the reference's backend builds (bench.retrieval_graph_pairs: previous
+    # keyframe + RetrievalDatabase.update top-k hits, main_monster_slam.py:109-130)
+    ii, jj, lc, _ = bench.retrieval_graph_pairs([frames.feat[i] for i in range(NKF)], NPAIRS,
+                                                device=dev)
+    E = len(ii)
+    assert E >= 16 and any(lc), (E, sum(lc))     # loop-closure candidates among the pairs
+    half = E // 2
     # the networks run (random weights: descriptors and Q are theirs), but their pointmaps
     # are replaced by the scene's geometry — Xii = X_i, Xji = T_i^-1 T_j X_j, Xjj = X_j,
     # Xij = T_j^-1 T_i X_i under the true poses, what a trained network regresses — so the
@@ -128,7 +134,7 @@ def test_factor_graph_add_factors_c4_vs_oracle(dev, scene, monkeypatch, parity_l
 
     # random-weight networks: choose Q_conf at the median fused Q of the matched pixels so
     # the per-edge match fractions spread, then a min_match_frac that splits batch 2
-    raw1, raw2 = raw_of(ii[:32], jj[:32]), raw_of(ii[32:], jj[32:])
+    raw1, raw2 = raw_of(ii[:half], jj[:half]), raw_of(ii[half:], jj[half:])
     Qj1, _ = fused(raw1)
     vm_frac = float(raw1[2].mean())
     cfg = default_config()["local_opt"]
@@ -144,16 +150,16 @@ def test_factor_graph_add_factors_c4_vs_oracle(dev, scene, monkeypatch, parity_l
     monkeypatch.setattr(U, "monst3r_match_symmetric", spy)
     graph = GO.FactorGraph(h, h, frames, device=dev)
     ref = FactorGraphRef(cfg)
-    # batch 1: the first 32 pairs, all accepted; batch 2: the rest at the splitting
-    # threshold; batch 3: a relocalisation with a weak edge → False, nothing added
-    cur["e"] = (ii[:32], jj[:32])
-    assert graph.add_factors(ii[:32], jj[:32], 0.0)
-    assert ref.add_factors(ii[:32], jj[:32], spy.calls[-1], 0.0)
+    # batch 1: the first half of the pairs, all accepted; batch 2: the rest at the
+    # splitting threshold; batch 3: a relocalisation with a weak edge → False, nothing added
+    cur["e"] = (ii[:half], jj[:half])
+    assert graph.add_factors(ii[:half], jj[:half], 0.0)
+    assert ref.add_factors(ii[:half], jj[:half], spy.calls[-1], 0.0)
     for a, c in zip(spy.calls[-1], raw1):                # the matcher is deterministic
         assert np.array_equal(a, c)
-    cur["e"] = (ii[32:], jj[32:])
-    added = graph.add_factors(ii[32:], jj[32:], thr)
-    assert added == ref.add_factors(ii[32:], jj[32:], spy.calls[-1], thr)
+    cur["e"] = (ii[half:], jj[half:])
+    added = graph.add_factors(ii[half:], jj[half:], thr)
+    assert added == ref.add_factors(ii[half:], jj[half:], spy.calls[-1], thr)
     for a, c in zip(spy.calls[-1], raw2):                # the matcher is deterministic
         assert np.array_equal(a, c)
     n_before = graph.ii.numel()
@@ -161,12 +167,13 @@ def test_factor_graph_add_factors_c4_vs_oracle(dev, scene, monkeypatch, parity_l
     assert not graph.add_factors([0, 2], [5, 9], 1.01, is_reloc=True)
     assert not ref.add_factors([0, 2], [5, 9], spy.calls[-1], 1.01, is_reloc=True)
     assert graph.ii.numel() == n_before
-    parity_log("c4_add_factors", edges=int(n_before), threshold=thr, Q_conf=cfg["Q_conf"],
+    parity_log("c4_add_factors", edges=int(n_before), pairs=E, pairs_from_retrieval=int(sum(lc)),
+               threshold=thr, Q_conf=cfg["Q_conf"],
                valid_match_frac=vm_frac,
                match_frac_levels=int(len(levels)),
                matched_frac_median=float(np.median(np.minimum(fj, fi))))
     assert vm_frac > 0.5 and len(levels) > 1
-    assert 32 < n_before < NPAIRS
+    assert half < n_before < E
     for name in ("ii", "jj", "idx_ii2jj", "idx_jj2ii", "valid_match_j", "valid_match_i",
                  "Q_ii2jj", "Q_jj2ii"):
         got = getattr(graph, name).cpu().numpy()
