@@ -289,7 +289,7 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
     buf = slot[:, :128].view(cap, 64, 2)
     # block log (common.h M3sTlEnd): one record per block of every instrumented launch
     nlog = 1 << 21
-    blog = torch.zeros((nlog, 4), dtype=torch.int64, device=dev)
+    blog = torch.zeros((nlog, 8), dtype=torch.int64, device=dev)
     bcnt = torch.zeros(2, dtype=torch.int32, device=dev)
     slot[:, 128] = 0
     slot[:, 129] = bcnt.data_ptr()

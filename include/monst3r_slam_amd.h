@@ -50,7 +50,7 @@ int m3s_device_count(void);
  * [min of the starts, max of the ends]; the caller fills every pair with {UINT64_MAX, 0}
  * before a run; then a 4-u64 header {block-log buffer or 0, pointer to its u32 record
  * counter, capacity in records, 0}: when set, the first wave of every block appends
- * {start, end, slot address, HW_ID | XCC_ID << 32} (4 u64) at the counter — the busy
+ * {start, end, slot address, HW_ID | XCC_ID << 32, 4 phase marks} (8 u64) at the counter — the busy
  * intervals of every CU).  A null d_buf
  * disarms it (later launches carry no slot).  m3s_timeline_count() = slots taken since the
  * last set; m3s_timeline_meta() copies their kinds (1 GEMM, 2 attention, 3 implicit 3x3

@@ -51,8 +51,10 @@ __device__ __forceinline__ double m3s_wave_sum_d(double v) {
 // is null and the kernels only test it.
 // A slot is M3S_TL_SLOT u64: the M3S_TL_SUB pairs, then a header the host fills before a
 // replay — [0] a block-log buffer or 0, [1] its u32 record counter, [2] its capacity in
-// records — through which the first wave of every block appends one 32-B record {start,
-// end, slot address, HW_ID | XCC_ID << 32} (bench.step_timeline: which CUs are busy when).
+// records — through which the first wave of every block appends one 64-B record {start,
+// end, slot address, HW_ID | XCC_ID << 32, phase marks 0-3} (bench.step_timeline: which
+// CUs are busy when; the GEMM marks prologue issued / first K-tile ready / K-loop done /
+// epilogue tile in LDS, s_memrealtime, 0 where a kernel sets none).
 enum { M3S_TL_GEMM = 1, M3S_TL_ATTN = 2, M3S_TL_CONV = 3 };  // CONV: implicit 3x3 GEMM
 #define M3S_TL_SUB 64
 #define M3S_TL_SLOT (2 * M3S_TL_SUB + 4)
@@ -69,8 +71,13 @@ __device__ __forceinline__ void m3s_tl_begin(unsigned long long* tl) {
 struct M3sTlEnd {  // stamps the wave's end on every return path
   unsigned long long* p;
   unsigned long long t0;
+  unsigned long long ph[4] = {0ull, 0ull, 0ull, 0ull};
   __device__ __forceinline__ M3sTlEnd(unsigned long long* slot)
       : p(slot), t0(slot ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull) {}
+  // phase mark i (block log only; wave-uniform branch, nothing when the timeline is off)
+  __device__ __forceinline__ void mark(int i) {
+    if (p) ph[i] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+  }
   __device__ __forceinline__ ~M3sTlEnd() {
     if (p && (threadIdx.x & 63) == 0) {
       const unsigned long long now = (unsigned long long)__builtin_amdgcn_s_memrealtime();
@@ -84,10 +91,12 @@ struct M3sTlEnd {  // stamps the wave's end on every return path
           unsigned hw, xcc;
           asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
           asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-          ulonglong2* r = reinterpret_cast<ulonglong2*>(log + 4 * (size_t)i);
+          ulonglong2* r = reinterpret_cast<ulonglong2*>(log + 8 * (size_t)i);
           r[0] = make_ulonglong2(t0, now);
           r[1] = make_ulonglong2(reinterpret_cast<unsigned long long>(p),
                                  (unsigned long long)hw | ((unsigned long long)xcc << 32));
+          r[2] = make_ulonglong2(ph[0], ph[1]);
+          r[3] = make_ulonglong2(ph[2], ph[3]);
         }
       }
     }

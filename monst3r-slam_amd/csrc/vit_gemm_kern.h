@@ -400,7 +400,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
   constexpr int NT = WM * WN * 64;            // 4 waves (8: two per SIMD, see T128W8)
   M3S_T(t_start);
   m3s_tl_begin(a.tl);
-  const M3sTlEnd tl_end{a.tl};
+  M3sTlEnd tl_end{a.tl};
 #ifdef M3S_GEMM_STAMPS
   const long long rt_start = (long long)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -563,6 +563,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
   for (int s = 0; s < STAGES - 1; s++)
     if (s < nk) issue(kbase + s, s);
   M3S_T(t_pro);
+  tl_end.mark(0);
 #ifdef M3S_GEMM_STAMPS
   long long s_wait = 0, s_bar = 0, s_comp = 0;
 #endif
@@ -638,6 +639,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
     read_frags(0, lds, 0);
   }
   M3S_T(t_first);
+  tl_end.mark(1);
 
   const int nsteady = nk - (STAGES - 1);      // kt < nsteady: tile kt+STAGES-1 exists
   int kt = 0;
@@ -701,6 +703,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
     }
   }
   M3S_T(t_loop);
+  tl_end.mark(2);
   if constexpr (F8) {  // dequant: acc(i, j) *= col_scale[n] (n = this lane's column)
     const float* cs_g = a.cscale + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sCscale;
 #pragma unroll
@@ -828,6 +831,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
       }
   block_sync_lds();
   M3S_T(t_e2);
+  tl_end.mark(3);
 
   if constexpr (EPI >= 0 && (EPI & M3S_EPI_DPT_OUT) != 0) {
     // fused DPT tail: one pixel (row) per thread, all BN = 128 channels in the LDS tile

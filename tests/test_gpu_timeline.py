@@ -27,9 +27,10 @@ def test_timeline_records_every_launch(dev):
     buf = slot[:, :128].view(cap, 64, 2)
     buf[..., 0] = -1
     buf[..., 1] = 0
-    # block log: one 4-u64 record per block {start, end, slot address, HW_ID | XCC_ID << 32}
+    # block log: one 8-u64 record per block {start, end, slot address, HW_ID | XCC_ID << 32,
+    # GEMM phase marks}
     nlog = 1 << 16
-    blog = torch.zeros((nlog, 4), dtype=torch.int64, device=dev)
+    blog = torch.zeros((nlog, 8), dtype=torch.int64, device=dev)
     bcnt = torch.zeros(2, dtype=torch.int32, device=dev)
     slot[:, 128] = blog.data_ptr()
     slot[:, 129] = bcnt.data_ptr()
@@ -81,4 +82,15 @@ def test_timeline_records_every_launch(dev):
     xcc = (lg[:, 3] >> 32) & 0xF
     assert xcc.max() <= 7
     assert set(np.unique(sl)) == set(range(n))      # no launch without a block record
+    # GEMM blocks carry their phase marks in order: prologue issued <= first K-tile ready <=
+    # K-loop done <= epilogue tile in LDS, inside the block's lifetime; attention blocks none
+    kk = k[np.clip(sl, 0, n - 1)]
+    gm = lg[kk != 2]
+    ph = gm[:, 4:8]
+    assert (ph[:, :3] > 0).all()           # (split-K slices that are not the last skip mark 3)
+    assert (gm[:, 0] <= ph[:, 0]).all() and (np.diff(ph[:, :3], axis=1) >= 0).all()
+    full = ph[:, 3] > 0
+    assert full.mean() > 0.5 and (ph[full, 3] >= ph[full, 2]).all()
+    assert (ph[full, 3] <= gm[full, 1]).all()
+    assert (lg[kk == 2][:, 4:8] == 0).all()
 

@@ -43,6 +43,12 @@ cap_slots = 256
 slot = torch.empty((cap_slots, 132), dtype=torch.int64, device=dev)
 tl = slot[:, :128].view(cap_slots, 64, 2)
 slot[:, 128:] = 0
+nlog = 1 << 16
+blog = torch.zeros((nlog, 8), dtype=torch.int64, device=dev)
+bcnt = torch.zeros(2, dtype=torch.int32, device=dev)
+slot[:, 128] = blog.data_ptr()
+slot[:, 129] = bcnt.data_ptr()
+slot[:, 130] = nlog
 
 
 def capture(fn, st, timeline=False):
@@ -84,9 +90,13 @@ graphs = {"hot": capture(chain(False), s1, True), "cold": capture(chain(True), s
 g_heavy, g_tiny = capture(heavy, s2), capture(tinies, s2)
 
 
-def run(which, other):
+phases = {}
+
+
+def run(which, other, name=None):
     tl[..., 0] = -1
     tl[..., 1] = 0
+    bcnt.zero_()
     torch.cuda.synchronize()
     if other is not None:
         with torch.cuda.stream(s2):
@@ -97,6 +107,14 @@ def run(which, other):
     with torch.cuda.stream(s1):
         graphs[which].replay()
     torch.cuda.synchronize()
+    lg = blog[:min(int(bcnt[0]), nlog)].cpu().numpy().astype(np.float64)
+    ph = lg[:, 4:8]
+    ok = (ph > 0).all(1)
+    x, ph = lg[ok], ph[ok]
+    if name is not None and len(x):
+        phases[name] = ((x[:, 1] - x[:, 0]).mean() * 1e-2, (ph[:, 0] - x[:, 0]).mean() * 1e-2,
+                        (ph[:, 1] - ph[:, 0]).mean() * 1e-2, (ph[:, 2] - ph[:, 1]).mean() * 1e-2,
+                        (x[:, 1] - ph[:, 2]).mean() * 1e-2)
     t = tl[:REP].cpu().numpy()
     st = np.where(t[..., 0] > 0, t[..., 0], np.iinfo(np.int64).max).min(1)
     en = t[..., 1].max(1)
@@ -108,8 +126,12 @@ cases = [("alone", "hot", None), ("cold", "cold", None), ("tiny", "hot", "tiny")
 res = {name: [] for name, _, _ in cases}
 for _ in range(3):
     for name, which, other in cases:
-        res[name].append(run(which, other))
+        res[name].append(run(which, other, name))
 fl = 2.0 * M * N * K * B
 line = " | ".join(f"{k} {sorted(v)[1]:.1f}" for k, v in res.items())
 print(f"GEMM [{M},{N},{K},x{B}] launch span us (in-kernel stamps, median): {line}  "
       f"(alone = {fl / sorted(res['alone'])[1] / 1e6:.0f} TF/s)", flush=True)
+for k, v in phases.items():
+    print(f"   {k:11s} block life {v[0]:6.2f} us = prologue {v[1]:5.2f} + first tile {v[2]:5.2f} + "
+          f"K-loop {v[3]:6.2f} + epilogue {v[4]:5.2f}", flush=True)
+
