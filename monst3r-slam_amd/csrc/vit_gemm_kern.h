@@ -414,7 +414,9 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
   // __shared__ object made hipcc wait vmcnt(0) before the LDS reads of every MFMA phase in
   // the SPLIT instantiations — the DMA ring drained 4x per K-tile (cdna_hip_programming.md
   // §5 'Projection GEMM at M = 256' item 4(a)); measured as split-K K-tiles 2.4x slower
-  __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES + 16];
+  // (+ the DPT tail's 1x1 weights and conv bias, staged once per block: DPT_OUT below)
+  constexpr bool DPT = EPI >= 0 && (EPI & M3S_EPI_DPT_OUT) != 0;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES + 16 + (DPT ? 640 * 4 : 0)];
 
   // 1-D grid over (batch x split) groups x tiles.  Workgroups are dispatched to the 8
   // XCDs round-robin by linear id; the bijective remap gives each XCD a contiguous range
@@ -809,6 +811,16 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
   };
   if (!SPLIT) epi_setup(false);   // split-K: only the tile's last split needs the operands
   float* cs = reinterpret_cast<float*>(lds);
+  // DPT tail operands: w4 [4][128] then the conv bias [128] (zeros without BIAS), requested
+  // now and written beside the tile after the K-loop's last LDS reads
+  float4 dpt_stage = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (DPT) {
+    const int gw = a.wmod > 0 ? g % a.wmod : g;
+    if (tid < 128)
+      dpt_stage = reinterpret_cast<const float4*>(a.dpt_w4 + (int64_t)gw * 512)[tid];
+    else if (tid < 160 && (EPI & M3S_EPI_BIAS))
+      dpt_stage = reinterpret_cast<const float4*>(a.bias + (int64_t)gw * a.sBias)[tid - 128];
+  }
 #pragma unroll
   for (int pass = 0; pass < PASSES; pass++) {
   rb = pass * EROWS;
@@ -829,49 +841,76 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
         if (PASSES == 1 || wm == pass)
           cs[row * C::CST + wn * (BN / WN) + j * 32 + fr] = acc[i][j][r];
       }
+  if constexpr (DPT) {
+    if (tid < 160)
+      reinterpret_cast<float4*>(lds + C::LDS_BYTES + 16)[tid] = dpt_stage;
+  }
   block_sync_lds();
   M3S_T(t_e2);
   tl_end.mark(3);
 
-  if constexpr (EPI >= 0 && (EPI & M3S_EPI_DPT_OUT) != 0) {
-    // fused DPT tail: one pixel (row) per thread, all BN = 128 channels in the LDS tile
+  if constexpr (DPT) {
+    // fused DPT tail, all BN = 128 channels of a pixel (row) in the LDS tile: TPR threads
+    // per row (every thread of the block busy: 2-4 per row) each take 32 / TPR of the
+    // row's 4-channel groups — group q = (k % G) + G·h + 16·(k / G), G = 16 / TPR, so the
+    // 16 lanes of one ds_read_b128 hit 16 different bank quads — against the 1x1 weights
+    // and bias staged in LDS (broadcast reads), then the TPR partial sums meet by lane
+    // shuffle.  (One row per thread with the weights read from global memory took 8.8 us
+    // of a 27 us head.2 block in the C3 step: the block log, round 5.)
     static_assert(BN == 128 && !SPLIT && PASSES == 1,
                   "DPT_OUT needs the full 128-channel row in one tile");
+    constexpr int TPR = NT >= BM ? NT / BM : 1;
+    static_assert(TPR == 1 || TPR == 2 || TPR == 4 || TPR == 8, "threads per row");
+    constexpr int G = 16 / (TPR > 16 ? 16 : TPR);
     const int gw = a.wmod > 0 ? g % a.wmod : g;
-    const float* w4 = a.dpt_w4 + (int64_t)gw * 512;
     const float* b4 = a.dpt_b4 + (int64_t)gw * 4;
-    const float* cb = (EPI & M3S_EPI_BIAS) ? a.bias + (int64_t)gw * a.sBias : nullptr;
-    for (int row = tid; row < BM; row += NT) {
+    const float b40 = b4[0], b41 = b4[1], b42 = b4[2], b43 = b4[3];
+    const float* wl = reinterpret_cast<const float*>(lds + C::LDS_BYTES + 16);
+    const float* bl = wl + 512;
+    const int h = tid % TPR;
+    for (int row = tid / TPR; row < BM; row += NT / TPR) {
       const int m = m0 + row;
-      if (m >= a.M) break;
-      float o4[4] = {b4[0], b4[1], b4[2], b4[3]};
+      float o4[4] = {0.f, 0.f, 0.f, 0.f};
       const float* src = cs + row * C::CST;
-#pragma unroll 4
-      for (int c = 0; c < 128; c += 4) {
+#pragma unroll 8
+      for (int k = 0; k < 32 / TPR; k++) {
+        const int c = 4 * ((k % G) + G * h + 16 * (k / G));
         float4 x = *reinterpret_cast<const float4*>(src + c);
-        if (cb) {
-          x.x += cb[c];
-          x.y += cb[c + 1];
-          x.z += cb[c + 2];
-          x.w += cb[c + 3];
+        if constexpr ((EPI & M3S_EPI_BIAS) != 0) {
+          const float4 bb = *reinterpret_cast<const float4*>(bl + c);
+          x.x += bb.x;
+          x.y += bb.y;
+          x.z += bb.z;
+          x.w += bb.w;
         }
         x.x = fmaxf(x.x, 0.f);
         x.y = fmaxf(x.y, 0.f);
         x.z = fmaxf(x.z, 0.f);
         x.w = fmaxf(x.w, 0.f);
 #pragma unroll
-        for (int oo = 0; oo < 4; oo++)
-          o4[oo] += w4[oo * 128 + c] * x.x + w4[oo * 128 + c + 1] * x.y +
-                    w4[oo * 128 + c + 2] * x.z + w4[oo * 128 + c + 3] * x.w;
+        for (int oo = 0; oo < 4; oo++) {
+          const float4 w = *reinterpret_cast<const float4*>(wl + oo * 128 + c);
+          o4[oo] += w.x * x.x + w.y * x.y + w.z * x.z + w.w * x.w;
+        }
       }
-      // reg_dense_depth('exp') + conf ('exp', conf_min): as dpt_out_kernel (vit_misc.hip)
-      const float d = sqrtf(o4[0] * o4[0] + o4[1] * o4[1] + o4[2] * o4[2]);
-      const float sc = expm1f(d) / fmaxf(d, 1e-8f);
-      float* P = a.dpt_pts + ((int64_t)g * a.M + m) * 3;
-      P[0] = o4[0] * sc;
-      P[1] = o4[1] * sc;
-      P[2] = o4[2] * sc;
-      a.dpt_conf[(int64_t)g * a.M + m] = a.dpt_conf_min + expf(o4[3]);
+#pragma unroll
+      for (int off = 1; off < TPR; off <<= 1)
+#pragma unroll
+        for (int oo = 0; oo < 4; oo++) o4[oo] += __shfl_xor(o4[oo], off, 64);
+      if (h == 0 && m < a.M) {
+        o4[0] += b40;
+        o4[1] += b41;
+        o4[2] += b42;
+        o4[3] += b43;
+        // reg_dense_depth('exp') + conf ('exp', conf_min): as dpt_out_kernel (vit_misc.hip)
+        const float d = sqrtf(o4[0] * o4[0] + o4[1] * o4[1] + o4[2] * o4[2]);
+        const float sc = expm1f(d) / fmaxf(d, 1e-8f);
+        float* P = a.dpt_pts + ((int64_t)g * a.M + m) * 3;
+        P[0] = o4[0] * sc;
+        P[1] = o4[1] * sc;
+        P[2] = o4[2] * sc;
+        a.dpt_conf[(int64_t)g * a.M + m] = a.dpt_conf_min + expf(o4[3]);
+      }
     }
     return;
   }
