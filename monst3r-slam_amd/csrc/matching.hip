@@ -316,6 +316,113 @@ __global__ __launch_bounds__(kBlock) void refine_matches_r_kernel(
   p1_new[2 * q + 1] = v_new;
 }
 
+// The same search with the window's columns split over lanes (round 5): lane ii of a group
+// of 2R+1 lanes scores window column ii (its 2R+1 candidates, 3(2R+1) 16-B loads in flight)
+// for one query, and the group merges the columns in the reference's visiting order.  The
+// one-lane kernel above runs 3 waves per SIMD over 49 dependent candidate columns per
+// query and stalls on the texture path; here a wave covers 9 queries (63 lanes, the last
+// lane idle), 7x the waves for the same work.  Arithmetic per candidate is unchanged (each
+// lane runs the full 24-term f16 chain); the merge is exact:
+//   the sequential scan with strict > ends each dilation on the FIRST candidate holding the
+//   window maximum, if that maximum beats the running max_score.  Lane ii scans its column
+//   from the dilation's starting max_score, so it holds the column's first maximum (or
+//   nothing); folding the columns in order ii = 0..2R with strict > then picks the same
+//   candidate.  A column whose maximum does not beat the running value changes nothing in
+//   either form.
+// Every lane of a group computes the merge (7 shuffles of score and row), so the group
+// agrees on (u0, v0) for the next dilation without a broadcast.
+template <int R>
+__global__ __launch_bounds__(kBlock) void refine_matches_c_kernel(
+    const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
+    const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
+    int dilation_max) {
+  constexpr int S = 2 * R + 1;
+  constexpr int QW = 64 / S;                 // queries per wave
+  constexpr int QB = QW * (kBlock / 64);     // queries per workgroup
+  const int n = h * w;
+  const int nblk = (n + QB - 1) / QB;
+  const int lin = blockIdx.x, xcd = lin & 7, loc = lin >> 3;
+  const int tq = nblk >> 3, tr = nblk & 7;
+  const int t = xcd < tr ? xcd * (tq + 1) + loc : tr * (tq + 1) + (xcd - tr) * tq + loc;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int grp = lane / S, ii = lane - grp * S, base = grp * S;
+  // every lane takes part in the shuffles: the idle lane and queries past the end run a
+  // clamped query and store nothing
+  const int qi = t * QB + wv * QW + grp;
+  const bool qok = grp < QW && qi < n;
+  const int64_t q = (int64_t)blockIdx.y * n + min(qi, n - 1);
+  _Float16 qd[24];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(D21 + q * 24);
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      uint4 v = src[c];
+      __builtin_memcpy(&qd[8 * c], &v, 16);
+    }
+  }
+  const uint4* img = reinterpret_cast<const uint4*>(D11 + (int64_t)blockIdx.y * n * 24);
+  // the reference's coordinates are int64; h*w < 2^31 (host check) keeps in-image ones in
+  // int; a start point beyond +-2^30 has no in-image candidate at any dilation, so it
+  // never moves and the int arithmetic below stays clear of overflow
+  const int64_t u0_64 = p1[2 * q + 0], v0_64 = p1[2 * q + 1];
+  const bool far = u0_64 < -(1LL << 30) || u0_64 > (1LL << 30) || v0_64 < -(1LL << 30) ||
+                   v0_64 > (1LL << 30);
+  int u0 = far ? 0 : (int)u0_64;
+  int v0 = far ? 0 : (int)v0_64;
+  _Float16 max_score = (_Float16)0.0f;
+  bool moved = false;
+  for (int d = dilation_max; d > 0; d--) {
+    const int rd = R * d;
+    const int u = u0 - rd + ii * d;
+    const bool uok = !far && u >= 0 && u < w;
+    uint4 buf[S][3];
+    bool ok[S];
+#pragma unroll
+    for (int jj = 0; jj < S; jj++) {
+      const int v = v0 - rd + jj * d;
+      ok[jj] = uok && v >= 0 && v < h;
+      const int off = ok[jj] ? v * w + u : 0;
+#pragma unroll
+      for (int c = 0; c < 3; c++) buf[jj][c] = img[off * 3 + c];
+    }
+    _Float16 best = max_score;
+    int bj = -1;
+#pragma unroll
+    for (int jj = 0; jj < S; jj++) {
+      _Float16 cd[24];
+      __builtin_memcpy(cd, buf[jj], 48);
+      const _Float16 score = desc_score<24>(qd, cd, 24);
+      if (ok[jj] && (float)score > (float)best) {
+        best = score;
+        bj = jj;
+      }
+    }
+    // merge the group's columns in visiting order
+    const int mine = (int)__builtin_bit_cast(unsigned short, best) | ((bj + 1) << 16);
+    int pick_i = -1, pick_j = -1;
+#pragma unroll
+    for (int k = 0; k < S; k++) {
+      const int o = __shfl(mine, base + k);
+      const int oj = (o >> 16) - 1;
+      const _Float16 os = __builtin_bit_cast(_Float16, (unsigned short)(o & 0xFFFF));
+      if (oj >= 0 && (float)os > (float)max_score) {
+        max_score = os;
+        pick_i = k;
+        pick_j = oj;
+      }
+    }
+    if (pick_i >= 0) {
+      u0 = u0 - rd + pick_i * d;
+      v0 = v0 - rd + pick_j * d;
+      moved = true;
+    }
+  }
+  if (qok && ii == 0) {
+    p1_new[2 * q + 0] = moved ? (int64_t)u0 : u0_64;
+    p1_new[2 * q + 1] = moved ? (int64_t)v0 : v0_64;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // prep_for_iter_proj (matching.py:25-49) + img_gradient (image.py:5-38), fused.
 // ---------------------------------------------------------------------------
@@ -450,6 +557,15 @@ extern "C" int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21,
   static const char* kind = getenv("M3S_REFINE_KERNEL");
   static const bool rows = kind && !strcmp(kind, "rows");
   static const bool tile = kind && !strcmp(kind, "tile");
+  static const bool lane1 = kind && !strcmp(kind, "lane");  // the one-lane radius-3 kernel
+  if (fdim == 24 && aligned && n == h * w && radius == 3 && h * w < (1LL << 31) && !rows &&
+      !tile && !lane1) {
+    dim3 gridq((unsigned)m3s_div_up(h * w, (64 / 7) * (kBlock / 64)), (unsigned)b);
+    hipLaunchKernelGGL(refine_matches_c_kernel<3>, gridq, dim3(kBlock), 0, m3s_stream(stream),
+                       D11, D21, d_p1, d_p1_new, (int)h, (int)w, dilation_max);
+    M3S_LAUNCH_CHECK();
+    return M3S_OK;
+  }
   if (fdim == 24 && aligned && n == h * w && radius == 3 && h * w < (1LL << 31) && !rows &&
       !tile) {
     dim3 grid2((unsigned)(m3s_div_up(w, 16) * m3s_div_up(h, 16)), (unsigned)b);

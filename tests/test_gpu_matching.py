@@ -73,16 +73,22 @@ def test_refine_matches_scattered(oracle, dev, radius, dmax):
     np.testing.assert_array_equal(got.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("case", ["outliers", "shifted", "wide_jitter"])
+@pytest.mark.parametrize("case", ["outliers", "shifted", "wide_jitter", "ties", "off_image"])
 def test_refine_matches_match_fields(oracle, dev, case):
     """Radius-3 refine on match fields between the smooth and the scattered tests: smooth
     matches with 2 % scattered outliers (a tile's windows both local and spread over the
-    image), a large shift (windows cut by the image edges) and +-12 px jitter (a tile's
-    windows wider than at +-4) — bit-exact against the oracle."""
+    image), a large shift (windows cut by the image edges), +-12 px jitter (a tile's
+    windows wider than at +-4), descriptors on a coarse grid (many equal scores: the first
+    maximum in visiting order must win, across the window columns the column-split kernel
+    merges) and start points off the image (unclamped, out to +-2^40) — bit-exact against
+    the oracle."""
     import mast3r_slam_backends as mb
-    rng = np.random.default_rng({"outliers": 21, "shifted": 22, "wide_jitter": 23}[case])
+    rng = np.random.default_rng({"outliers": 21, "shifted": 22, "wide_jitter": 23, "ties": 24,
+                                 "off_image": 25}[case])
     b, h, w = 2, 96, 160
     d11 = rng.normal(size=(b, h, w, 24)).astype(np.float16)
+    if case == "ties":
+        d11 = (np.sign(d11) * (np.abs(d11) > 0.8)).astype(np.float16) * np.float16(0.25)
     d21 = rng.normal(size=(b, h * w, 24)).astype(np.float16)
     yy, xx = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
     p1 = np.stack([xx, yy], -1).reshape(1, -1, 2).repeat(b, 0).astype(np.int64)
@@ -92,9 +98,17 @@ def test_refine_matches_match_fields(oracle, dev, case):
         p1[out] = rng.integers(0, [w, h], size=(int(out.sum()), 2))
     elif case == "shifted":
         p1 += np.array([37, -21]) + rng.integers(-2, 3, p1.shape)
-    else:
+    elif case == "wide_jitter":
         p1 += rng.integers(-12, 13, p1.shape)
-    p1 = np.clip(p1, 0, [w - 1, h - 1]).astype(np.int64)
+    else:
+        p1 += rng.integers(-3, 4, p1.shape)
+    if case == "off_image":
+        p1 += rng.integers(-20, 21, p1.shape)        # up to 20 px off every edge, unclamped
+        far = rng.uniform(size=p1.shape[:2]) < 0.01
+        p1[far] = rng.choice([-(1 << 40), -(1 << 31), 1 << 31, 1 << 40], size=(int(far.sum()), 2))
+    else:
+        p1 = np.clip(p1, 0, [w - 1, h - 1])
+    p1 = p1.astype(np.int64)
     ref = oracle.refine_matches(d11, d21, p1, 3, 5)
     (got,) = mb.refine_matches(_t(d11, dev), _t(d21, dev), _t(p1, dev), 3, 5)
     np.testing.assert_array_equal(got.cpu().numpy(), ref)
