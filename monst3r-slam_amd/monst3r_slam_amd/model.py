@@ -257,6 +257,53 @@ ENC_FP8 = ("qkv_w", "proj_w", "fc1_w", "fc2_w")
 DEC_FP8 = ("qkv_w", "proj_w", "q_w", "kv_w", "cproj_w", "fc1_w", "fc2_w")
 
 
+def _fp8_shifted_params(W, cal):
+    """Calibrated fp8 parameter copies (PairModel.calibrate_fp8): cal[(site, layer)] = the
+    per-channel mean of that e4m3 operand ([C] for the encoder, [Z, C] per decoder problem;
+    Z = 4 from the pair calibration).  Returns (encoder dict of [L, ...] stacks, decoder
+    list of per-layer dicts of [4, ...] stacks), f32."""
+    f64 = torch.float64
+    mv = lambda w, mu: torch.einsum("...nk,...k->...n", w.to(f64), mu)  # noqa: E731
+
+    def deq(q8, b):
+        q, sc = q8
+        return q.view(torch.float8_e4m3fn).to(f64) * sc.to(f64)[..., None] - b.to(f64)
+
+    L = W.arch.enc_depth
+    P, P8 = W.enc, W.enc8
+    st = lambda site: torch.stack([cal[(site, i)] for i in range(L)])  # noqa: E731
+    m1, ma, m2, mh = st("enc.ln1"), st("enc.att"), st("enc.ln2"), st("enc.hid")
+    E = m1.shape[-1]
+    enc = {"ln1_b": P["ln1_b"].to(f64) - m1, "ln2_b": P["ln2_b"].to(f64) - m2}
+    qkv_b = P["qkv_b"].to(f64) + mv(P["qkv_w"], m1)
+    qkv_b[:, 2 * E:] -= ma
+    enc["qkv_b"] = qkv_b
+    enc["proj_b"] = P["proj_b"].to(f64) + mv(P["proj_w"], ma)
+    enc["fc1_b"] = P["fc1_b"].to(f64) + mv(P["fc1_w"], m2)
+    enc["fc2_b"] = P["fc2_b"].to(f64) - mv(deq(P8["fc2_w"], P["fc2_w"]), mh)
+    enc = {k: v.float().contiguous() for k, v in enc.items()}
+    dec = []
+    for i, (P, P8) in enumerate(zip(W.dec, W.dec8)):
+        m1, ma, my, m2, mc, m3, mh = (cal[(s, i)] for s in (
+            "dec.ln1", "dec.att", "dec.lny", "dec.ln2", "dec.catt", "dec.ln3", "dec.hid"))
+        D = m1.shape[-1]
+        d = {"ln1_b": P["ln1_b"].to(f64) - m1, "lny_b": P["lny_b"].to(f64) - my,
+             "ln2_b": P["ln2_b"].to(f64) - m2, "ln3_b": P["ln3_b"].to(f64) - m3}
+        qkv_b = P["qkv_b"].to(f64) + mv(P["qkv_w"], m1)
+        qkv_b[:, 2 * D:] -= ma
+        d["qkv_b"] = qkv_b
+        d["proj_b"] = P["proj_b"].to(f64) + mv(P["proj_w"], ma)
+        kv_b = P["kv_b"].to(f64) + mv(P["kv_w"], my)
+        kv_b[:, D:] -= mc
+        d["kv_b"] = kv_b
+        d["q_b"] = P["q_b"].to(f64) + mv(P["q_w"], m2)
+        d["cproj_b"] = P["cproj_b"].to(f64) + mv(P["cproj_w"], mc)
+        d["fc1_b"] = P["fc1_b"].to(f64) + mv(P["fc1_w"], m3)
+        d["fc2_b"] = P["fc2_b"].to(f64) - mv(deq(P8["fc2_w"], P["fc2_w"]), mh)
+        dec.append({k: v.float().contiguous() for k, v in d.items()})
+    return enc, dec
+
+
 class PackedWeights:
     """Device weights.  Encoder from MonST3R; decoders and heads stacked over
     z = model*2 + side (model 0 = MonST3R, 1 = MASt3R; side 0 = dec_blocks/head1,
@@ -385,6 +432,8 @@ class PackedWeights:
         self.lf_fc2_w = bf(torch.stack([sd_mast3r[f"{h}.head_local_features.fc2.weight"] for h in lf]))
         self.lf_fc2_b = f32(torch.stack([sd_mast3r[f"{h}.head_local_features.fc2.bias"] for h in lf]))
         self.enc8 = self.dec8 = None
+        self.fp8_shift_enc, self.fp8_shift_dec = {}, [{} for _ in self.dec]
+        self.fp8_calibrated = False
 
     def enable_fp8(self):
         """e4m3 copies (+ per-row scales) of the encoder / decoder transformer weights,
@@ -468,14 +517,78 @@ class PairModel:
         self._ev_heads = None
         self.head_aux = None  # stream for the DPT heads' off-chain branches (_head_aux)
 
-    def set_fp8(self, on=True):
+    def set_fp8(self, on=True, calibrate=True):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
         operands on the scaled MFMA — LayerNorm, attention and the fc1 GELU epilogue emit
         e4m3 activations (unscaled, saturated to ±448), weights are per-row scaled, the
-        residual stream stays f32 and q/k/v stay bf16 (attention runs in bf16)."""
+        residual stream stays f32 and q/k/v stay bf16 (attention runs in bf16).
+        calibrate: on first use, per-channel activation shifts and bias correction from two
+        synthetic calibration frames (calibrate_fp8)."""
         if on:
             self.w.enable_fp8()
         self.fp8 = bool(on)
+        if on and calibrate and not self.w.fp8_calibrated:
+            self.calibrate_fp8()
+
+    def calibrate_fp8(self, hw=(512, 512), frames=2, seed=100):
+        """Static per-channel calibration of the fp8 path (round 5; tools/fp8_error_budget.py,
+        tools/fp8_mono_diag.py).  The e4m3 errors are not noise: a channel whose activation
+        sits near a constant over all tokens rounds the same way in every token, and a
+        quantised weight row meets the same per-channel input mean in every token, so both
+        errors come out as a per-channel offset of the features (88 % of the fp8 encoder's
+        feature error energy at 512x512).  Measured means mu (over the tokens of `frames`
+        uniform-noise frames, seeds `seed`.., never the test frames) are folded into
+        parameters — no kernel changes:
+          LayerNorm -> GEMM   beta' = beta - mu, b' = b + W mu (the e4m3 operand carries
+                              x - mu; W exact)
+          attention -> proj   the v bias - mu (softmax rows sum to 1, so the output shifts
+                              by -mu), b' = b + W mu
+          GELU -> fc2         b' = b - (Wq - W) mu (bias correction of the quantised rows)
+        In the fake-quant restatement: X median 5.5 % -> 1.9 %, feature cosine 0.99597 ->
+        0.99936 (mono 512x512)."""
+        W, dev = self.w, self.dev
+        was = self.fp8
+        self.fp8 = True
+        W.fp8_shift_enc, W.fp8_shift_dec = {}, [{} for _ in W.dec]   # plain biases first
+        self._cal = {}
+        try:
+            gen = torch.Generator(device=dev).manual_seed(seed)
+            img = torch.rand(frames, 3, hw[0], hw[1], device=dev, generator=gen) * 2 - 1
+            feat, _ = self.encode(img)
+            gh, gw = hw[0] // self.a.patch, hw[1] // self.a.patch
+            f = feat.reshape(frames, gh * gw, self.a.enc_dim)
+            # pairs (frame k, frame k+1): both models, both sides
+            self.decode_multi(f.contiguous(), f.roll(1, 0).contiguous(), gh, gw)
+            torch.cuda.synchronize(dev)
+            cal = {k: (v / n) for k, (v, n) in self._cal.items()}
+        finally:
+            self._cal = None
+            self.fp8 = was
+        W.fp8_shift_enc, W.fp8_shift_dec = _fp8_shifted_params(W, cal)
+        W.fp8_calibrated = True
+
+    def _calib(self, site, i, t, z=None):
+        """Calibration hook: accumulate the per-channel mean of e4m3 operand t (rows ×
+        channels, or [Z, S, C] per problem z when z is given)."""
+        if getattr(self, "_cal", None) is None:
+            return
+        v = t.view(torch.float8_e4m3fn).double()
+        C = v.shape[-1]
+        if z is None:
+            m = v.reshape(-1, C).mean(0)
+        else:   # problems z = (g·models + model)·2 + side read weight stack z % wm
+            m = v.reshape(z, -1, C).mean(1).reshape(-1, self._wm, C).mean(0)
+        key = (site, i)
+        acc, n = self._cal.get(key, (0.0, 0))
+        self._cal[key] = (acc + m, n + 1)
+
+    def _pb(self, P, key, i=None, layer=None):
+        """Bias / LayerNorm beta `key`: the fp8 path's calibrated copy when fp8 is on."""
+        if self.fp8:
+            Q = self.w.fp8_shift_enc if layer is None else self.w.fp8_shift_dec[layer]
+            if key in Q:
+                return Q[key] if i is None else Q[key][i]
+        return P[key] if i is None else P[key][i]
 
     def _wt(self, P, P8, key, i=None, n=None):
         """(B operand, extra gemm kwargs) for weight `key` (layer i of a stacked pack, or
@@ -632,22 +745,27 @@ class PairModel:
                 o.gemm(hid, P["fc2_w"][j], x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][j], R=x,
                        tile=tiles.get("fc2"), **R32S)
                 yield i
+        pb = self._pb
         for i in (range(lo, hi) if not fold else ()):
-            o.ln(x, P["ln1_g"][i], P["ln1_b"][i], xn, M, E)
+            o.ln(x, P["ln1_g"][i], pb(P, "ln1_b", i), xn, M, E)
+            self._calib("enc.ln1", i, xn)
             # qkv projection with RoPE2D on q and k fused into the epilogue
             w, kw = self._wt(P, P8, "qkv_w", i)
-            o.gemm(xn, w, qkv, M, 3 * E, E, bias=P["qkv_b"][i], rope=(rt, 2 * E, S), **kw)
+            o.gemm(xn, w, qkv, M, 3 * E, E, bias=pb(P, "qkv_b", i), rope=(rt, 2 * E, S), **kw)
             o.attn(qkv, 3 * E, S * 3 * E, qkv[:, E:], qkv[:, 2 * E:], 3 * E, S * 3 * E, att, E,
                    S * E, B, a.enc_heads, S, S)
+            self._calib("enc.att", i, att)
             w, kw = self._wt(P, P8, "proj_w", i)
-            o.gemm(att, w, x, M, E, E, bias=P["proj_b"][i], R=x,
+            o.gemm(att, w, x, M, E, E, bias=pb(P, "proj_b", i), R=x,
                    flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, **kw)
-            o.ln(x, P["ln2_g"][i], P["ln2_b"][i], xn, M, E)
+            o.ln(x, P["ln2_g"][i], pb(P, "ln2_b", i), xn, M, E)
+            self._calib("enc.ln2", i, xn)
             w, kw = self._wt(P, P8, "fc1_w", i)
-            o.gemm(xn, w, hid, M, a.mlp_ratio * E, E, bias=P["fc1_b"][i],
+            o.gemm(xn, w, hid, M, a.mlp_ratio * E, E, bias=pb(P, "fc1_b", i),
                    flags=_lib.EPI_GELU, out_fp8=self.fp8, **kw)
+            self._calib("enc.hid", i, hid)
             w, kw = self._wt(P, P8, "fc2_w", i)
-            o.gemm(hid, w, x, M, E, a.mlp_ratio * E, bias=P["fc2_b"][i], R=x,
+            o.gemm(hid, w, x, M, E, a.mlp_ratio * E, bias=pb(P, "fc2_b", i), R=x,
                    flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, **kw)
             yield i
         if not end:
@@ -739,50 +857,58 @@ class PairModel:
             # side stream, overlapping the self-attention half of the layer (the side chain
             # must read x before this layer's first residual update writes it)
             w, kw = wt("kv_w", 2 * D)
+            pb = lambda key: self._pb(P, key, layer=i)  # noqa: E731
             if self.serial:
                 # norm1(x) and norm_y(other side's x) share the row statistics: one pass
-                o.ln_dual(x, P["ln1_g"], P["ln1_b"], xn, P["lny_g"], P["lny_b"], yn, S, D, Z,
+                o.ln_dual(x, P["ln1_g"], pb("ln1_b"), xn, P["lny_g"], pb("lny_b"), yn, S, D, Z,
                           S * D, S * D, D, pmod=wm)
+                self._calib("dec.lny", i, yn, Z)
                 o.gemm(yn, w, kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
-                       sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=wm, **kw)
+                       sC=S * 2 * D, bias=pb("kv_b"), sBias=2 * D, rope=(rt, D, S), wmod=wm, **kw)
                 ev_lny = ev_kv = None
             else:
                 with self._on(0):
-                    o.ln(x, P["lny_g"], P["lny_b"], yn, S, D, Z, S * D, S * D, D, xor=1, pmod=wm)
+                    o.ln(x, P["lny_g"], pb("lny_b"), yn, S, D, Z, S * D, S * D, D, xor=1, pmod=wm)
                     ev_lny = self._event()
                     o.gemm(yn, w, kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
-                           sC=S * 2 * D, bias=P["kv_b"], sBias=2 * D, rope=(rt, D, S), wmod=wm,
+                           sC=S * 2 * D, bias=pb("kv_b"), sBias=2 * D, rope=(rt, D, S), wmod=wm,
                            **kw)
                     ev_kv = self._event()
-                o.ln(x, P["ln1_g"], P["ln1_b"], xn, S, D, Z, S * D, S * D, D, pmod=wm)
+                o.ln(x, P["ln1_g"], pb("ln1_b"), xn, S, D, Z, S * D, S * D, D, pmod=wm)
+            self._calib("dec.ln1", i, xn, Z)
             # self-attention
             w, kw = wt("qkv_w", 3 * D)
             o.gemm(xn, w, qkv, S, 3 * D, D, Z, sA=S * D, sB=3 * D * D, sC=S * 3 * D,
-                   bias=P["qkv_b"], sBias=3 * D, rope=(rt, 2 * D, S), wmod=wm, **kw)
+                   bias=pb("qkv_b"), sBias=3 * D, rope=(rt, 2 * D, S), wmod=wm, **kw)
             o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,
                    D, S * D, Z, a.dec_heads, S, S)
+            self._calib("dec.att", i, att, Z)
             self._wait(ev_lny)
             w, kw = wt("proj_w", D)
-            o.gemm(att, w, x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["proj_b"],
+            o.gemm(att, w, x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=pb("proj_b"),
                    sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
             # cross-attention: q from norm2(x), k/v from y_
-            o.ln(x, P["ln2_g"], P["ln2_b"], xn, S, D, Z, S * D, S * D, D, pmod=wm)
+            o.ln(x, P["ln2_g"], pb("ln2_b"), xn, S, D, Z, S * D, S * D, D, pmod=wm)
+            self._calib("dec.ln2", i, xn, Z)
             w, kw = wt("q_w", D)
-            o.gemm(xn, w, q, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=P["q_b"],
+            o.gemm(xn, w, q, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=pb("q_b"),
                    sBias=D, rope=(rt, D, S), wmod=wm, **kw)
             self._wait(ev_kv)
             o.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, att, D, S * D, Z, a.dec_heads,
                    S, S)
+            self._calib("dec.catt", i, att, Z)
             w, kw = wt("cproj_w", D)
             o.gemm(att, w, x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D,
-                   bias=P["cproj_b"], sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
+                   bias=pb("cproj_b"), sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
             # MLP
-            o.ln(x, P["ln3_g"], P["ln3_b"], xn, S, D, Z, S * D, S * D, D, pmod=wm)
+            o.ln(x, P["ln3_g"], pb("ln3_b"), xn, S, D, Z, S * D, S * D, D, pmod=wm)
+            self._calib("dec.ln3", i, xn, Z)
             w, kw = wt("fc1_w", Dm)
-            o.gemm(xn, w, hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm, bias=P["fc1_b"],
+            o.gemm(xn, w, hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm, bias=pb("fc1_b"),
                    sBias=Dm, flags=_lib.EPI_GELU, wmod=wm, out_fp8=self.fp8, **kw)
+            self._calib("dec.hid", i, hid, Z)
             w, kw = wt("fc2_w", D)
-            o.gemm(hid, w, x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D, bias=P["fc2_b"],
+            o.gemm(hid, w, x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D, bias=pb("fc2_b"),
                    sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
             if (i + 1) in hk:
                 hb = self._buf(f"h{i + 1}", (Z, S, D), BF16)

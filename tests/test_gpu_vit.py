@@ -487,9 +487,11 @@ def test_attention_fp8_out(ops, dev, monkeypatch, splits):
 
 def test_fp8_model_vs_fp32_restatement_512(dev, parity_log):
     """the fp8 transformer path (e4m3 activations + per-row weight scales on
-    the scaled MFMA; heads in bf16) at 512x512 against the fp32 restatement.  Stated fp8
-    tolerances (looser than the bf16 path's in _compare_pair): pointmap median relative
-    error < 8 %, conf median < 8 %, descriptor median cosine > 0.97."""
+    the scaled MFMA, calibrated per-channel shifts / bias correction; heads in bf16) at
+    512x512 against the fp32 restatement.  Stated fp8 tolerances (looser than the bf16
+    path's in _compare_pair): pointmap median relative error < 6 %, conf median < 8 %,
+    descriptor median cosine > 0.97 and minimum > 0.98.  Measured round 5: X 2.85 %, D cos
+    min 0.9958 (5.86 % / 0.962 before the calibration)."""
     from monst3r_slam_amd import model as Mdl
     from oracle import vit_ref as V
     m, (sdm, am, sdM, aM) = Mdl.build(dev)
@@ -511,8 +513,8 @@ def test_fp8_model_vs_fp32_restatement_512(dev, parity_log):
                  D_cos_min=float(cos_D.min()), Q_med=float(rel_Q.median()))
     print("fp8-512-vs-fp32", stats)
     parity_log("fp8-512-vs-fp32", **stats)
-    assert stats["X_med"] < 0.08 and stats["C_med"] < 0.08, stats
-    assert stats["D_cos_med"] > 0.97 and stats["Q_med"] < 0.15, stats
+    assert stats["X_med"] < 0.06 and stats["C_med"] < 0.08, stats
+    assert stats["D_cos_med"] > 0.97 and stats["D_cos_min"] > 0.98 and stats["Q_med"] < 0.15, stats
     m.set_fp8(False)
 
 
@@ -520,11 +522,12 @@ def test_fp8_mono_512_vs_fp32_restatement(dev, parity_log):
     """SURVEY §8 C5's other decode: the MonST3R mono (self-pair) inference of a 512x512
     frame — the dyn-mask path's monst3r_inference_mono (monst3r_utils.py:187-211) — on the
     fp8 transformer path (encoder included) vs the fp32 restatement.  Stated tolerances:
-    C median relative error < 8 % as in the pair test; X median < 15 %: with random weights
-    the pointmap is a small residue (median |X| ~ 0.05) of the head's much larger terms, so
-    the fp8 encoder's error (feature cosine ~0.996) shows ~10x larger on X than on C — the
-    bf16 path measures 1.6 % / 0.03 % on the same frame (gpurun_out mono diagnostics,
-    DESIGN §fp8)."""
+    C median relative error < 8 % as in the pair test; X median < 10 %: with random weights
+    the pointmap is a small residue (median |X| ~ 0.06) of the head's much larger terms, so
+    a feature error shows ~10x larger on X than on C — the bf16 path measures 1.6 % / 0.03 %
+    on the same frame.  Round 5 (tools/fp8_mono_diag.py): the uncalibrated
+    fp8 encoder's feature error was 88 % a per-channel offset (X 14.5 %, feature cosine
+    0.996); with calibrate_fp8 X 3.7 %, feature cosine 0.9993."""
     from monst3r_slam_amd import model as Mdl
     from oracle import vit_ref as V
     m, (sdm, am, _, _) = Mdl.build(dev)
@@ -546,8 +549,8 @@ def test_fp8_mono_512_vs_fp32_restatement(dev, parity_log):
     stats = dict(feat_cos_med=float(cos_f.median()), X_med=float(rel_X.median()),
                  X_p99=float(rel_X.quantile(0.99)), C_med=float(rel_C.median()))
     parity_log("fp8-mono-512-vs-fp32", **stats)
-    assert stats["feat_cos_med"] > 0.99, stats
-    assert stats["X_med"] < 0.15 and stats["C_med"] < 0.08, stats
+    assert stats["feat_cos_med"] > 0.998, stats
+    assert stats["X_med"] < 0.10 and stats["C_med"] < 0.08, stats
 
 
 def test_split_heads_match_batched(dev):
