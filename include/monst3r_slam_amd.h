@@ -411,6 +411,12 @@ int m3s_copy_rows(const void* d_src, void* d_dst, int64_t rows, int64_t row_byte
  * optional d_add [B][oh][ow][C] is added (fuses the fusion block's skip add). C % 8 == 0. */
 int m3s_vit_upsample2x(const void* d_in, void* d_out, const void* d_add, int64_t batch,
                        int64_t h, int64_t w, int64_t c, int64_t oh, int64_t ow, void* stream);
+/* The same upsample with an OCP e4m3 output of v * inv_scale (d_out: uint8 [b][oh][ow][c]):
+ * the A operand of an fp8 implicit conv (C5 fp8 heads; the conv's per-column scales carry
+ * 1 / inv_scale).  inv_scale must be finite and > 0.  (ABI 0.3) */
+int m3s_vit_upsample2x_e4m3(const void* d_in, void* d_out, const void* d_add, int64_t batch,
+                            int64_t h, int64_t w, int64_t c, int64_t oh, int64_t ow,
+                            float inv_scale, void* stream);
 
 /* DPT regression head tail, fused: t = relu(conv3x3 output) [B][P][128] bf16 is reduced
  * by the final 1x1 conv (128 → 4, per-head W4 f32 [B][4][128], b4 [B][4]) and post-processed

@@ -112,8 +112,11 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     return M3S_ERR_INVALID_ARG;
   if (d->batch > 65535) return M3S_ERR_TOO_LARGE;
   const bool f8 = d->flags & M3S_IN_FP8;
-  if (f8 && (d->mode != 0 || d->K % 16 || d->lda % 16 || d->ldb % 16 || d->strideA % 16 ||
-             d->strideB % 16 || !d->col_scale || (d->flags & M3S_EPI_CONVT)))
+  // fp8 implicit conv (mode 1): e4m3 NHWC input whose channel count fills whole K-tiles in
+  // 2-byte units (Cin % 128); no ReLU prologue (the e4m3 fragments are not rectified)
+  if (f8 && (d->mode > 1 || (d->mode == 0 && d->lda % 16) || d->K % 16 || d->ldb % 16 ||
+             d->strideA % 16 || d->strideB % 16 || !d->col_scale ||
+             (d->flags & (M3S_EPI_CONVT | M3S_PRO_RELU)) || (d->mode == 1 && d->Cin % 128)))
     return M3S_ERR_INVALID_ARG;
   if ((d->flags & M3S_EPI_OUT_FP8) && (d->flags & M3S_EPI_OUT_F32)) return M3S_ERR_INVALID_ARG;
   // fp8 operands are addressed in 2-byte units (the bf16 kernel's byte layout, §F8)
@@ -121,7 +124,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   const int64_t eldb = f8 ? d->ldb / 2 : d->ldb;
   // buffer addressing: each operand's per-batch span must fit a 31-bit byte offset
   const int64_t spanA = d->mode == 0 ? ((int64_t)(d->M - 1) * elda + eK) * 2
-                                     : (int64_t)d->Hin * d->Win * d->Cin * 2;
+                                     : (int64_t)d->Hin * d->Win * (f8 ? d->Cin / 2 : d->Cin) * 2;
   const int64_t spanB = ((int64_t)(d->N - 1) * eldb + eK) * 2;
   if (spanA >= NUM_RECORDS || spanB >= NUM_RECORDS) return M3S_ERR_TOO_LARGE;
   Args a;
@@ -196,6 +199,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     a.ldb = eldb;
     a.sA = d->strideA / 2;
     a.sB = d->strideB / 2;
+    a.Cin = d->Cin / 2;
   }
   const bool out32 = d->flags & M3S_EPI_OUT_F32;
   const bool has_bias = d->bias && (d->flags & M3S_EPI_BIAS);
@@ -208,7 +212,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   if ((ln_stats || ln_fold) && !a.vec) return M3S_ERR_INVALID_ARG;
   if (d->flags & M3S_EPI_DPT_OUT) {
     // compiled only as the conv variant BIAS? | RELU | DPT_OUT on the 8-wide vector path
-    const int rest = d->flags & ~(M3S_EPI_DPT_OUT | M3S_EPI_RELU | M3S_EPI_BIAS);
+    const int rest = d->flags & ~(M3S_EPI_DPT_OUT | M3S_EPI_RELU | M3S_EPI_BIAS | M3S_IN_FP8);
     if (d->mode != 1 || d->N != 128 || rest != 0 || !(d->flags & M3S_EPI_RELU) || !a.vec ||
         !d->dpt_w4 || !d->dpt_b4 || !d->dpt_pts || !d->dpt_conf)
       return M3S_ERR_INVALID_ARG;

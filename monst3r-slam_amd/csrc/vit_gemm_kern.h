@@ -1209,22 +1209,32 @@ bool try_epi_b(Args& a, dim3 grid, hipStream_t s, int key) {
   return true;
 }
 
-// fp8 operands (GEMM mode): the epilogue sets the ViT uses — qkv / q / kv (+RoPE), fc1
-// (+GELU, fp8 out for the next fp8 GEMM), proj / fc2 (f32 residual), plain bf16 / f32
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC>
+// fp8 operands.  GEMM mode: the epilogue sets the ViT uses — qkv / q / kv (+RoPE), fc1
+// (+GELU, fp8 out for the next fp8 GEMM), proj / fc2 (f32 residual), plain bf16 / f32.
+// Implicit conv (MODE 1, C5's full-resolution DPT head convs, round 5): bf16 out (head.0)
+// and ReLU + the fused DPT tail (head.2).  The A operand is e4m3 NHWC and Cin arrives in
+// 2-byte units like K, so the tap / channel addressing is the bf16 kernel's unchanged.
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE>
 void launch_main_f8(Args& a, dim3 grid, hipStream_t s) {
   const int key = a.flags & ~(M3S_IN_FP8 | (a.bias ? 0 : M3S_EPI_BIAS));
   if (a.vec) {
-    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_ROPE, true>(a, grid, s, key)) return;
-    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_GELU | M3S_EPI_OUT_FP8, true>(
-            a, grid, s, key))
-      return;
-    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, true>(
-            a, grid, s, key))
-      return;
-    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, 0, true>(a, grid, s, key)) return;
+    if constexpr (MODE == 0) {
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_ROPE, true>(a, grid, s, key))
+        return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_GELU | M3S_EPI_OUT_FP8, true>(
+              a, grid, s, key))
+        return;
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, true>(
+              a, grid, s, key))
+        return;
+    } else if constexpr (BN == 128) {
+      if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RELU | M3S_EPI_DPT_OUT, true>(
+              a, grid, s, key))
+        return;
+    }
+    if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, 0, true>(a, grid, s, key)) return;
   }
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, false, -1, true>), grid,
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, MODE, false, -1, true>), grid,
                      dim3(WM * WN * 64), 0, s, a);
 }
 
@@ -1342,7 +1352,10 @@ int launch(Args& a, int batch, hipStream_t s) {
                          dim3(256), 0, s, a);
     }
   } else if constexpr (F8) {
-    launch_main_f8<BM, BN, BK, WM, WN, STAGES, OCC>(a, grid, s);
+    if (a.mode == 0)
+      launch_main_f8<BM, BN, BK, WM, WN, STAGES, OCC, 0>(a, grid, s);
+    else
+      launch_main_f8<BM, BN, BK, WM, WN, STAGES, OCC, 1>(a, grid, s);
   } else if (a.mode == 0) {
     launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 0>(a, grid, s);
   } else if (a.flags & M3S_PRO_RELU) {

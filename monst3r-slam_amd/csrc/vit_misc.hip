@@ -146,12 +146,14 @@ __global__ __launch_bounds__(256) void patchify_kernel(const float* __restrict__
 // ---- bilinear x2, align_corners=True (torch upsample_bilinear2d formula) -------------
 // IT: index type — 32-bit whenever the element count allows (the 64-bit div/mod of the
 // index decomposition otherwise costs more than the memory traffic).
-template <typename IT>
+// F8OUT: the output is OCP e4m3 of v * inv_scale (the A operand of an fp8 implicit conv,
+// C5; the conv's column scales carry the activation scale back).
+template <typename IT, bool F8OUT = false>
 __global__ __launch_bounds__(256) void upsample2x_kernel(const bf16_t* __restrict__ in,
-                                                         bf16_t* __restrict__ out,
+                                                         void* __restrict__ out_,
                                                          const bf16_t* __restrict__ addend,
                                                          int h, int w, int c, int oh, int ow,
-                                                         IT total) {
+                                                         IT total, float inv_scale = 1.f) {
   const IT idx = (IT)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
   const IT c8 = (IT)(c / 8);
@@ -177,15 +179,23 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const bf16_t* __restric
   const int64_t oidx = (((b * oh + oy) * (int64_t)ow) + ox) * c + cc;
   bf16x8 ad = {};
   if (addend) ad = *reinterpret_cast<const bf16x8*>(addend + oidx);
-  bf16x8 o;
+  float v[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    float v = hy * (hx * bf2f(a[k]) + lx * bf2f(bb[k])) +
-              ly * (hx * bf2f(cq[k]) + lx * bf2f(dq[k]));
-    if (addend) v += bf2f(ad[k]);
-    o[k] = f2bf(v);
+    v[k] = hy * (hx * bf2f(a[k]) + lx * bf2f(bb[k])) + ly * (hx * bf2f(cq[k]) + lx * bf2f(dq[k]));
+    if (addend) v[k] += bf2f(ad[k]);
   }
-  *reinterpret_cast<bf16x8*>(out + oidx) = o;
+  if constexpr (F8OUT) {
+    uint2 o;
+    o.x = pack4_fp8(v[0] * inv_scale, v[1] * inv_scale, v[2] * inv_scale, v[3] * inv_scale);
+    o.y = pack4_fp8(v[4] * inv_scale, v[5] * inv_scale, v[6] * inv_scale, v[7] * inv_scale);
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(out_) + oidx) = o;
+  } else {
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[k] = f2bf(v[k]);
+    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16_t*>(out_) + oidx) = o;
+  }
 }
 
 // ---- DPT output tail: 1x1 conv 128→4 + postprocess ------------------------------------
@@ -381,24 +391,40 @@ extern "C" int m3s_copy_rows(const void* d_src, void* d_dst, int64_t rows, int64
   return M3S_OK;
 }
 
+namespace {
+template <bool F8OUT>
+int upsample2x_launch(const void* d_in, void* d_out, const void* d_add, int64_t batch, int64_t h,
+                      int64_t w, int64_t c, int64_t oh, int64_t ow, float inv_scale,
+                      void* stream) {
+  if (!d_in || !d_out || batch <= 0 || h <= 0 || w <= 0 || c % 8) return M3S_ERR_INVALID_ARG;
+  if (oh <= 0 || ow <= 0 || oh > 2 * h || ow > 2 * w) return M3S_ERR_INVALID_ARG;
+  if (F8OUT && !(inv_scale > 0.f && inv_scale < 3.0e38f)) return M3S_ERR_INVALID_ARG;
+  const int64_t total = batch * oh * ow * (c / 8);
+  if (total < (int64_t(1) << 31) - 256)
+    hipLaunchKernelGGL((upsample2x_kernel<uint32_t, F8OUT>), dim3(m3s_div_up(total, 256)),
+                       dim3(256), 0, m3s_stream(stream), reinterpret_cast<const bf16_t*>(d_in),
+                       d_out, reinterpret_cast<const bf16_t*>(d_add), (int)h, (int)w, (int)c,
+                       (int)oh, (int)ow, (uint32_t)total, inv_scale);
+  else
+    hipLaunchKernelGGL((upsample2x_kernel<int64_t, F8OUT>), dim3(m3s_div_up(total, 256)),
+                       dim3(256), 0, m3s_stream(stream), reinterpret_cast<const bf16_t*>(d_in),
+                       d_out, reinterpret_cast<const bf16_t*>(d_add), (int)h, (int)w, (int)c,
+                       (int)oh, (int)ow, total, inv_scale);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+}  // namespace
+
 extern "C" int m3s_vit_upsample2x(const void* d_in, void* d_out, const void* d_add,
                                   int64_t batch, int64_t h, int64_t w, int64_t c, int64_t oh,
                                   int64_t ow, void* stream) {
-  if (!d_in || !d_out || batch <= 0 || h <= 0 || w <= 0 || c % 8) return M3S_ERR_INVALID_ARG;
-  if (oh <= 0 || ow <= 0 || oh > 2 * h || ow > 2 * w) return M3S_ERR_INVALID_ARG;
-  const int64_t total = batch * oh * ow * (c / 8);
-  if (total < (int64_t(1) << 31) - 256)
-    hipLaunchKernelGGL(upsample2x_kernel<uint32_t>, dim3(m3s_div_up(total, 256)), dim3(256), 0,
-                       m3s_stream(stream), reinterpret_cast<const bf16_t*>(d_in),
-                       reinterpret_cast<bf16_t*>(d_out), reinterpret_cast<const bf16_t*>(d_add),
-                       (int)h, (int)w, (int)c, (int)oh, (int)ow, (uint32_t)total);
-  else
-    hipLaunchKernelGGL(upsample2x_kernel<int64_t>, dim3(m3s_div_up(total, 256)), dim3(256), 0,
-                       m3s_stream(stream), reinterpret_cast<const bf16_t*>(d_in),
-                       reinterpret_cast<bf16_t*>(d_out), reinterpret_cast<const bf16_t*>(d_add),
-                       (int)h, (int)w, (int)c, (int)oh, (int)ow, total);
-  M3S_LAUNCH_CHECK();
-  return M3S_OK;
+  return upsample2x_launch<false>(d_in, d_out, d_add, batch, h, w, c, oh, ow, 1.f, stream);
+}
+
+extern "C" int m3s_vit_upsample2x_e4m3(const void* d_in, void* d_out, const void* d_add,
+                                       int64_t batch, int64_t h, int64_t w, int64_t c, int64_t oh,
+                                       int64_t ow, float inv_scale, void* stream) {
+  return upsample2x_launch<true>(d_in, d_out, d_add, batch, h, w, c, oh, ow, inv_scale, stream);
 }
 
 extern "C" int m3s_vit_dpt_out(const void* d_t, const float* d_w4, const float* d_b4,

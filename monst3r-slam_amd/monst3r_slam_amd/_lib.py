@@ -72,6 +72,7 @@ SIGNATURES = {
     "m3s_copy_rows": (_I, [_P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64, _I64,
                            _I64, _I64, _P]),
     "m3s_vit_upsample2x": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _P]),
+    "m3s_vit_upsample2x_e4m3": (_I, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, _F, _P]),
     "m3s_vit_dpt_out": (_I, [_P, _P, _P, _P, _P, _I64, _F, _I64, _I64, _I64, _I64, _P]),
     "m3s_vit_local_features": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _P]),
     "m3s_ego_flow": (_I, [_P, _P, _I64, _I64, _P, _P]),

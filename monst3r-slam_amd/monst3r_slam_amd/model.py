@@ -192,7 +192,13 @@ class Ops:
     def patchify(self, img, out, b, h, w):
         _lib.check(self.lib.m3s_vit_patchify(_p(img), _p(out), b, h, w, self._s()), "patchify")
 
-    def up2(self, x, out, b, h, w, c, oh=None, ow=None, add=None):
+    def up2(self, x, out, b, h, w, c, oh=None, ow=None, add=None, inv_scale=1.0):
+        """out uint8 / float8_e4m3fn: e4m3 of the upsample times inv_scale."""
+        if out.element_size() == 1:
+            _lib.check(self.lib.m3s_vit_upsample2x_e4m3(
+                _p(x), _p(out), _p(add), b, h, w, c, oh or 2 * h, ow or 2 * w, float(inv_scale),
+                self._s()), "upsample2x_e4m3")
+            return
         _lib.check(self.lib.m3s_vit_upsample2x(_p(x), _p(out), _p(add), b, h, w, c,
                                                oh or 2 * h, ow or 2 * w, self._s()), "upsample2x")
 
@@ -255,6 +261,10 @@ def ln_fold(w, b, g, beta, dev):
 # decoder_embed and the DPT/local-feature heads stay bf16
 ENC_FP8 = ("qkv_w", "proj_w", "fc1_w", "fc2_w")
 DEC_FP8 = ("qkv_w", "proj_w", "q_w", "kv_w", "cproj_w", "fc1_w", "fc2_w")
+# ... and the DPT heads' two full-resolution 3x3 convs (round 5): their inputs are the
+# bilinear upsamples (path1 → head.0, head.0 → head.2), which emit e4m3 directly
+HEAD_FP8 = ("head0", "head2")
+FP8_ACT_HEADROOM = 2.0   # calibrated amax maps to 448 / 2: test frames may run hotter
 
 
 def _fp8_shifted_params(W, cal):
@@ -434,6 +444,7 @@ class PackedWeights:
         self.enc8 = self.dec8 = None
         self.fp8_shift_enc, self.fp8_shift_dec = {}, [{} for _ in self.dec]
         self.fp8_calibrated = False
+        self.h8, self.h8_cs, self.h8_inv = None, {}, {}
 
     def enable_fp8(self):
         """e4m3 copies (+ per-row scales) of the encoder / decoder transformer weights,
@@ -441,6 +452,10 @@ class PackedWeights:
         if self.enc8 is None:
             self.enc8 = {k: quant_e4m3(self.enc[k]) for k in ENC_FP8}
             self.dec8 = [{k: quant_e4m3(P[k]) for k in DEC_FP8} for P in self.dec]
+            # the DPT heads' full-resolution convs (head.0, head.2: Cin 256 / 128, packed
+            # [Cout][ky][kx][Cin] rows), per-Cout scales; their e4m3 inputs come from the
+            # upsample with a calibrated per-tensor scale (h8_cs = row scale x act scale)
+            self.h8 = {k: quant_e4m3(self.h[k + "_w"]) for k in HEAD_FP8}
 
 
 # ---------------------------------------------------------------------------------------
@@ -490,6 +505,7 @@ class PairModel:
         self.side = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
         self.serial = True
         self.fp8 = False
+        self.fp8_convs = os.environ.get("M3S_FP8_CONVS", "0") == "1"
         # bf16 path: the blocks' LayerNorms folded into the following projections (ln_fold;
         # LN_STATS / LN_FOLD epilogues) instead of separate LayerNorm launches
         self.lnfold = os.environ.get("M3S_LNFOLD", "1") != "0"
@@ -517,15 +533,22 @@ class PairModel:
         self._ev_heads = None
         self.head_aux = None  # stream for the DPT heads' off-chain branches (_head_aux)
 
-    def set_fp8(self, on=True, calibrate=True):
+    def set_fp8(self, on=True, calibrate=True, convs=None):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
         operands on the scaled MFMA — LayerNorm, attention and the fc1 GELU epilogue emit
         e4m3 activations (unscaled, saturated to ±448), weights are per-row scaled, the
         residual stream stays f32 and q/k/v stay bf16 (attention runs in bf16).
         calibrate: on first use, per-channel activation shifts and bias correction from two
-        synthetic calibration frames (calibrate_fp8)."""
+        synthetic calibration frames (calibrate_fp8).
+        convs: also run the DPT heads' two full-resolution convs (head.0, head.2) on the
+        fp8 MFMA (e4m3 upsample outputs with a calibrated per-tensor scale).  Off by default:
+        measured on the C5 frame 10.10 → 9.74 ms for pointmap error 2.85 → 5.41 % (pair X
+        median, 512x512).  None keeps the current setting (M3S_FP8_CONVS=1
+        turns it on for the bench / sweeps)."""
         if on:
             self.w.enable_fp8()
+        if convs is not None:
+            self.fp8_convs = bool(convs)
         self.fp8 = bool(on)
         if on and calibrate and not self.w.fp8_calibrated:
             self.calibrate_fp8()
@@ -558,13 +581,20 @@ class PairModel:
             gh, gw = hw[0] // self.a.patch, hw[1] // self.a.patch
             f = feat.reshape(frames, gh * gw, self.a.enc_dim)
             # pairs (frame k, frame k+1): both models, both sides
-            self.decode_multi(f.contiguous(), f.roll(1, 0).contiguous(), gh, gw)
+            hooks = self.decode_multi(f.contiguous(), f.roll(1, 0).contiguous(), gh, gw)
+            # the heads (bf16 convs until calibrated) for the upsample outputs' amax
+            self.heads(hooks, gh, gw, hw[0], hw[1])
             torch.cuda.synchronize(dev)
-            cal = {k: (v / n) for k, (v, n) in self._cal.items()}
+            amax = {k: float(v) for k, v in self._cal.items() if k[0] == "amax"}
+            cal = {k: v[0] / v[1] for k, v in self._cal.items() if k[0] != "amax"}
         finally:
             self._cal = None
             self.fp8 = was
         W.fp8_shift_enc, W.fp8_shift_dec = _fp8_shifted_params(W, cal)
+        for k in HEAD_FP8:
+            s = max(amax[("amax", k)], 1e-30) * FP8_ACT_HEADROOM / 448.0
+            W.h8_inv[k] = 1.0 / s
+            W.h8_cs[k] = (W.h8[k][1] * s).contiguous()
         W.fp8_calibrated = True
 
     def _calib(self, site, i, t, z=None):
@@ -581,6 +611,28 @@ class PairModel:
         key = (site, i)
         acc, n = self._cal.get(key, (0.0, 0))
         self._cal[key] = (acc + m, n + 1)
+
+    def _calib_amax(self, name, t):
+        if getattr(self, "_cal", None) is not None:
+            prev = self._cal.get(("amax", name), 0.0)
+            self._cal[("amax", name)] = max(prev, float(t.float().abs().max()))
+
+    def _fp8_convs(self):
+        """The DPT head convs on the fp8 MFMA: fp8 mode with convs on (set_fp8), calibrated."""
+        return (self.fp8 and self.fp8_convs and self.w.fp8_calibrated and
+                self.w.h8 is not None)
+
+    def _conv3_f8(self, x, key, out, b, hin, win, cin, cout, bias_key=None, flags=0, dpt=None):
+        """3x3 stride-1 conv on the fp8 MFMA: x e4m3 NHWC (scaled by h8_inv[key]), weights
+        e4m3 per-Cout rows; the column scales undo both."""
+        o, H, W = self.ops, self._hw, self.w
+        q, cs = W.h8[key][0], W.h8_cs[key]
+        if self._wbase:
+            q, cs = q[self._wbase:], cs[self._wbase:]
+        o.gemm(x, q, out, hin * win, cout, 9 * cin, b, sA=hin * win * cin, sB=cout * 9 * cin,
+               sC=hin * win * cout, bias=H(bias_key) if bias_key else None, sBias=cout,
+               flags=flags, conv=(hin, win, cin, hin, win, 1), wmod=self._wm, dpt=dpt,
+               fp8=(cs, cout))
 
     def _pb(self, P, key, i=None, layer=None):
         """Bias / LayerNorm beta `key`: the fp8 path's calibrated copy when fp8 is on."""
@@ -1030,7 +1082,7 @@ class PairModel:
                     R=addend_res if addend_res is not None else x,
                     flags=_lib.PRO_RELU | _lib.EPI_RES_BF16)
 
-    def _fusion(self, k, s1, b, h, w, next_hw, next_u, out, ev_u=None):
+    def _fusion(self, k, s1, b, h, w, next_hw, next_u, out, ev_u=None, inv_scale=1.0):
         """FeatureFusionBlock (dpt_block.py:185-218) at resolution (h, w), from its input
         s1 = path + RCU1(skip) (refinenet4: the path alone): s = RCU2(s1);
         out = up2(out_conv(s)) + next_u — out_conv commuted before the upsample, and the
@@ -1046,7 +1098,7 @@ class PairModel:
         oh, ow = next_hw
         if ev_u is not None:
             torch.cuda.current_stream(self.dev).wait_event(ev_u)
-        o.up2(oc, out, b, h, w, F, oh, ow, add=next_u)
+        o.up2(oc, out, b, h, w, F, oh, ow, add=next_u, inv_scale=inv_scale)
 
     def _rcu1_skip(self, k, skip, b, h, w):
         """refinenet k's RCU1 on its skip (layer_rn output): u = conv2(relu(conv1(relu(skip))))
@@ -1238,19 +1290,35 @@ class PairModel:
         self._fusion(3, p4, Z, gh, gw, (2 * gh, 2 * gw), u[2], p3, ev_u.get(2))
         p2 = self._buf("path2", (Z, 4 * gh, 4 * gw, F), BF16)
         self._fusion(2, p3, Z, 2 * gh, 2 * gw, (4 * gh, 4 * gw), u[1], p2, ev_u.get(1))
-        p1 = self._buf("path1", (Z, 8 * gh, 8 * gw, F), BF16)
-        self._fusion(1, p2, Z, 4 * gh, 4 * gw, (8 * gh, 8 * gw), None, p1)
+        # fp8 mode (C5): path1 and the head's upsample are emitted as e4m3 for the two
+        # full-resolution convs (the others stay bf16)
+        f8c = self._fp8_convs()
+        inv = self.w.h8_inv
+        p1 = self._buf("path1" if not f8c else "path1_e4m3", (Z, 8 * gh, 8 * gw, F),
+                       U8 if f8c else BF16)
+        self._fusion(1, p2, Z, 4 * gh, 4 * gw, (8 * gh, 8 * gw), None, p1,
+                     inv_scale=inv.get("head0", 1.0) if f8c else 1.0)
+        self._calib_amax("head0", p1)
         # head: conv3x3 F→F/2 @ (H/2, W/2), up2, conv3x3 → last_dim + ReLU, 1x1 → 4 + post
         h2, w2 = 8 * gh, 8 * gw
         hd0 = self._buf("head0", (Z, h2, w2, F // 2), BF16)
-        self._conv3(p1, "head0_w", hd0, Z, h2, w2, F, F // 2, bias_key="head0_b")
-        hup = self._buf("head_up", (Z, H, W, F // 2), BF16)
-        o.up2(hd0, hup, Z, h2, w2, F // 2, H, W)
+        if f8c:
+            self._conv3_f8(p1, "head0", hd0, Z, h2, w2, F, F // 2, bias_key="head0_b")
+        else:
+            self._conv3(p1, "head0_w", hd0, Z, h2, w2, F, F // 2, bias_key="head0_b")
+        hup = self._buf("head_up" if not f8c else "head_up_e4m3", (Z, H, W, F // 2),
+                        U8 if f8c else BF16)
+        o.up2(hd0, hup, Z, h2, w2, F // 2, H, W, inv_scale=inv.get("head2", 1.0) if f8c else 1.0)
+        self._calib_amax("head2", hup)
         # conv3x3 → last_dim + ReLU with the 1x1 (last_dim → 4) + reg_dense_depth / conf
         # fused into its epilogue: the 128-channel map never reaches HBM
-        self._conv3(hup, "head2_w", pts, Z, H, W, F // 2, a.last_dim, bias_key="head2_b",
-                    flags=_lib.EPI_RELU,
-                    dpt=(Hw("head4_w"), Hw("head4_b"), pts, conf, a.conf_min))
+        dpt = (Hw("head4_w"), Hw("head4_b"), pts, conf, a.conf_min)
+        if f8c:
+            self._conv3_f8(hup, "head2", pts, Z, H, W, F // 2, a.last_dim, bias_key="head2_b",
+                           flags=_lib.EPI_RELU, dpt=dpt)
+        else:
+            self._conv3(hup, "head2_w", pts, Z, H, W, F // 2, a.last_dim, bias_key="head2_b",
+                        flags=_lib.EPI_RELU, dpt=dpt)
         self._tag, self._wbase = None, 0
 
 
