@@ -7,16 +7,19 @@ is well formed only if the capture stream, before capture_end, has waited on an 
 recorded on every such side stream after its last work (the join).  On this ROCm stack a
 malformed or over-wide capture does not fail cleanly: hipStreamEndCapture / the graph
 instantiate segfaulted (profiles/r03_capture_segfault.txt) when more streams took part than
-the HIP runtime has hardware queues to spare (measured: 6 streams over GPU_MAX_HW_QUEUES=4
-and 4 streams over 2 crash; 4 streams over 3 or 4 queues capture; DESIGN §5 "Capture
-topology").  CaptureTopology records the fork/join graph while the step is issued — a vector
-clock per stream, advanced by every native launch (_lib.stream) and every entry into a
-stream context — and raises TopologyError before capture_end when
+the HIP runtime has hardware queues to spare (measured: 6 and 5 streams over
+GPU_MAX_HW_QUEUES=4 and 4 streams over 2 crash; 4 streams over 3 or 4 queues capture; DESIGN §5
+"Capture topology"), and when a stream waited on an event recorded on itself (round 5: a
+fork / join whose two ends were the same stream crashed every capture that had it, at 3 and
+4 streams alike).  CaptureTopology records the fork/join graph while the step is issued — a
+vector clock per stream, advanced by every native launch (_lib.stream) and every entry into
+a stream context — and raises TopologyError before capture_end when
 
   * a side stream's last work is not ordered before the end of the capture stream
     (an unjoined fork: CUDA semantics return cudaErrorStreamCaptureUnjoined, HIP crashed);
   * an event waited on inside the capture was recorded outside it (a cross-capture edge);
-  * more streams take part than GPU_MAX_HW_QUEUES + 1.
+  * a stream waits on an event it recorded itself (e.g. s.wait_stream(s));
+  * more streams take part than min(GPU_MAX_HW_QUEUES + 1, 4).
 
 Host-only bookkeeping at capture time; replays are untouched.
 """
@@ -42,8 +45,9 @@ def hw_queues() -> int:
 
 
 def max_capture_streams() -> int:
-    """Widest capture this stack survives: one stream more than its hardware queues."""
-    return hw_queues() + 1
+    """Widest capture this stack survives: one stream more than its hardware queues, and
+    never more than four (five over four queues crashed, round 5)."""
+    return min(hw_queues() + 1, 4)
 
 
 class CaptureTopology:
@@ -66,12 +70,16 @@ class CaptureTopology:
         c[h] = c.get(h, 0) + 1
 
     def record(self, ev, h):
-        ev._m3s_vc = (id(self), dict(self._clock(h)))
+        ev._m3s_vc = (id(self), dict(self._clock(h)), h)
 
     def wait(self, h, ev):
         tag = getattr(ev, "_m3s_vc", None)
         if tag is None or tag[0] != id(self):
             self.errors.append(f"stream {h:#x} waits on an event recorded outside the capture")
+            return
+        if tag[2] == h:
+            self.errors.append(f"stream {h:#x} waits on an event it recorded itself (a fork / "
+                               "join onto the same stream: capture_end segfaults)")
             return
         c = self._clock(h)
         for k, v in tag[1].items():
@@ -143,9 +151,9 @@ class CaptureTopology:
                            f"capture stream (joined up to {end.get(h, 0)})")
         n = len(self.streams())
         if n > self.max_streams:
-            out.append(f"{n} streams take part in the capture, more than GPU_MAX_HW_QUEUES + 1 = "
-                       f"{self.max_streams} (the HIP runtime segfaults at capture_end past that "
-                       "width, DESIGN §5)")
+            out.append(f"{n} streams take part in the capture, more than the {self.max_streams} "
+                       "this stack survives (min(GPU_MAX_HW_QUEUES + 1, 4): the HIP runtime "
+                       "segfaults at capture_end past that width, DESIGN §5)")
         return out
 
     def check(self):

@@ -91,5 +91,18 @@ def test_width_limit():
 def test_budget_follows_hw_queues(monkeypatch):
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "2")
     assert max_capture_streams() == 3
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
+    assert max_capture_streams() == 4        # five streams over four queues crashed (round 5)
     monkeypatch.delenv("GPU_MAX_HW_QUEUES")
-    assert max_capture_streams() == 5
+    assert max_capture_streams() == 4
+
+
+def test_self_wait_raises():
+    """s.wait_stream(s) inside a capture (round 5: capture_end segfaulted on it)."""
+    t = _topo()
+    _fork(t, CAP, A)
+    t.tick(A)
+    _fork(t, A, A)            # the stream waits on its own event
+    _fork(t, A, CAP)
+    with pytest.raises(TopologyError, match="recorded itself"):
+        t.check()
