@@ -86,6 +86,9 @@ def test_timeline_records_every_launch(dev):
     # K-loop done <= epilogue tile in LDS, inside the block's lifetime; attention blocks none
     kk = k[np.clip(sl, 0, n - 1)]
     gm = lg[kk != 2]
+    # (a separate split-K reduce launch logs its blocks into its GEMM's slot, unmarked)
+    gm = gm[(gm[:, 4:8] != 0).any(1)]
+    assert set(np.unique(sl[kk != 2])) == set(np.unique((gm[:, 2] - base) // (132 * 8)))
     ph = gm[:, 4:8]
     assert (ph[:, :3] > 0).all()           # (split-K slices that are not the last skip mark 3)
     assert (gm[:, 0] <= ph[:, 0]).all() and (np.diff(ph[:, :3], axis=1) >= 0).all()
