@@ -258,10 +258,6 @@ class FramePipeline:
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
             self.encode_side(img_next, k)
-        self.tr.model.head_aux = self.side   # DPT heads' off-chain branches (model._head_aux)
-        try:
-            res = self.tr.track(img_cur, T_WCf_init, feat_i=self.feat[k % 2])
-        finally:
-            self.tr.model.head_aux = None
+        res = self.tr.track(img_cur, T_WCf_init, feat_i=self.feat[k % 2])
         main.wait_stream(self.side)
         return res

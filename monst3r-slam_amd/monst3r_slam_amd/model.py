@@ -531,7 +531,6 @@ class PairModel:
         self._wbase = 0       # first head-weight stack of that set
         self._wm = 4
         self._ev_heads = None
-        self.head_aux = None  # stream for the DPT heads' off-chain branches (_head_aux)
 
     def set_fp8(self, on=True, calibrate=True, convs=None):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
@@ -661,22 +660,6 @@ class PairModel:
         main = torch.cuda.current_stream(self.dev)
         self.side[k].wait_stream(main)
         return torch.cuda.stream(self.side[k])
-
-    def _head_aux(self):
-        """Stream for the DPT head set's off-chain work (`_dpt`): the caller's `head_aux`
-        (FramePipeline hands its prefetch stream, idle once the step's encoder part is
-        issued, so the captured step keeps its three streams), else side stream 1; None —
-        everything on the current stream — for the split MASt3R set (already a side
-        chain) or M3S_HEAD_AUX=0."""
-        # default: the chain's own stream.  M3S_HEAD_AUX=1: the caller's stream (the step's
-        # prefetch stream: that captured step segfaulted at graph replay, round 5), side1:
-        # side stream 1 (a fourth captured stream: 232.6 vs 231.4 frames/s, noise)
-        mode = os.environ.get("M3S_HEAD_AUX", "0")
-        if self._tag == "mast3r" or mode == "0":
-            return None
-        if mode == "side1" or self.head_aux is None:
-            return self.side[1]
-        return self.head_aux
 
     def _event(self):
         if self.serial:
@@ -1082,12 +1065,12 @@ class PairModel:
                     R=addend_res if addend_res is not None else x,
                     flags=_lib.PRO_RELU | _lib.EPI_RES_BF16)
 
-    def _fusion(self, k, s1, b, h, w, next_hw, next_u, out, ev_u=None, inv_scale=1.0):
+    def _fusion(self, k, s1, b, h, w, next_hw, next_u, out, inv_scale=1.0):
         """FeatureFusionBlock (dpt_block.py:185-218) at resolution (h, w), from its input
         s1 = path + RCU1(skip) (refinenet4: the path alone): s = RCU2(s1);
         out = up2(out_conv(s)) + next_u — out_conv commuted before the upsample, and the
-        next level's `+ RCU1(skip)` (next_u, computed off this chain: `_rcu1_skip`, ready
-        at event ev_u) added by the upsample, so `out` is the next level's s1."""
+        next level's `+ RCU1(skip)` (next_u, computed ahead of this chain: `_rcu1_skip`)
+        added by the upsample, so `out` is the next level's s1."""
         o, H = self.ops, self._hw
         F = self.a.feature_dim
         s2 = self._buf(("fus_s2", h, w), (b, h, w, F), BF16)
@@ -1096,8 +1079,6 @@ class PairModel:
         o.gemm(s2, H(f"r{k}_out_w"), oc, h * w, F, F, b, sA=h * w * F, sB=F * F, sC=h * w * F,
                bias=H(f"r{k}_out_b"), sBias=F, wmod=self._wm)
         oh, ow = next_hw
-        if ev_u is not None:
-            torch.cuda.current_stream(self.dev).wait_event(ev_u)
         o.up2(oc, out, b, h, w, F, oh, ow, add=next_u, inv_scale=inv_scale)
 
     def _rcu1_skip(self, k, skip, b, h, w):
@@ -1265,31 +1246,23 @@ class PairModel:
         R = self._rn_bufs(gh, gw, Z)
         # The refinenet chain needs the act_postprocess / layer_rn outputs one level at a
         # time (R[3] first, R[0] last), and each level's RCU1 depends on its skip R[k-1]
-        # alone: branch 3 opens the chain; branches 2, 1, 0, each followed by its level's
-        # RCU1 (u3, u2, u1), run in that order on the aux stream (`head_aux`: the chain's
-        # own stream is the tracking-critical one) and are joined by event at the upsample
-        # that adds them — 11 of the chain's ~36 launches leave it.
-        aux = self._head_aux()
+        # alone: branches 2, 1, 0, each followed by its level's RCU1 (u3, u2, u1), then
+        # branch 3 and the refinenets, whose upsamples add the u's.  (The branches + RCU1s
+        # on a stream of their own measured 232.6 vs 231.5 frames/s, noise, on the prefetch
+        # stream the replayed step segfaulted: round 5, removed.)
         h_of = {3: (gh, gw), 2: (2 * gh, 2 * gw), 1: (4 * gh, 4 * gw)}
-        u, ev_u = {}, {}
-        main = torch.cuda.current_stream(self.dev)
-        if aux is not None:
-            aux.wait_stream(main)
-        with (torch.cuda.stream(aux) if aux is not None else _Nullctx()):
-            for lvl, br in ((3, 2), (2, 1), (1, 0)):
-                self._ap_branch(br, hooks, gh, gw, Z, R)
-                u[lvl] = self._rcu1_skip(lvl, R[br], Z, *h_of[lvl])
-                if aux is not None:
-                    ev_u[lvl] = torch.cuda.Event()
-                    ev_u[lvl].record(aux)
+        u = {}
+        for lvl, br in ((3, 2), (2, 1), (1, 0)):
+            self._ap_branch(br, hooks, gh, gw, Z, R)
+            u[lvl] = self._rcu1_skip(lvl, R[br], Z, *h_of[lvl])
         self._ap_branch(3, hooks, gh, gw, Z, R)
         # refinenets: s1_k = path_k + RCU1_k(R_{k-1}); path_{k-1} = up2(out_conv(RCU2(s1_k)))
         p4 = self._buf("path4", (Z, gh, gw, F), BF16)
-        self._fusion(4, R[3], Z, g3h, g3w, (gh, gw), u[3], p4, ev_u.get(3))
+        self._fusion(4, R[3], Z, g3h, g3w, (gh, gw), u[3], p4)
         p3 = self._buf("path3", (Z, 2 * gh, 2 * gw, F), BF16)
-        self._fusion(3, p4, Z, gh, gw, (2 * gh, 2 * gw), u[2], p3, ev_u.get(2))
+        self._fusion(3, p4, Z, gh, gw, (2 * gh, 2 * gw), u[2], p3)
         p2 = self._buf("path2", (Z, 4 * gh, 4 * gw, F), BF16)
-        self._fusion(2, p3, Z, 2 * gh, 2 * gw, (4 * gh, 4 * gw), u[1], p2, ev_u.get(1))
+        self._fusion(2, p3, Z, 2 * gh, 2 * gw, (4 * gh, 4 * gw), u[1], p2)
         # fp8 mode (C5): path1 and the head's upsample are emitted as e4m3 for the two
         # full-resolution convs (the others stay bf16)
         f8c = self._fp8_convs()

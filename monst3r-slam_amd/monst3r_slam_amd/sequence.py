@@ -281,14 +281,7 @@ class SequenceLoop:
                 # the decoders are issued instead, into the head phase's idle CUs: 196 vs
                 # 231.5 frames/s, round 5 — the head phase cannot absorb it)
                 prefetch()
-                # the DPT heads' off-chain branches follow this step's encoder part on the
-                # prefetch stream (the step keeps its three streams)
-                m.head_aux = pipe.side
-                try:
-                    out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i,
-                                 split_heads=split)
-                finally:
-                    m.head_aux = None
+                out = m.pair(self.img_cur, feat_j=tr.kf.feat, feat_i=feat_i, split_heads=split)
             else:
                 self.gather(self.img_cur, 0)
                 out = m.pair(self.img_cur, feat_j=tr.kf.feat, split_heads=split)
