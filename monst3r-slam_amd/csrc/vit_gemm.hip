@@ -27,7 +27,6 @@
 //   offset are block-uniform (Cin % BK == 0); ReLU is applied to the A fragments in
 //   registers (v_pk_max_i16 on the bf16 bits).
 // XCD-aware bijective tile order (cdna_hip_programming.md T1).
-#include <stdio.h>
 #include <stdlib.h>
 #include <algorithm>
 #include "vit_gemm_kern.h"
@@ -265,21 +264,6 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   if (conv && d->Cin % 64 == 0 && cfg == T128K32) cfg = T128;
   int splits = d->split_k;
   if (tuned && splits <= 0) splits = tuned->splits;
-  // in-step sweep knob for the latency-bound small DPT convs (M ≤ 3072 on 64x128 tiles):
-  // M3S_CONV_SPLIT="mink,fused" re-derives their split-K with at least `mink` K-tiles per
-  // split (table and heuristic use 8) while the grid stays within one round of 2 blocks
-  // per CU, fused = last-arriving split reduces (1) or a reduce launch (0)
-  static const char* conv_split = getenv("M3S_CONV_SPLIT");
-  int conv_split_fused = -1;
-  if (conv_split && conv && cfg == T64 && d->M <= 3072 && d->split_k <= 0 &&
-      !(d->flags & M3S_EPI_DPT_OUT)) {
-    int mink = 8;
-    sscanf(conv_split, "%d,%d", &mink, &conv_split_fused);
-    if (mink < 1) mink = 1;
-    const int64_t tiles64 = (int64_t)((d->M + 63) / 64) * ((d->N + 127) / 128) * d->batch;
-    splits = 1;
-    while (tiles64 * splits * 2 <= 512 && nk / (splits * 2) >= mink) splits *= 2;
-  }
   if (const char* e = getenv("M3S_GEMM_SPLITS")) splits = atoi(e);  // tuning override
   if (splits <= 0) {
     splits = 1;
@@ -306,7 +290,6 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   // needs the fused path (the reduce kernel has no fold)
   int fused = ln_fold ? 1 : (tuned ? tuned->fused : 0);
   if (const char* e = getenv("M3S_GEMM_FUSED")) fused = atoi(e) != 0 || ln_fold;  // tuning
-  if (conv_split_fused >= 0) fused = conv_split_fused;
   const bool can_split = split_cfg && !f8 && !(d->flags & (M3S_EPI_CONVT | M3S_EPI_DPT_OUT)) &&
                          d->workspace &&
                          (!fused || (d->tile_counters && tiles_cfg <= (int64_t)d->tile_counters_len)) &&
