@@ -552,7 +552,7 @@ class PairModel:
         if on and calibrate and not self.w.fp8_calibrated:
             self.calibrate_fp8()
 
-    def calibrate_fp8(self, hw=(512, 512), frames=2, seed=100):
+    def calibrate_fp8(self, hw=(512, 512), frames=2, seed=100, images=None):
         """Static per-channel calibration of the fp8 path (round 5; tools/fp8_error_budget.py,
         tools/fp8_mono_diag.py).  The e4m3 errors are not noise: a channel whose activation
         sits near a constant over all tokens rounds the same way in every token, and a
@@ -567,15 +567,22 @@ class PairModel:
                               by -mu), b' = b + W mu
           GELU -> fc2         b' = b - (Wq - W) mu (bias correction of the quantised rows)
         In the fake-quant restatement: X median 5.5 % -> 1.9 %, feature cosine 0.99597 ->
-        0.99936 (mono 512x512)."""
+        0.99936 (mono 512x512).  images: calibration frames [n >= 2, 3, H, W] in [-1, 1]
+        (frames of the target domain with real checkpoints) instead of the noise frames."""
         W, dev = self.w, self.dev
         was = self.fp8
         self.fp8 = True
         W.fp8_shift_enc, W.fp8_shift_dec = {}, [{} for _ in W.dec]   # plain biases first
         self._cal = {}
         try:
-            gen = torch.Generator(device=dev).manual_seed(seed)
-            img = torch.rand(frames, 3, hw[0], hw[1], device=dev, generator=gen) * 2 - 1
+            if images is not None:
+                img = images.to(device=dev, dtype=torch.float32)
+                if img.dim() != 4 or img.shape[0] < 2:
+                    raise ValueError("calibrate_fp8: images must be [n >= 2, 3, H, W]")
+                frames, hw = img.shape[0], tuple(img.shape[-2:])
+            else:
+                gen = torch.Generator(device=dev).manual_seed(seed)
+                img = torch.rand(frames, 3, hw[0], hw[1], device=dev, generator=gen) * 2 - 1
             feat, _ = self.encode(img)
             gh, gw = hw[0] // self.a.patch, hw[1] // self.a.patch
             f = feat.reshape(frames, gh * gw, self.a.enc_dim)
