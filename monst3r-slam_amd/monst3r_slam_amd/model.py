@@ -625,8 +625,10 @@ class PairModel:
 
     def _fp8_convs(self):
         """The DPT head convs on the fp8 MFMA: fp8 mode with convs on (set_fp8), calibrated."""
+        F = self.a.feature_dim
+        # (the fp8 implicit conv takes Cin % 128 == 0: head.0 reads F, head.2 F / 2 channels)
         return (self.fp8 and self.fp8_convs and self.w.fp8_calibrated and
-                self.w.h8 is not None)
+                self.w.h8 is not None and F % 256 == 0)
 
     def _conv3_f8(self, x, key, out, b, hin, win, cin, cout, bias_key=None, flags=0, dpt=None):
         """3x3 stride-1 conv on the fp8 MFMA: x e4m3 NHWC (scaled by h8_inv[key]), weights
