@@ -728,12 +728,20 @@ def c5_bench(model, dev, steps):
 
         def step():
             feat_i, pos = model.encode(img)
-            Xm, _ = model.mono(feat_i, H5, W5)
-            sR, t = U.sim3_relative_matrix(Ti, Tk)
-            ego = U.ego_flow(Xm[0], sR, t, K, K)
-            mask = U.dynamic_mask_from_flow(flow, ego, 0.35)
+            # the mono branch (decode + heads + ego flow + mask) and the pair branch share
+            # only the encoder features: the mono branch runs on side stream 1 beside the
+            # pair decode / heads (side stream 0 carries the pair decoder's second chain)
+            main = torch.cuda.current_stream(dev)
+            mono_s = model.side[1]
+            mono_s.wait_stream(main)
+            with torch.cuda.stream(mono_s):
+                Xm, _ = model.mono(feat_i, H5, W5)
+                sR, t = U.sim3_relative_matrix(Ti, Tk)
+                ego = U.ego_flow(Xm[0], sR, t, K, K)
+                mask = U.dynamic_mask_from_flow(flow, ego, 0.35)
             hooks = model.decode(feat_i[0], feat_k[0], pos, gh, gw)
             pts, conf, d16, d32, dq = model.heads(hooks, gh, gw, H5, W5)
+            main.wait_stream(mono_s)
             return U.apply_dynamic_mask_to_pointmaps(pts[0:2], conf[0:2], mask, d16, dq)
 
         for _ in range(2):
