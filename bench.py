@@ -754,7 +754,8 @@ def c5_bench(model, dev, steps):
         del gph
     model.set_fp8(False, convs=False)
     return {"workload": "configs[4]: 512x512 frame, fp8 encoder+decoders, mono decode + ego "
-                        "flow + flow-error mask + pair decode/heads + apply_dynamic_mask",
+                        "flow + flow-error mask (on a side stream) beside pair decode/heads, "
+                        "then apply_dynamic_mask",
             "ms_per_frame_fp8": res["fp8"], "ms_per_frame_bf16": res["bf16"],
             "frames_per_s_fp8": 1e3 / res["fp8"], "speedup_vs_bf16": res["bf16"] / res["fp8"],
             "ms_per_frame_fp8_convs": res["fp8_convs"],
