@@ -880,6 +880,36 @@ class PairModel:
             return hooks
         if fold:
             return self._decode_folded(x, xb, st, h0, Z, S, E, D, gh, gw, wm, on_hook)
+        if (self.dec_split and models == 2 and G == 1 and on_hook is None and
+                getattr(self, "_cal", None) is None):
+            # the fp8 (unfolded) decoder split by model as the folded one above: two batch-2
+            # chains, model 1 on side stream 0 (C5's pair decode, round 5)
+            main = torch.cuda.current_stream(self.dev)
+            side = self.side[0]
+            side.wait_stream(main)
+            g0 = self._decode_plain_gen(x, h0, Z, S, D, gh, gw, wm, None, part=0)
+            g1 = self._decode_plain_gen(x, h0, Z, S, D, gh, gw, wm, None, part=1)
+            hooks = _drain(g0)
+            with torch.cuda.stream(side):
+                _drain(g1)
+            main.wait_stream(side)
+        else:
+            hooks = _drain(self._decode_plain_gen(x, h0, Z, S, D, gh, gw, wm, on_hook))
+        h12 = self._buf("h12", (Z, S, D), BF16)
+        o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
+        hooks["h12"] = h12
+        if on_hook is not None:
+            on_hook("h12", hooks)
+        return hooks
+
+    def _decode_plain_gen(self, x, h0, Z, S, D, gh, gw, wm, on_hook=None, part=None):
+        """(Generator: yields after issuing each block; returns the hooks h0, h6, h9 — the
+        caller adds h12.)  decode_multi's blocks with separate LayerNorm launches: the fp8
+        path (e4m3 LayerNorm / attention / GELU outputs as the fp8 GEMMs' A operands, the
+        calibrated shifts of calibrate_fp8) and the bf16 path when the fold is off.
+        part: one model's two problems (z in [2·part, 2·part + 2)), buffers, weights and
+        calibrated parameters sliced, weight_mod 2."""
+        o, a, W = self.ops, self.a, self.w
         adt = U8 if self.fp8 else BF16
         xn = self._buf("dec_xn", (Z, S, D), adt)
         yn = self._buf("dec_yn", (Z, S, D), adt)
@@ -888,37 +918,38 @@ class PairModel:
         q = self._buf("dec_q", (Z, S, D), BF16)
         att = self._buf("dec_att", (Z, S, D), adt)
         hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), adt)
+        hook_bufs = {k: self._buf(f"h{k}", (Z, S, D), BF16) for k in a.hooks[1:3]}
         hooks = {"h0": h0}
+        sl = None
+        if part is not None:
+            sl = slice(2 * part, 2 * part + 2)
+            xn, yn, qkv, kv, q, att, hid, x = (t[sl] for t in (xn, yn, qkv, kv, q, att, hid, x))
+            Z, wm = 2, 2
         rt = self.rope_tab(gh, gw)
-        hk = set(a.hooks[1:3])
         R32 = _lib.EPI_OUT_F32 | _lib.EPI_RES_F32
         Dm = a.mlp_ratio * D
         for i in range(a.dec_depth):
             P = W.dec[i]
             P8 = W.dec8[i] if self.fp8 else None
-            wt = lambda key, n: self._wt(P, P8, key, None, n)  # noqa: E731
-            # y_ = norm_y(previous output of the other side), then its k/v projection: on a
-            # side stream, overlapping the self-attention half of the layer (the side chain
-            # must read x before this layer's first residual update writes it)
+            Q = W.fp8_shift_dec[i] if self.fp8 else {}
+            if sl is not None:
+                P = {k: v[sl] for k, v in P.items()}
+                P8 = {k: (v[0][sl], v[1][sl]) for k, v in P8.items()} if P8 else None
+                Q = {k: v[sl] for k, v in Q.items()}
+
+            def wt(key, n, P=P, P8=P8):
+                return self._wt(P, P8, key, None, n)
+
+            def pb(key, P=P, Q=Q):   # bias / LayerNorm beta: the calibrated copy in fp8 mode
+                return Q[key] if key in Q else P[key]
+            # norm1(x) and norm_y(other side's x) share the row statistics: one pass; then
+            # y_'s k/v projection
             w, kw = wt("kv_w", 2 * D)
-            pb = lambda key: self._pb(P, key, layer=i)  # noqa: E731
-            if self.serial:
-                # norm1(x) and norm_y(other side's x) share the row statistics: one pass
-                o.ln_dual(x, P["ln1_g"], pb("ln1_b"), xn, P["lny_g"], pb("lny_b"), yn, S, D, Z,
-                          S * D, S * D, D, pmod=wm)
-                self._calib("dec.lny", i, yn, Z)
-                o.gemm(yn, w, kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
-                       sC=S * 2 * D, bias=pb("kv_b"), sBias=2 * D, rope=(rt, D, S), wmod=wm, **kw)
-                ev_lny = ev_kv = None
-            else:
-                with self._on(0):
-                    o.ln(x, P["lny_g"], pb("lny_b"), yn, S, D, Z, S * D, S * D, D, xor=1, pmod=wm)
-                    ev_lny = self._event()
-                    o.gemm(yn, w, kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
-                           sC=S * 2 * D, bias=pb("kv_b"), sBias=2 * D, rope=(rt, D, S), wmod=wm,
-                           **kw)
-                    ev_kv = self._event()
-                o.ln(x, P["ln1_g"], pb("ln1_b"), xn, S, D, Z, S * D, S * D, D, pmod=wm)
+            o.ln_dual(x, P["ln1_g"], pb("ln1_b"), xn, P["lny_g"], pb("lny_b"), yn, S, D, Z,
+                      S * D, S * D, D, pmod=wm)
+            self._calib("dec.lny", i, yn, Z)
+            o.gemm(yn, w, kv, S, 2 * D, D, Z, sA=S * D, sB=2 * D * D,
+                   sC=S * 2 * D, bias=pb("kv_b"), sBias=2 * D, rope=(rt, D, S), wmod=wm, **kw)
             self._calib("dec.ln1", i, xn, Z)
             # self-attention
             w, kw = wt("qkv_w", 3 * D)
@@ -927,7 +958,6 @@ class PairModel:
             o.attn(qkv, 3 * D, S * 3 * D, qkv[:, :, D:], qkv[:, :, 2 * D:], 3 * D, S * 3 * D, att,
                    D, S * D, Z, a.dec_heads, S, S)
             self._calib("dec.att", i, att, Z)
-            self._wait(ev_lny)
             w, kw = wt("proj_w", D)
             o.gemm(att, w, x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=pb("proj_b"),
                    sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
@@ -937,7 +967,6 @@ class PairModel:
             w, kw = wt("q_w", D)
             o.gemm(xn, w, q, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=pb("q_b"),
                    sBias=D, rope=(rt, D, S), wmod=wm, **kw)
-            self._wait(ev_kv)
             o.attn(q, D, S * D, kv, kv[:, :, D:], 2 * D, S * 2 * D, att, D, S * D, Z, a.dec_heads,
                    S, S)
             self._calib("dec.catt", i, att, Z)
@@ -954,17 +983,13 @@ class PairModel:
             w, kw = wt("fc2_w", D)
             o.gemm(hid, w, x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D, bias=pb("fc2_b"),
                    sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
-            if (i + 1) in hk:
-                hb = self._buf(f"h{i + 1}", (Z, S, D), BF16)
-                hb.copy_(x)
+            if (i + 1) in hook_bufs:
+                hb = hook_bufs[i + 1]
+                (hb if sl is None else hb[sl]).copy_(x)
                 hooks[f"h{i + 1}"] = hb
                 if on_hook is not None:
                     on_hook(f"h{i + 1}", hooks)
-        h12 = self._buf("h12", (Z, S, D), BF16)
-        o.ln(x, W.dec_norm_g, W.dec_norm_b, h12, S, D, Z, S * D, S * D, D, pmod=wm)
-        hooks["h12"] = h12
-        if on_hook is not None:
-            on_hook("h12", hooks)
+            yield i
         return hooks
 
     def _decode_folded(self, *args, **kw):

@@ -866,12 +866,15 @@ def test_concurrent_encoder_tiles_match_table(dev):
 
 
 @pytest.mark.gpu
-def test_decoder_split_by_model_matches_batched(dev):
+@pytest.mark.parametrize("fp8", [False, True])
+def test_decoder_split_by_model_matches_batched(dev, fp8):
     """dec_split (the two models' decoders as two batch-2 chains on two streams) against the
     batch-4 decoder: the same math on per-shape tiles that may split K differently, so
-    equal up to f32 summation order."""
+    equal up to f32 summation order.  fp8: the unfolded (calibrated e4m3) decoder's split."""
     from monst3r_slam_amd import model as Mdl
     m, _ = Mdl.build(dev)
+    if fp8:
+        m.set_fp8(True)
     g = torch.Generator(device=dev).manual_seed(9)
     img = torch.rand(1, 3, 384, 512, device=dev, generator=g) * 2 - 1
     feat_k = m.encode(torch.rand(1, 3, 384, 512, device=dev, generator=g) * 2 - 1)[0].clone()
