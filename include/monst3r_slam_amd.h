@@ -349,7 +349,8 @@ int m3s_vit_rope_table(const int64_t* d_pos, int64_t tokens, float base, float* 
 
 /* LayerNorm over the last dim (eps), x f32/bf16 [rows][dim] → y (x_is_bf16 flag;
  * y_type 0 bf16, 1 f32, 2 OCP fp8 e4m3 saturated to ±448 — the A operand of the
- * M3S_IN_FP8 GEMMs); batch strides in elements.  dim ≤ 4096, dim % 4 == 0.
+ * M3S_IN_FP8 GEMMs); batch strides in elements.  dim ≤ 4096, dim % 4 == 0; gamma / beta
+ * 16-byte aligned, stride_param % 4 == 0 (else M3S_ERR_INVALID_ARG).
  * param_mod > 0: batch b uses gamma/beta of batch b % param_mod.
  * Batch b of y normalises batch (b ^ x_batch_xor) of x: with x_batch_xor = 1 the
  * decoder's norm_y(other side) (croco/blocks.py:187) runs for both sides in one launch. */
@@ -361,7 +362,7 @@ int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_gamma,
 /* Two LayerNorms of the same f32 rows in one pass (the decoder's norm1 of x and norm_y of
  * the other side, croco/blocks.py:184-187): y[b] = LN(x[b]; gamma/beta of b) and
  * y2[b ^ 1] = LN(x[b]; gamma2/beta2 of b ^ 1), both bf16 (y_fp8 = 0) or both e4m3
- * (y_fp8 = 1); batch even; param_mod as above. */
+ * (y_fp8 = 1); batch even; param_mod and the parameter alignment as above. */
 int m3s_vit_layernorm_dual(const float* d_x, const float* d_gamma, const float* d_beta,
                            void* d_y, const float* d_gamma2, const float* d_beta2, void* d_y2,
                            int y_fp8, int64_t rows, int64_t dim, float eps, int64_t batch,

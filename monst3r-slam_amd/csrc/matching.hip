@@ -331,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void refine_matches_r_kernel(
 //   either form.
 // Every lane of a group computes the merge (7 shuffles of score and row), so the group
 // agrees on (u0, v0) for the next dilation without a broadcast.
-template <int R>
+template <int R, bool BUF>
 __global__ __launch_bounds__(kBlock) void refine_matches_c_kernel(
     const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
     const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
@@ -361,6 +361,8 @@ __global__ __launch_bounds__(kBlock) void refine_matches_c_kernel(
     }
   }
   const uint4* img = reinterpret_cast<const uint4*>(D11 + (int64_t)blockIdx.y * n * 24);
+  const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint4*>(img), (short)0, 0x7ffffff0, 0x00020000);
   // the reference's coordinates are int64; h*w < 2^31 (host check) keeps in-image ones in
   // int; a start point beyond +-2^30 has no in-image candidate at any dilation, so it
   // never moves and the int arithmetic below stays clear of overflow
@@ -383,7 +385,14 @@ __global__ __launch_bounds__(kBlock) void refine_matches_c_kernel(
       ok[jj] = uok && v >= 0 && v < h;
       const int off = ok[jj] ? v * w + u : 0;
 #pragma unroll
-      for (int c = 0; c < 3; c++) buf[jj][c] = img[off * 3 + c];
+      for (int c = 0; c < 3; c++) {
+        if constexpr (BUF) {
+          buf[jj][c] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rD, (unsigned)(off * 3 + c) * 16u, 0, 0));
+        } else {
+          buf[jj][c] = img[off * 3 + c];
+        }
+      }
     }
     _Float16 best = max_score;
     int bj = -1;
@@ -558,10 +567,17 @@ extern "C" int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21,
   static const bool rows = kind && !strcmp(kind, "rows");
   static const bool tile = kind && !strcmp(kind, "tile");
   static const bool lane1 = kind && !strcmp(kind, "lane");  // the one-lane radius-3 kernel
-  if (fdim == 24 && aligned && n == h * w && radius == 3 && h * w < (1LL << 31) && !rows &&
-      !tile && !lane1) {
+  // the column-split kernel's buffer offsets (off * 3 + c) * 16 stay below the descriptor's
+  // 0x7ffffff0-byte range: one image of D11 under 2 GB (h * w < 44.7 M)
+  if (fdim == 24 && aligned && n == h * w && radius == 3 && h * w * 48 < 0x7ffffff0LL &&
+      !rows && !tile && !lane1) {
     dim3 gridq((unsigned)m3s_div_up(h * w, (64 / 7) * (kBlock / 64)), (unsigned)b);
-    hipLaunchKernelGGL(refine_matches_c_kernel<3>, gridq, dim3(kBlock), 0, m3s_stream(stream),
+    // buffer loads (32-bit offsets from one descriptor) by default: 168-172 vs 182-184 us on
+    // a random match field, equal on a coherent one (profiles/r05_refine_buf_ab.txt);
+    // "flat" = 64-bit per-lane addresses
+    static const bool flat = kind && !strcmp(kind, "flat");
+    hipLaunchKernelGGL(flat ? (refine_matches_c_kernel<3, false>) : (refine_matches_c_kernel<3, true>),
+                       gridq, dim3(kBlock), 0, m3s_stream(stream),
                        D11, D21, d_p1, d_p1_new, (int)h, (int)w, dilation_max);
     M3S_LAUNCH_CHECK();
     return M3S_OK;

@@ -11,7 +11,9 @@ namespace {
 // pass writes y[b] = LN(x[b ^ xxor]; params b) and y2[b ^ 1] = LN(x[b]; params2 of b ^ 1)
 // from one set of row statistics (y2 only with xxor == 0).
 // YT: output type 0 bf16, 1 f32, 2 OCP e4m3 (the A operand of the fp8 GEMMs, unscaled).
-template <bool XBF, int YT, bool DUAL = false>
+// MAXV: float4 vectors per lane (dim <= 256 * MAXV).  gamma / beta are requested with the
+// row, before the two reductions, so the launch pays one memory round trip, not two.
+template <bool XBF, int YT, bool DUAL = false, int MAXV = 16>
 __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ x,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
@@ -28,8 +30,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
   const int64_t pb = pmod > 0 ? b % pmod : b;
   const float* g = gamma + pb * sp;
   const float* be = beta + pb * sp;
-  constexpr int MAXV = 16;  // dim <= 64 * 4 * 16 = 4096
+  const int64_t b2 = b ^ 1;
+  const int64_t pb2 = pmod > 0 ? b2 % pmod : b2;
   float v[MAXV][4];
+  float4 gv[MAXV], bv[MAXV], gv2[DUAL ? MAXV : 1], bv2[DUAL ? MAXV : 1];
   const int nvec = dim / 4;
   float s = 0.f;
 #pragma unroll
@@ -50,10 +54,19 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
         v[i][2] = f.z;
         v[i][3] = f.w;
       }
-#pragma unroll
-      for (int k = 0; k < 4; k++) s += v[i][k];
+      gv[i] = reinterpret_cast<const float4*>(g)[c4];
+      bv[i] = reinterpret_cast<const float4*>(be)[c4];
+      if constexpr (DUAL) {
+        gv2[i] = reinterpret_cast<const float4*>(gamma2 + pb2 * sp)[c4];
+        bv2[i] = reinterpret_cast<const float4*>(beta2 + pb2 * sp)[c4];
+      }
     }
   }
+#pragma unroll
+  for (int i = 0; i < MAXV; i++)
+    if (lane + i * 64 < nvec)
+#pragma unroll
+      for (int k = 0; k < 4; k++) s += v[i][k];
   s = m3s_wave_sum(s);
   const float mean = s / (float)dim;
   float ss = 0.f;
@@ -74,9 +87,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
   for (int i = 0; i < MAXV; i++) {
     const int c4 = lane + i * 64;
     if (c4 < nvec) {
+      const float gk[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w};
+      const float bk[4] = {bv[i].x, bv[i].y, bv[i].z, bv[i].w};
       float o[4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) o[k] = (v[i][k] - mean) * rstd * g[4 * c4 + k] + be[4 * c4 + k];
+      for (int k = 0; k < 4; k++) o[k] = (v[i][k] - mean) * rstd * gk[k] + bk[k];
       if constexpr (YT == 1) {
         float* yr = reinterpret_cast<float*>(y) + b * sy + row * dim;
         *reinterpret_cast<float4*>(yr + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
@@ -91,13 +106,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
         *reinterpret_cast<bf16x4*>(yr + 4 * c4) = ob;
       }
       if constexpr (DUAL) {
-        const int64_t b2 = b ^ 1;
-        const int64_t pb2 = pmod > 0 ? b2 % pmod : b2;
-        const float* g2 = gamma2 + pb2 * sp;
-        const float* be2 = beta2 + pb2 * sp;
+        const float gk2[4] = {gv2[i].x, gv2[i].y, gv2[i].z, gv2[i].w};
+        const float bk2[4] = {bv2[i].x, bv2[i].y, bv2[i].z, bv2[i].w};
         float o2[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) o2[k] = (v[i][k] - mean) * rstd * g2[4 * c4 + k] + be2[4 * c4 + k];
+        for (int k = 0; k < 4; k++) o2[k] = (v[i][k] - mean) * rstd * gk2[k] + bk2[k];
         if constexpr (YT == 2) {
           *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(y2) + b2 * sy + row * dim +
                                        4 * c4) = pack4_fp8(o2[0], o2[1], o2[2], o2[3]);
@@ -295,10 +308,21 @@ extern "C" int m3s_vit_layernorm(const void* d_x, int x_is_bf16, const float* d_
   if (dim % 4 || dim > 4096 || dim <= 0 || y_type < 0 || y_type > 2) return M3S_ERR_INVALID_ARG;
   dim3 grid(m3s_div_up(rows, 4), (unsigned)batch);
   hipStream_t s = m3s_stream(stream);
+  // float4 loads of gamma / beta: 16-byte aligned parameter rows
+  if ((uintptr_t)d_gamma % 16 || (uintptr_t)d_beta % 16 || stride_param % 4)
+    return M3S_ERR_INVALID_ARG;
+  const bool narrow = dim <= 1024;
 #define M3S_LN(XB, YT)                                                                        \
-  hipLaunchKernelGGL((layernorm_kernel<XB, YT>), grid, dim3(256), 0, s, d_x, d_gamma, d_beta, \
-                     d_y, rows, (int)dim, eps, stride_x, stride_y, stride_param, param_mod,    \
-                     x_batch_xor)
+  do {                                                                                        \
+  if (narrow)                                                                                 \
+    hipLaunchKernelGGL((layernorm_kernel<XB, YT, false, 4>), grid, dim3(256), 0, s, d_x,      \
+                       d_gamma, d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y,         \
+                       stride_param, param_mod, x_batch_xor);                                 \
+  else                                                                                        \
+    hipLaunchKernelGGL((layernorm_kernel<XB, YT, false, 16>), grid, dim3(256), 0, s, d_x,     \
+                       d_gamma, d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y,         \
+                       stride_param, param_mod, x_batch_xor);                                 \
+  } while (0)
   if (x_is_bf16) {
     if (y_type == 0) M3S_LN(true, 0);
     else if (y_type == 1) M3S_LN(true, 1);
@@ -323,15 +347,23 @@ extern "C" int m3s_vit_layernorm_dual(const float* d_x, const float* d_gamma,
       batch <= 0 || batch % 2)
     return M3S_ERR_INVALID_ARG;
   if (dim % 4 || dim > 4096 || dim <= 0) return M3S_ERR_INVALID_ARG;
+  if ((uintptr_t)d_gamma % 16 || (uintptr_t)d_beta % 16 || (uintptr_t)d_gamma2 % 16 ||
+      (uintptr_t)d_beta2 % 16 || stride_param % 4)
+    return M3S_ERR_INVALID_ARG;
   dim3 grid(m3s_div_up(rows, 4), (unsigned)batch);
-  if (y_fp8)
-    hipLaunchKernelGGL((layernorm_kernel<false, 2, true>), grid, dim3(256), 0,
-                       m3s_stream(stream), d_x, d_gamma, d_beta, d_y, rows, (int)dim, eps,
-                       stride_x, stride_y, stride_param, param_mod, 0, d_gamma2, d_beta2, d_y2);
-  else
-    hipLaunchKernelGGL((layernorm_kernel<false, 0, true>), grid, dim3(256), 0,
-                       m3s_stream(stream), d_x, d_gamma, d_beta, d_y, rows, (int)dim, eps,
-                       stride_x, stride_y, stride_param, param_mod, 0, d_gamma2, d_beta2, d_y2);
+  hipStream_t s = m3s_stream(stream);
+#define M3S_LN2(YT, MV)                                                                       \
+  hipLaunchKernelGGL((layernorm_kernel<false, YT, true, MV>), grid, dim3(256), 0, s, d_x,     \
+                     d_gamma, d_beta, d_y, rows, (int)dim, eps, stride_x, stride_y,           \
+                     stride_param, param_mod, 0, d_gamma2, d_beta2, d_y2)
+  if (dim <= 1024) {
+    if (y_fp8) M3S_LN2(2, 4);
+    else M3S_LN2(0, 4);
+  } else {
+    if (y_fp8) M3S_LN2(2, 16);
+    else M3S_LN2(0, 16);
+  }
+#undef M3S_LN2
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }
