@@ -161,7 +161,7 @@ def kernel_rooflines(tr, out, dev):
     res = {}
     for name, fn, nbytes, note in (
             ("iter_proj", iproj, 65 * n, "65 B/pixel"),
-            ("refine_matches", refine, 128 * n, "128 B/pixel; VALU-bound (1.16 G f16 FMA)"),
+            ("refine_matches", refine, 128 * n, "128 B/pixel; bound by the vector-L1 address path (TA busy 88 %, profiles/r05_refine_pmc.txt), not HBM"),
             ("track_gn", gn, 29 * n * iters, f"29 B/pixel/iteration x {iters} iterations "
                                              "(init + persistent GN + finish launches)")):
         ms = replay_ms(fn, dev)
