@@ -377,6 +377,36 @@ def test_layernorm_dual(ops, dev):
     assert _rel(y, ref1) < 1e-2 and _rel(y2, ref2) < 1e-2
 
 
+@pytest.mark.parametrize("dim", [1028, 2048, 4096])
+def test_layernorm_wide_rows(ops, dev, dim):
+    """dim > 1024: the 16-vectors-per-lane variant, single and dual (γ/β requested with the
+    row in both)."""
+    g = torch.Generator(device=dev).manual_seed(dim)
+    x = torch.randn(4, 40, dim, device=dev, generator=g) * 2 + 0.3
+    g1, b1, g2, b2 = (torch.randn(2, dim, device=dev, generator=g) for _ in range(4))
+    y = torch.empty(4, 40, dim, device=dev, dtype=torch.bfloat16)
+    y2 = torch.empty_like(y)
+    ops.ln(x, g1, b1, y, 40, dim, 4, 40 * dim, 40 * dim, dim, pmod=2)
+    ref = torch.stack([F.layer_norm(x[b], (dim,), g1[b % 2], b1[b % 2], 1e-6) for b in range(4)])
+    assert _rel(y, ref) < 1e-2
+    ops.ln_dual(x, g1, b1, y, g2, b2, y2, 40, dim, 4, 40 * dim, 40 * dim, dim, pmod=2)
+    ref2 = torch.stack([F.layer_norm(x[b ^ 1], (dim,), g2[b % 2], b2[b % 2], 1e-6)
+                        for b in range(4)])
+    assert _rel(y, ref) < 1e-2 and _rel(y2, ref2) < 1e-2
+
+
+def test_layernorm_rejects_misaligned_params(ops, dev):
+    """γ / β are read as 16-byte vectors: a misaligned row is an argument error, not a
+    misaligned read."""
+    x = torch.randn(2, 8, 768, device=dev)
+    gb = torch.randn(2 * 768 + 1, device=dev)
+    y = torch.empty(2, 8, 768, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="vit_layernorm"):
+        ops.ln(x, gb[1:769], gb[769:], y, 8, 768, 2, 8 * 768, 8 * 768, 0)
+    with pytest.raises(RuntimeError, match="vit_layernorm"):
+        ops.ln(x, gb[:768], gb[768:1536], y, 8, 768, 2, 8 * 768, 8 * 768, 3)
+
+
 def _fp8(t):
     return t.clamp(-448, 448).to(torch.float8_e4m3fn)
 
