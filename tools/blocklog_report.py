@@ -16,7 +16,7 @@ a, b = gr[gi]
 sel = (sl >= a) & (sl < b)
 L, S = lg[sel], sl[sel] - a
 launches = tl["launches"]
-agg = defaultdict(lambda: np.zeros(8))
+agg = defaultdict(lambda: np.zeros(9))
 for s in np.unique(S):
     m = S == s
     x = L[m].astype(np.float64)
@@ -27,15 +27,18 @@ for s in np.unique(S):
     first = (ph[ok, 1] - ph[ok, 0]) * 1e-2
     loop = (ph[ok, 2] - ph[ok, 1]) * 1e-2
     epi = (x[ok, 1] - ph[ok, 2]) * 1e-2
+    # epilogue split at mark 3: operand setup + accumulators → LDS + barrier, then the
+    # vector pass (LDS reads, epilogue math, stores)
+    e_lds = (ph[ok, 3] - ph[ok, 2]) * 1e-2
     ln = launches[s] if s < len(launches) else {"kind": "?", "dims": []}
     key = (ln["kind"], tuple(ln["dims"]), int(m.sum()))
     v = agg[key]
     v += [1, life.mean(), pro.mean() if ok.any() else 0, first.mean() if ok.any() else 0,
           loop.mean() if ok.any() else 0, epi.mean() if ok.any() else 0,
-          (ln.get("gflop") or 0), 0]
+          (ln.get("gflop") or 0), 0, e_lds.mean() if ok.any() else 0]
 rows = sorted(agg.items(), key=lambda kv: -kv[1][0] * kv[1][1] * kv[0][2])
-print("kind  dims                          blocks  n   life  prolog first  kloop   epi  (us, mean per block)")
+print("kind  dims                          blocks  n   life  prolog first  kloop   epi (to-LDS  vec)  (us, mean per block)")
 for (kind, dims, nb), v in rows:
     n = v[0]
     print(f"{kind:5s} {str(list(dims)):28s} {nb:6d} {int(n):3d} {v[1]/n:6.1f} {v[2]/n:6.2f} "
-          f"{v[3]/n:6.2f} {v[4]/n:6.1f} {v[5]/n:6.2f}")
+          f"{v[3]/n:6.2f} {v[4]/n:6.1f} {v[5]/n:6.2f} ({v[8]/n:5.2f} {(v[5]-v[8])/n:5.2f})")
