@@ -331,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void refine_matches_r_kernel(
 //   either form.
 // Every lane of a group computes the merge (7 shuffles of score and row), so the group
 // agrees on (u0, v0) for the next dilation without a broadcast.
-template <int R, bool BUF>
+template <int R, bool BUF, bool TILE = false>
 __global__ __launch_bounds__(kBlock) void refine_matches_c_kernel(
     const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
     const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
@@ -340,7 +340,10 @@ __global__ __launch_bounds__(kBlock) void refine_matches_c_kernel(
   constexpr int QW = 64 / S;                 // queries per wave
   constexpr int QB = QW * (kBlock / 64);     // queries per workgroup
   const int n = h * w;
-  const int nblk = (n + QB - 1) / QB;
+  // TILE: a workgroup takes a QW x 4 pixel tile (one image row per wave) instead of QB
+  // consecutive pixels, so its windows overlap in both directions
+  const int tiles_x = (w + QW - 1) / QW;
+  const int nblk = TILE ? tiles_x * ((h + 3) / 4) : (n + QB - 1) / QB;
   const int lin = blockIdx.x, xcd = lin & 7, loc = lin >> 3;
   const int tq = nblk >> 3, tr = nblk & 7;
   const int t = xcd < tr ? xcd * (tq + 1) + loc : tr * (tq + 1) + (xcd - tr) * tq + loc;
@@ -348,8 +351,17 @@ __global__ __launch_bounds__(kBlock) void refine_matches_c_kernel(
   const int grp = lane / S, ii = lane - grp * S, base = grp * S;
   // every lane takes part in the shuffles: the idle lane and queries past the end run a
   // clamped query and store nothing
-  const int qi = t * QB + wv * QW + grp;
-  const bool qok = grp < QW && qi < n;
+  int qi;
+  bool qok;
+  if constexpr (TILE) {
+    const int ty = t / tiles_x, tx = t - ty * tiles_x;
+    const int px = tx * QW + grp, py = ty * 4 + wv;
+    qok = grp < QW && px < w && py < h;
+    qi = qok ? py * w + px : 0;
+  } else {
+    qi = t * QB + wv * QW + grp;
+    qok = grp < QW && qi < n;
+  }
   const int64_t q = (int64_t)blockIdx.y * n + min(qi, n - 1);
   _Float16 qd[24];
   {
@@ -571,7 +583,20 @@ extern "C" int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21,
   // 0x7ffffff0-byte range: one image of D11 under 2 GB (h * w < 44.7 M)
   if (fdim == 24 && aligned && n == h * w && radius == 3 && h * w * 48 < 0x7ffffff0LL &&
       !rows && !tile && !lane1) {
-    dim3 gridq((unsigned)m3s_div_up(h * w, (64 / 7) * (kBlock / 64)), (unsigned)b);
+    // 9 x 4 pixel tiles per workgroup (one row per wave): 165-167 vs 170-172 us on a random
+    // match field, coherent unchanged (profiles/r05_refine_tile2_ab.txt); "rowmajor" = 36
+    // consecutive pixels per workgroup
+    static const bool tile2 = !(kind && !strcmp(kind, "rowmajor"));
+    dim3 gridq((unsigned)(tile2 ? m3s_div_up(w, 64 / 7) * m3s_div_up(h, kBlock / 64)
+                                : m3s_div_up(h * w, (64 / 7) * (kBlock / 64))),
+               (unsigned)b);
+    if (tile2) {
+      hipLaunchKernelGGL((refine_matches_c_kernel<3, true, true>), gridq, dim3(kBlock), 0,
+                         m3s_stream(stream), D11, D21, d_p1, d_p1_new, (int)h, (int)w,
+                         dilation_max);
+      M3S_LAUNCH_CHECK();
+      return M3S_OK;
+    }
     // buffer loads (32-bit offsets from one descriptor) by default: 168-172 vs 182-184 us on
     // a random match field, equal on a coherent one (profiles/r05_refine_buf_ab.txt);
     // "flat" = 64-bit per-lane addresses
