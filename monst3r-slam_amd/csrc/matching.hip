@@ -331,19 +331,19 @@ __global__ __launch_bounds__(kBlock) void refine_matches_r_kernel(
 //   either form.
 // Every lane of a group computes the merge (7 shuffles of score and row), so the group
 // agrees on (u0, v0) for the next dilation without a broadcast.
-template <int R, bool BUF, bool TILE = false>
-__global__ __launch_bounds__(kBlock) void refine_matches_c_kernel(
+template <int R, bool BUF, bool TILE = false, int RB = kBlock / 64>
+__global__ __launch_bounds__(64 * RB) void refine_matches_c_kernel(
     const _Float16* __restrict__ D11, const _Float16* __restrict__ D21,
     const int64_t* __restrict__ p1, int64_t* __restrict__ p1_new, int h, int w,
     int dilation_max) {
   constexpr int S = 2 * R + 1;
   constexpr int QW = 64 / S;                 // queries per wave
-  constexpr int QB = QW * (kBlock / 64);     // queries per workgroup
+  constexpr int QB = QW * RB;                // queries per workgroup (RB waves)
   const int n = h * w;
   // TILE: a workgroup takes a QW x 4 pixel tile (one image row per wave) instead of QB
   // consecutive pixels, so its windows overlap in both directions
   const int tiles_x = (w + QW - 1) / QW;
-  const int nblk = TILE ? tiles_x * ((h + 3) / 4) : (n + QB - 1) / QB;
+  const int nblk = TILE ? tiles_x * ((h + RB - 1) / RB) : (n + QB - 1) / QB;
   const int lin = blockIdx.x, xcd = lin & 7, loc = lin >> 3;
   const int tq = nblk >> 3, tr = nblk & 7;
   const int t = xcd < tr ? xcd * (tq + 1) + loc : tr * (tq + 1) + (xcd - tr) * tq + loc;
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(kBlock) void refine_matches_c_kernel(
   bool qok;
   if constexpr (TILE) {
     const int ty = t / tiles_x, tx = t - ty * tiles_x;
-    const int px = tx * QW + grp, py = ty * 4 + wv;
+    const int px = tx * QW + grp, py = ty * RB + wv;
     qok = grp < QW && px < w && py < h;
     qi = qok ? py * w + px : 0;
   } else {
@@ -583,14 +583,31 @@ extern "C" int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21,
   // 0x7ffffff0-byte range: one image of D11 under 2 GB (h * w < 44.7 M)
   if (fdim == 24 && aligned && n == h * w && radius == 3 && h * w * 48 < 0x7ffffff0LL &&
       !rows && !tile && !lane1) {
-    // 9 x 4 pixel tiles per workgroup (one row per wave): 165-167 vs 170-172 us on a random
-    // match field, coherent unchanged (profiles/r05_refine_tile2_ab.txt); "rowmajor" = 36
-    // consecutive pixels per workgroup
+    // 9-pixel-wide tiles per workgroup (one image row per wave), 8 rows by default: the
+    // windows of a workgroup overlap in both directions (profiles/r05_refine_tile2_ab.txt);
+    // "rowmajor" = 36 consecutive pixels per workgroup
     static const bool tile2 = !(kind && !strcmp(kind, "rowmajor"));
     dim3 gridq((unsigned)(tile2 ? m3s_div_up(w, 64 / 7) * m3s_div_up(h, kBlock / 64)
                                 : m3s_div_up(h * w, (64 / 7) * (kBlock / 64))),
                (unsigned)b);
     if (tile2) {
+      // rows per workgroup (M3S_REFINE_RB A/B: 4 | 8 | 16): 9 x 8 tiles of 512 threads
+      // measured fastest (random 165 → 159.6 us, coherent 130.6 → 128.6;
+      // profiles/r05_refine_tile2_ab.txt)
+      static const int rbk = getenv("M3S_REFINE_RB") ? atoi(getenv("M3S_REFINE_RB")) : 8;
+      if (rbk == 8 || rbk == 16) {
+        dim3 g2((unsigned)(m3s_div_up(w, 64 / 7) * m3s_div_up(h, rbk)), (unsigned)b);
+        if (rbk == 8)
+          hipLaunchKernelGGL((refine_matches_c_kernel<3, true, true, 8>), g2, dim3(512), 0,
+                             m3s_stream(stream), D11, D21, d_p1, d_p1_new, (int)h, (int)w,
+                             dilation_max);
+        else
+          hipLaunchKernelGGL((refine_matches_c_kernel<3, true, true, 16>), g2, dim3(1024), 0,
+                             m3s_stream(stream), D11, D21, d_p1, d_p1_new, (int)h, (int)w,
+                             dilation_max);
+        M3S_LAUNCH_CHECK();
+        return M3S_OK;
+      }
       hipLaunchKernelGGL((refine_matches_c_kernel<3, true, true>), gridq, dim3(kBlock), 0,
                          m3s_stream(stream), D11, D21, d_p1, d_p1_new, (int)h, (int)w,
                          dilation_max);
