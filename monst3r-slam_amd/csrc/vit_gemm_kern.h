@@ -355,17 +355,15 @@ __device__ __forceinline__ bf16x8 relu_frag(bf16x8 x) {
 __device__ long long* g_m3s_stamps;
 #define M3S_T(v) long long v = (long long)__builtin_amdgcn_s_memtime()
 // [0] prologue [1] vmcnt wait [2] barrier [3] MFMA phases (per-K-tile sums) [4] epilogue
-// [5] K-tiles [6] block total [7] start (shader cycles) [8..11] epilogue parts
+// [5] K-tiles [6] block total [7] start (shader cycles) [8] epilogue ([9..11] unused)
 // [12] / [13] s_memrealtime (100 MHz) at start / end [14] 1 = early exit (non-last split)
 // [15] first K-tile wait (prologue issue → first fragments read) [16] tail K-tiles
 #define M3S_STAMP_OUT_(early)                                                     \
   if (tid == 0) {                                                                 \
     M3S_T(t_end);                                                                 \
     long long* o = g_m3s_stamps + (int64_t)blockIdx.x * 20;                       \
-    o[8] = t_e0 - t_loop;                                                         \
-    o[9] = t_e1 - t_e0;                                                           \
-    o[10] = t_e2 - t_e1;                                                          \
-    o[11] = t_end - t_e2;                                                         \
+    o[8] = t_end - t_loop;                                                        \
+    o[9] = o[10] = o[11] = 0;                                                     \
     o[0] = t_pro - t_start;                                                       \
     o[1] = s_wait;                                                                \
     o[2] = s_bar;                                                                 \
@@ -387,6 +385,429 @@ __device__ long long* g_m3s_stamps;
 #define M3S_STAMP_OUT()
 #define M3S_STAMP_EARLY()
 #endif
+
+// ---------------------------------------------------------------------------------------
+// epilogue (shared by gemm_kernel and the 256x256 ping-pong gemm_pp_kernel)
+// ---------------------------------------------------------------------------------------
+// The block's f32 accumulator tile goes through LDS in PASSES passes of BM / PASSES rows:
+// store_acc(pass, cs) writes the accumulators of that pass's rows into cs[row][CST]
+// (CST = BN + 4), then row-contiguous 8-column vectors per thread run the fused epilogue
+// (bias, LayerNorm fold, GELU, RoPE, residual, ReLU, f32 / bf16 / e4m3 stores, LayerNorm
+// statistics, ConvTranspose scatter, the DPT tail) — or, split-K, the slice's partial
+// tile is published and the tile's last slice reduces.  Returns false for a split-K slice
+// that is not its tile's last (it stored nothing).
+template <int BM, int BN, int NT, int PASSES, int LDS_BYTES, bool SPLIT, int EPI, class StoreAcc>
+__device__ __forceinline__ bool gemm_epilogue(const Args& a, char* lds, int g, int zz, int nwg,
+                                              int wgid, int split, int m0, int n0,
+                                              M3sTlEnd& tl_end, StoreAcc&& store_acc) {
+  constexpr int CST = BN + 4;
+  constexpr int EROWS = BM / PASSES;
+  constexpr bool DPT = EPI >= 0 && (EPI & M3S_EPI_DPT_OUT) != 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  constexpr int VPR = BN / 8;                 // 8-column vectors per row
+  static_assert(PASSES == 1 || !SPLIT, "two-pass epilogue: unsplit");
+  constexpr int NV = EROWS * VPR / NT;        // vectors per thread (per pass)
+  constexpr int RSTEP = NT / VPR;             // rows between one thread's vectors
+  static_assert(NT % VPR == 0, "epilogue layout");
+  // Vector path: a thread owns columns [n, n+8) of rows r0 + v*RSTEP.  Its bias and, per
+  // group of EG vectors, the residual (or RoPE cos/sin) operands are loaded ahead of use —
+  // the first group before the LDS round trip — so their latency is overlapped.
+  // EG must divide NV (96-row tiles have NV = 6: groups of 4 would run past the tile into
+  // the next tile's rows)
+  constexpr int EG = NV % 4 == 0 ? 4 : NV % 3 == 0 ? 3 : NV % 2 == 0 ? 2 : 1;
+  const int ec = (tid % VPR) * 8, er0 = tid / VPR;
+  const int en = n0 + ec;
+  const int fl = EPI >= 0 ? EPI : a.flags;
+  const bool vec = EPI >= 0 ? true : (a.vec != 0);
+  const bool vec_path = vec && en < a.N;
+  float e_b[8], e_pb[8], e_x[EG][16];
+  float e_c1[8], e_pc1[8], e_mu[EG], e_rs[EG];  // LN_FOLD: c1 columns, row mean / rstd
+  // LN_FOLD: the 16 lanes of a row group own rows er0 + v·RSTEP (v < NV ≤ 16); lane v
+  // combines the statistics of row v once, the others read it by lane shuffle
+  float ln_mu = 0.f, ln_rs = 0.f;
+  static_assert(NV <= 16, "one row per lane of the group");
+  int rb = 0;                                 // first tile row of the epilogue pass
+  auto ln_setup = [&]() {
+    if ((fl & M3S_EPI_LN_FOLD) && (lane & 15) < NV)
+      ln_row_stats(a, g ^ a.a_xor, min(m0 + rb + er0 + (lane & 15) * RSTEP, a.M - 1), a.K >> 7,
+                   ln_mu, ln_rs);
+  };
+  Epi e = make_epi(a, g);
+  e.flags = fl;
+  const bool e_rope = (fl & M3S_EPI_ROPE) && en < a.rope_cols;
+  auto e_prefetch = [&](int v0) {
+#pragma unroll
+    for (int u = 0; u < EG; u++) {
+      const int m = min(m0 + rb + er0 + (v0 + u) * RSTEP, a.M - 1);  // rows ≥ M are not stored
+      if (fl & M3S_EPI_LN_FOLD) {  // row v0 + u's statistics, held by lane v0 + u of the row group
+        const int src = (lane & ~15) | (v0 + u);
+        e_mu[u] = __shfl(ln_mu, src, 64);
+        e_rs[u] = __shfl(ln_rs, src, 64);
+      }
+#pragma unroll
+      for (int t = 0; t < 16; t++) e_x[u][t] = 0.f;
+      if (fl & M3S_EPI_RES_F32) {
+        const float* r = reinterpret_cast<const float*>(e.R) + (int64_t)m * e.ldr + en;
+        *reinterpret_cast<float4*>(&e_x[u][0]) = *reinterpret_cast<const float4*>(r);
+        *reinterpret_cast<float4*>(&e_x[u][4]) = *reinterpret_cast<const float4*>(r + 4);
+      } else if (fl & M3S_EPI_RES_BF16) {
+        const bf16x8 r = *reinterpret_cast<const bf16x8*>(
+            reinterpret_cast<const bf16_t*>(e.R) + (int64_t)m * e.ldr + en);
+#pragma unroll
+        for (int t = 0; t < 8; t++) e_x[u][t] = bf2f(r[t]);
+      } else if (e_rope) {  // RoPE GEMMs carry no residual: cos → [0, 8), sin → [8, 16)
+        const float* tb = e.rope_tab +
+                          ((int64_t)(m % e.rope_tokens) * 2 + ((en >> 5) & 1)) * 32 + (en & 15);
+        *reinterpret_cast<float4*>(&e_x[u][0]) = *reinterpret_cast<const float4*>(tb);
+        *reinterpret_cast<float4*>(&e_x[u][4]) = *reinterpret_cast<const float4*>(tb + 4);
+        *reinterpret_cast<float4*>(&e_x[u][8]) = *reinterpret_cast<const float4*>(tb + 16);
+        *reinterpret_cast<float4*>(&e_x[u][12]) = *reinterpret_cast<const float4*>(tb + 20);
+      }
+    }
+  };
+  auto epi_setup = [&](bool prefetch_rows) {
+    if (!vec_path) return;
+    int co;
+    (void)out_offset(e, m0, en, co);
+#pragma unroll
+    for (int t = 0; t < 8; t++) e_b[t] = e_pb[t] = 0.f;
+    if (e.bias) {
+      *reinterpret_cast<float4*>(&e_b[0]) = *reinterpret_cast<const float4*>(e.bias + co);
+      *reinterpret_cast<float4*>(&e_b[4]) = *reinterpret_cast<const float4*>(e.bias + co + 4);
+      if (e_rope) {
+        *reinterpret_cast<float4*>(&e_pb[0]) = *reinterpret_cast<const float4*>(e.bias + (en ^ 16));
+        *reinterpret_cast<float4*>(&e_pb[4]) =
+            *reinterpret_cast<const float4*>(e.bias + (en ^ 16) + 4);
+      }
+    }
+    if (fl & M3S_EPI_LN_FOLD) {
+      const float* c1 = a.ln_c1 + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sBias;
+      *reinterpret_cast<float4*>(&e_c1[0]) = *reinterpret_cast<const float4*>(c1 + en);
+      *reinterpret_cast<float4*>(&e_c1[4]) = *reinterpret_cast<const float4*>(c1 + en + 4);
+      if (e_rope) {
+        *reinterpret_cast<float4*>(&e_pc1[0]) = *reinterpret_cast<const float4*>(c1 + (en ^ 16));
+        *reinterpret_cast<float4*>(&e_pc1[4]) =
+            *reinterpret_cast<const float4*>(c1 + (en ^ 16) + 4);
+      }
+    }
+    if (prefetch_rows) e_prefetch(0);
+  };
+  if (!SPLIT) epi_setup(false);   // split-K: only the tile's last split needs the operands
+  float* cs = reinterpret_cast<float*>(lds);
+  // DPT tail operands: w4 [4][128] then the conv bias [128] (zeros without BIAS), requested
+  // now and written beside the tile after the K-loop's last LDS reads
+  float4 dpt_stage = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (DPT) {
+    const int gw = a.wmod > 0 ? g % a.wmod : g;
+    if (tid < 128)
+      dpt_stage = reinterpret_cast<const float4*>(a.dpt_w4 + (int64_t)gw * 512)[tid];
+    else if (tid < 160 && (EPI & M3S_EPI_BIAS))
+      dpt_stage = reinterpret_cast<const float4*>(a.bias + (int64_t)gw * a.sBias)[tid - 128];
+  }
+#pragma unroll
+  for (int pass = 0; pass < PASSES; pass++) {
+  rb = pass * EROWS;
+  if (!SPLIT) {
+    ln_setup();
+    if (vec_path) e_prefetch(0);
+  }
+  block_sync_lds();
+  store_acc(pass, cs);
+  if constexpr (DPT) {
+    if (tid < 160)
+      reinterpret_cast<float4*>(lds + LDS_BYTES + 16)[tid] = dpt_stage;
+  }
+  block_sync_lds();
+  tl_end.mark(3);
+
+  if constexpr (DPT) {
+    // fused DPT tail, all BN = 128 channels of a pixel (row) in the LDS tile: TPR threads
+    // per row (every thread of the block busy: 2-4 per row) each take 32 / TPR of the
+    // row's 4-channel groups — group q = (k % G) + G·h + 16·(k / G), G = 16 / TPR, so the
+    // 16 lanes of one ds_read_b128 hit 16 different bank quads — against the 1x1 weights
+    // and bias staged in LDS (broadcast reads), then the TPR partial sums meet by lane
+    // shuffle.  (One row per thread with the weights read from global memory took 8.8 us
+    // of a 27 us head.2 block in the C3 step: the block log, round 5.)
+    static_assert(BN == 128 && !SPLIT && PASSES == 1,
+                  "DPT_OUT needs the full 128-channel row in one tile");
+    constexpr int TPR = NT >= BM ? NT / BM : 1;
+    static_assert(TPR == 1 || TPR == 2 || TPR == 4 || TPR == 8, "threads per row");
+    constexpr int G = 16 / (TPR > 16 ? 16 : TPR);
+    const int gw = a.wmod > 0 ? g % a.wmod : g;
+    const float* b4 = a.dpt_b4 + (int64_t)gw * 4;
+    const float b40 = b4[0], b41 = b4[1], b42 = b4[2], b43 = b4[3];
+    const float* wl = reinterpret_cast<const float*>(lds + LDS_BYTES + 16);
+    const float* bl = wl + 512;
+    const int h = tid % TPR;
+    for (int row = tid / TPR; row < BM; row += NT / TPR) {
+      const int m = m0 + row;
+      float o4[4] = {0.f, 0.f, 0.f, 0.f};
+      const float* src = cs + row * CST;
+#pragma unroll 8
+      for (int k = 0; k < 32 / TPR; k++) {
+        const int c = 4 * ((k % G) + G * h + 16 * (k / G));
+        float4 x = *reinterpret_cast<const float4*>(src + c);
+        if constexpr ((EPI & M3S_EPI_BIAS) != 0) {
+          const float4 bb = *reinterpret_cast<const float4*>(bl + c);
+          x.x += bb.x;
+          x.y += bb.y;
+          x.z += bb.z;
+          x.w += bb.w;
+        }
+        x.x = fmaxf(x.x, 0.f);
+        x.y = fmaxf(x.y, 0.f);
+        x.z = fmaxf(x.z, 0.f);
+        x.w = fmaxf(x.w, 0.f);
+#pragma unroll
+        for (int oo = 0; oo < 4; oo++) {
+          const float4 w = *reinterpret_cast<const float4*>(wl + oo * 128 + c);
+          o4[oo] += w.x * x.x + w.y * x.y + w.z * x.z + w.w * x.w;
+        }
+      }
+#pragma unroll
+      for (int off = 1; off < TPR; off <<= 1)
+#pragma unroll
+        for (int oo = 0; oo < 4; oo++) o4[oo] += __shfl_xor(o4[oo], off, 64);
+      if (h == 0 && m < a.M) {
+        o4[0] += b40;
+        o4[1] += b41;
+        o4[2] += b42;
+        o4[3] += b43;
+        // reg_dense_depth('exp') + conf ('exp', conf_min): as dpt_out_kernel (vit_misc.hip)
+        const float d = sqrtf(o4[0] * o4[0] + o4[1] * o4[1] + o4[2] * o4[2]);
+        const float sc = expm1f(d) / fmaxf(d, 1e-8f);
+        float* P = a.dpt_pts + ((int64_t)g * a.M + m) * 3;
+        P[0] = o4[0] * sc;
+        P[1] = o4[1] * sc;
+        P[2] = o4[2] * sc;
+        a.dpt_conf[(int64_t)g * a.M + m] = a.dpt_conf_min + expf(o4[3]);
+      }
+    }
+    return true;
+  }
+
+  if constexpr (SPLIT) {
+    // publish this split's partial tile; the tile's last split sums them all
+    int& s_last = *reinterpret_cast<int*>(lds + LDS_BYTES);
+    const int64_t per_b = (int64_t)a.M * a.N;
+    float* P = a.ws + (int64_t)zz * per_b;
+#pragma unroll 4
+    for (int v = 0; v < NV; v++) {
+      const int idx = v * NT + tid;
+      const int row = idx / VPR, c = (idx % VPR) * 8;
+      const int m = m0 + row, n = n0 + c;
+      if (m >= a.M || n >= a.N) continue;
+      const float* src = cs + row * CST + c;
+      float* dst = P + (int64_t)m * a.N + n;
+      if (vec) {
+        *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+        *reinterpret_cast<float4*>(dst + 4) = *reinterpret_cast<const float4*>(src + 4);
+      } else {
+        for (int t = 0; t < 8 && n + t < a.N; t++) dst[t] = src[t];
+      }
+    }
+    if (!a.fused) return false;  // splitk_reduce_kernel follows
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      // the fence's own wait can be dropped by the compiler: wait here, before the ticket
+      // (cdna_hip_programming.md Guideline 16, Pitfall 12)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int* ctr = a.cnt + (int64_t)g * nwg + wgid;
+      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == a.splits - 1;
+      if (s_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    ln_setup();
+    epi_setup(true);
+    const float* P0 = a.ws + (int64_t)g * a.splits * per_b;
+    // slab by slab, all of this thread's vectors of a slab in flight at once (one L2
+    // round trip per slab instead of one per vector); the sum stays in split order
+    float xs[NV][8];
+#pragma unroll
+    for (int v = 0; v < NV; v++)
+#pragma unroll
+      for (int t = 0; t < 8; t++) xs[v][t] = 0.f;
+    for (int k = 0; k < a.splits; k++) {
+      float ys[NV][8];
+#pragma unroll
+      for (int v = 0; v < NV; v++) {
+        const int idx = v * NT + tid;
+        const int row = idx / VPR, c = (idx % VPR) * 8;
+        const int m = m0 + row, n = n0 + c;
+        const float* src = cs + row * CST + c;
+        if (k == split) {  // this workgroup's own partial is still in LDS
+          *reinterpret_cast<float4*>(&ys[v][0]) = *reinterpret_cast<const float4*>(src);
+          *reinterpret_cast<float4*>(&ys[v][4]) = *reinterpret_cast<const float4*>(src + 4);
+        } else if (m < a.M && vec && n < a.N) {
+          const float* q = P0 + k * per_b + (int64_t)m * a.N + n;
+          *reinterpret_cast<float4*>(&ys[v][0]) = *reinterpret_cast<const float4*>(q);
+          *reinterpret_cast<float4*>(&ys[v][4]) = *reinterpret_cast<const float4*>(q + 4);
+        } else {
+          const float* q = P0 + k * per_b + (int64_t)m * a.N + n;
+#pragma unroll
+          for (int t = 0; t < 8; t++) ys[v][t] = (m < a.M && n + t < a.N) ? q[t] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < NV; v++)
+#pragma unroll
+        for (int t = 0; t < 8; t++) xs[v][t] += ys[v][t];
+    }
+    block_sync_lds();  // every own-slab LDS read above is done before the overwrite
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      const int idx = v * NT + tid;
+      const int row = idx / VPR, c = (idx % VPR) * 8;
+      float* dst = cs + row * CST + c;
+      *reinterpret_cast<float4*>(dst) = make_float4(xs[v][0], xs[v][1], xs[v][2], xs[v][3]);
+      *reinterpret_cast<float4*>(dst + 4) = make_float4(xs[v][4], xs[v][5], xs[v][6], xs[v][7]);
+    }
+    block_sync_lds();
+  }
+  if (vec_path) {
+    const float sg = (en & 16) ? 1.f : -1.f;
+    const bool has_res = fl & (M3S_EPI_RES_F32 | M3S_EPI_RES_BF16);
+    const bool rope_now = e_rope && !has_res;
+    // per group: all LDS reads first, then the math and the global stores (a ds_read issued
+    // after a global store waits for that store: the compiler cannot prove it does not
+    // alias the LDS-DMA ring — one such wait per group instead of one per vector)
+#pragma unroll
+    for (int v0 = 0; v0 < NV; v0 += EG) {
+      if (v0 > 0) e_prefetch(v0);
+      float xv[EG][8], pv[EG][8];
+#pragma unroll
+      for (int u = 0; u < EG; u++) {
+        const int row = er0 + (v0 + u) * RSTEP;
+        const float* src = cs + row * CST + ec;
+        *reinterpret_cast<float4*>(&xv[u][0]) = *reinterpret_cast<const float4*>(src);
+        *reinterpret_cast<float4*>(&xv[u][4]) = *reinterpret_cast<const float4*>(src + 4);
+        if (rope_now) {
+          const float* psrc = cs + row * CST + (ec ^ 16);
+          *reinterpret_cast<float4*>(&pv[u][0]) = *reinterpret_cast<const float4*>(psrc);
+          *reinterpret_cast<float4*>(&pv[u][4]) = *reinterpret_cast<const float4*>(psrc + 4);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < EG; u++) {
+        const int m = m0 + rb + er0 + (v0 + u) * RSTEP;
+        if (m >= a.M) continue;
+        float* x = xv[u];
+        if (fl & M3S_EPI_LN_FOLD) {  // LN(x) W^T + b = rstd (acc - mean c1) + c2
+#pragma unroll
+          for (int t = 0; t < 8; t++) x[t] = fmaf(e_rs[u], fmaf(-e_mu[u], e_c1[t], x[t]), e_b[t]);
+          if (rope_now) {  // the partner columns' final values
+#pragma unroll
+            for (int t = 0; t < 8; t++)
+              pv[u][t] = fmaf(e_rs[u], fmaf(-e_mu[u], e_pc1[t], pv[u][t]), e_pb[t]);
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 8; t++) x[t] += e_b[t];
+          if (rope_now) {
+#pragma unroll
+            for (int t = 0; t < 8; t++) pv[u][t] += e_pb[t];
+          }
+        }
+        if (fl & M3S_EPI_GELU) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) x[t] = gelu_erf(x[t]);
+        }
+        if (rope_now) {
+#pragma unroll
+          for (int t = 0; t < 8; t++)
+            x[t] = x[t] * e_x[u][t] + sg * pv[u][t] * e_x[u][8 + t];
+        }
+        if (has_res) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) x[t] += e_x[u][t];
+        }
+        if (fl & M3S_EPI_RELU) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) x[t] = fmaxf(x[t], 0.f);
+        }
+        int co;
+        const int64_t off = out_offset(e, m, en, co);
+        if (fl & M3S_EPI_OUT_F32) {
+          float* cp = reinterpret_cast<float*>(e.C) + off;
+          *reinterpret_cast<float4*>(cp) = make_float4(x[0], x[1], x[2], x[3]);
+          *reinterpret_cast<float4*>(cp + 4) = make_float4(x[4], x[5], x[6], x[7]);
+          if (fl & M3S_EPI_LN_STATS) {  // the next LayerNorm's input: bf16 copy + row stats
+            store_bf16x8(a.C2 + (int64_t)g * a.sC + off, x);
+            ln_group_stats(a, g, m, en, x);
+          }
+        } else if (fl & M3S_EPI_OUT_FP8) {
+          *reinterpret_cast<uint2*>(e.C + off) = make_uint2(pack4_fp8(x[0], x[1], x[2], x[3]),
+                                                            pack4_fp8(x[4], x[5], x[6], x[7]));
+        } else {
+          bf16x8 o;
+#pragma unroll
+          for (int t = 0; t < 8; t++) o[t] = f2bf(x[t]);
+          *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16_t*>(e.C) + off) = o;
+        }
+      }
+    }
+  } else if (!vec) {
+    const bool rope = fl & M3S_EPI_ROPE;
+    for (int v = 0; v < NV; v++) {
+      const int idx = v * NT + tid;
+      const int row = idx / VPR, c = (idx % VPR) * 8;
+      const int m = m0 + rb + row, n = n0 + c;
+      if (m >= a.M || n >= a.N) continue;
+      const float* src = cs + row * CST + c;
+      const float* psrc = cs + row * CST + (c ^ 16);
+      for (int t = 0; t < 8 && n + t < a.N; t++) epi_one(e, src[t], rope ? psrc[t] : 0.f, m, n + t);
+    }
+  }
+  }  // pass (the next pass's first barrier orders these LDS reads before its writes)
+  return true;
+}
+
+
+// 1-D grid over (batch x split) groups x tiles.  Workgroups are dispatched to the 8 XCDs
+// round-robin by linear id; the bijective remap gives each XCD a contiguous range of
+// remapped ids (cdna_hip_programming.md T1), so neighbouring tiles share its L2.  Within a
+// group the tile order is M-major (an XCD sweeps N for one A band: A reused) or N-major (an
+// XCD sweeps the M bands of a few weight columns: B reused), whichever the host estimated
+// to fetch fewer bytes, or grouped (runs of group_m M-bands swept column by column, so an
+// XCD's contiguous chunk of tiles is a compact group_m x (chunk / group_m) block: fewer
+// distinct A bands + B columns fetched into its L2 than one row or column of tiles).
+// Split-K keeps split-major ids: an XCD's contiguous chunk then holds ONE K-slice of a run
+// of tiles, whose A / B slices fit its 4 MB L2 (measured: putting a tile's slices on one
+// XCD instead — same-XCD slab reads for the reducer — fetched more from beyond L2 than it
+// saved, tools/gemm_split_probe.py).
+__device__ __forceinline__ void block_tile(const Args& a, int& zz, int& wgid, int& tm, int& tn) {
+  const int nwg = a.tiles_m * a.tiles_n;
+  const int total = gridDim.x;
+  const int orig = blockIdx.x;
+  int wid_lin = orig;
+  if (total >= 16) {
+    const int q = total / 8, r = total % 8, xcd = orig % 8;
+    wid_lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  zz = wid_lin / nwg;
+  wgid = wid_lin - zz * nwg;
+  if (a.group_m > 0) {
+    const int per_group = a.group_m * a.tiles_n;
+    const int grp = wgid / per_group;
+    const int first_m = grp * a.group_m;
+    const int gsz = min(a.tiles_m - first_m, a.group_m);
+    const int in = wgid - grp * per_group;
+    tm = first_m + in % gsz;
+    tn = in / gsz;
+  } else if (a.nmajor) {
+    tn = wgid / a.tiles_m;
+    tm = wgid - tn * a.tiles_m;
+  } else {
+    tm = wgid / a.tiles_n;
+    tn = wgid - tm * a.tiles_n;
+  }
+}
 
 // EPI >= 0: the epilogue flag set, fixed at compile time (straight-line epilogue code, and
 // the 8-wide vector path assumed); EPI < 0: flags read at run time.
@@ -418,45 +839,10 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
   constexpr bool DPT = EPI >= 0 && (EPI & M3S_EPI_DPT_OUT) != 0;
   __shared__ __attribute__((aligned(16))) char lds[C::LDS_BYTES + 16 + (DPT ? 640 * 4 : 0)];
 
-  // 1-D grid over (batch x split) groups x tiles.  Workgroups are dispatched to the 8
-  // XCDs round-robin by linear id; the bijective remap gives each XCD a contiguous range
-  // of remapped ids (cdna_hip_programming.md T1), so neighbouring tiles share its L2.
-  // Within a group the tile order is M-major (an XCD sweeps N for one A band: A reused)
-  // or N-major (an XCD sweeps the M bands of a few weight columns: B reused), whichever
-  // the host estimated to fetch fewer bytes.
+  // tile of this workgroup (block_tile: XCD-aware order)
   const int nwg = a.tiles_m * a.tiles_n;
-  const int total = gridDim.x;
-  const int orig = blockIdx.x;
-  int wid_lin = orig;
-  if (total >= 16) {
-    const int q = total / 8, r = total % 8, xcd = orig % 8;
-    wid_lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-  }
-  // split-K keeps split-major ids: an XCD's contiguous chunk then holds ONE K-slice of a
-  // run of tiles, whose A / B slices fit its 4 MB L2 (measured: putting a tile's slices on
-  // one XCD instead — same-XCD slab reads for the reducer — fetched more from beyond L2
-  // than it saved, tools/gemm_split_probe.py)
-  const int zz = wid_lin / nwg;
-  const int wgid = wid_lin - zz * nwg;
-  int tm, tn;
-  if (a.group_m > 0) {
-    // grouped order: runs of group_m M-bands swept column by column, so an XCD's
-    // contiguous chunk of tiles is a compact group_m x (chunk / group_m) block (fewer
-    // distinct A bands + B columns fetched into its L2 than one row or column of tiles)
-    const int per_group = a.group_m * a.tiles_n;
-    const int grp = wgid / per_group;
-    const int first_m = grp * a.group_m;
-    const int gsz = min(a.tiles_m - first_m, a.group_m);
-    const int in = wgid - grp * per_group;
-    tm = first_m + in % gsz;
-    tn = in / gsz;
-  } else if (a.nmajor) {
-    tn = wgid / a.tiles_m;
-    tm = wgid - tn * a.tiles_m;
-  } else {
-    tm = wgid / a.tiles_n;
-    tn = wgid - tm * a.tiles_n;
-  }
+  int zz, wgid, tm, tn;
+  block_tile(a, zz, wgid, tm, tn);
   const int g = SPLIT ? zz / a.splits : zz;
   const int split = SPLIT ? zz - g * a.splits : 0;
   const int m0 = tm * BM;
@@ -719,389 +1105,26 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
     }
   }
 
-  // ---- epilogue through LDS: f32 tile [BM][CST] ----
-  constexpr int VPR = BN / 8;                 // 8-column vectors per row
-  constexpr int PASSES = C::PASSES, EROWS = C::EROWS;
-  static_assert(PASSES == 1 || (!SPLIT && WM == PASSES), "two-pass epilogue: unsplit, one wave row per pass");
-  constexpr int NV = EROWS * VPR / NT;        // vectors per thread (per pass)
-  constexpr int RSTEP = NT / VPR;             // rows between one thread's vectors
-  static_assert(NT % VPR == 0, "epilogue layout");
-  // Vector path: a thread owns columns [n, n+8) of rows r0 + v*RSTEP.  Its bias and, per
-  // group of EG vectors, the residual (or RoPE cos/sin) operands are loaded ahead of use —
-  // the first group before the LDS round trip — so their latency is overlapped.
-  // EG must divide NV (96-row tiles have NV = 6: groups of 4 would run past the tile into
-  // the next tile's rows)
-  constexpr int EG = NV % 4 == 0 ? 4 : NV % 3 == 0 ? 3 : NV % 2 == 0 ? 2 : 1;
-  const int ec = (tid % VPR) * 8, er0 = tid / VPR;
-  const int en = n0 + ec;
-  const int fl = EPI >= 0 ? EPI : a.flags;
-  const bool vec = EPI >= 0 ? true : (a.vec != 0);
-  const bool vec_path = vec && en < a.N;
-  float e_b[8], e_pb[8], e_x[EG][16];
-  float e_c1[8], e_pc1[8], e_mu[EG], e_rs[EG];  // LN_FOLD: c1 columns, row mean / rstd
-  // LN_FOLD: the 16 lanes of a row group own rows er0 + v·RSTEP (v < NV ≤ 16); lane v
-  // combines the statistics of row v once, the others read it by lane shuffle
-  float ln_mu = 0.f, ln_rs = 0.f;
-  static_assert(NV <= 16, "one row per lane of the group");
-  int rb = 0;                                 // first tile row of the epilogue pass
-  auto ln_setup = [&]() {
-    if ((fl & M3S_EPI_LN_FOLD) && (lane & 15) < NV)
-      ln_row_stats(a, g ^ a.a_xor, min(m0 + rb + er0 + (lane & 15) * RSTEP, a.M - 1), a.K >> 7,
-                   ln_mu, ln_rs);
-  };
-  Epi e = make_epi(a, g);
-  e.flags = fl;
-  const bool e_rope = (fl & M3S_EPI_ROPE) && en < a.rope_cols;
-  auto e_prefetch = [&](int v0) {
+  // ---- epilogue through LDS: f32 tile [EROWS][CST] per pass (gemm_epilogue) ----
+  const bool stored = gemm_epilogue<BM, BN, NT, C::PASSES, C::LDS_BYTES, SPLIT, EPI>(
+      a, lds, g, zz, nwg, wgid, split, m0, n0, tl_end, [&](int pass, float* cs) {
+        const int rb = pass * C::EROWS;
 #pragma unroll
-    for (int u = 0; u < EG; u++) {
-      const int m = min(m0 + rb + er0 + (v0 + u) * RSTEP, a.M - 1);  // rows ≥ M are not stored
-      if (fl & M3S_EPI_LN_FOLD) {  // row v0 + u's statistics, held by lane v0 + u of the row group
-        const int src = (lane & ~15) | (v0 + u);
-        e_mu[u] = __shfl(ln_mu, src, 64);
-        e_rs[u] = __shfl(ln_rs, src, 64);
-      }
+        for (int i = 0; i < TM; i++)
 #pragma unroll
-      for (int t = 0; t < 16; t++) e_x[u][t] = 0.f;
-      if (fl & M3S_EPI_RES_F32) {
-        const float* r = reinterpret_cast<const float*>(e.R) + (int64_t)m * e.ldr + en;
-        *reinterpret_cast<float4*>(&e_x[u][0]) = *reinterpret_cast<const float4*>(r);
-        *reinterpret_cast<float4*>(&e_x[u][4]) = *reinterpret_cast<const float4*>(r + 4);
-      } else if (fl & M3S_EPI_RES_BF16) {
-        const bf16x8 r = *reinterpret_cast<const bf16x8*>(
-            reinterpret_cast<const bf16_t*>(e.R) + (int64_t)m * e.ldr + en);
+          for (int j = 0; j < TN; j++)
 #pragma unroll
-        for (int t = 0; t < 8; t++) e_x[u][t] = bf2f(r[t]);
-      } else if (e_rope) {  // RoPE GEMMs carry no residual: cos → [0, 8), sin → [8, 16)
-        const float* tb = e.rope_tab +
-                          ((int64_t)(m % e.rope_tokens) * 2 + ((en >> 5) & 1)) * 32 + (en & 15);
-        *reinterpret_cast<float4*>(&e_x[u][0]) = *reinterpret_cast<const float4*>(tb);
-        *reinterpret_cast<float4*>(&e_x[u][4]) = *reinterpret_cast<const float4*>(tb + 4);
-        *reinterpret_cast<float4*>(&e_x[u][8]) = *reinterpret_cast<const float4*>(tb + 16);
-        *reinterpret_cast<float4*>(&e_x[u][12]) = *reinterpret_cast<const float4*>(tb + 20);
-      }
-    }
-  };
-  auto epi_setup = [&](bool prefetch_rows) {
-    if (!vec_path) return;
-    int co;
-    (void)out_offset(e, m0, en, co);
-#pragma unroll
-    for (int t = 0; t < 8; t++) e_b[t] = e_pb[t] = 0.f;
-    if (e.bias) {
-      *reinterpret_cast<float4*>(&e_b[0]) = *reinterpret_cast<const float4*>(e.bias + co);
-      *reinterpret_cast<float4*>(&e_b[4]) = *reinterpret_cast<const float4*>(e.bias + co + 4);
-      if (e_rope) {
-        *reinterpret_cast<float4*>(&e_pb[0]) = *reinterpret_cast<const float4*>(e.bias + (en ^ 16));
-        *reinterpret_cast<float4*>(&e_pb[4]) =
-            *reinterpret_cast<const float4*>(e.bias + (en ^ 16) + 4);
-      }
-    }
-    if (fl & M3S_EPI_LN_FOLD) {
-      const float* c1 = a.ln_c1 + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sBias;
-      *reinterpret_cast<float4*>(&e_c1[0]) = *reinterpret_cast<const float4*>(c1 + en);
-      *reinterpret_cast<float4*>(&e_c1[4]) = *reinterpret_cast<const float4*>(c1 + en + 4);
-      if (e_rope) {
-        *reinterpret_cast<float4*>(&e_pc1[0]) = *reinterpret_cast<const float4*>(c1 + (en ^ 16));
-        *reinterpret_cast<float4*>(&e_pc1[4]) =
-            *reinterpret_cast<const float4*>(c1 + (en ^ 16) + 4);
-      }
-    }
-    if (prefetch_rows) e_prefetch(0);
-  };
-  if (!SPLIT) epi_setup(false);   // split-K: only the tile's last split needs the operands
-  float* cs = reinterpret_cast<float*>(lds);
-  // DPT tail operands: w4 [4][128] then the conv bias [128] (zeros without BIAS), requested
-  // now and written beside the tile after the K-loop's last LDS reads
-  float4 dpt_stage = make_float4(0.f, 0.f, 0.f, 0.f);
-  if constexpr (DPT) {
-    const int gw = a.wmod > 0 ? g % a.wmod : g;
-    if (tid < 128)
-      dpt_stage = reinterpret_cast<const float4*>(a.dpt_w4 + (int64_t)gw * 512)[tid];
-    else if (tid < 160 && (EPI & M3S_EPI_BIAS))
-      dpt_stage = reinterpret_cast<const float4*>(a.bias + (int64_t)gw * a.sBias)[tid - 128];
-  }
-#pragma unroll
-  for (int pass = 0; pass < PASSES; pass++) {
-  rb = pass * EROWS;
-  if (!SPLIT) {
-    ln_setup();
-    if (vec_path) e_prefetch(0);
-  }
-  M3S_T(t_e0);
-  block_sync_lds();
-  M3S_T(t_e1);
-#pragma unroll
-  for (int i = 0; i < TM; i++)
-#pragma unroll
-    for (int j = 0; j < TN; j++)
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh - rb;
-        if (PASSES == 1 || wm == pass)
-          cs[row * C::CST + wn * (BN / WN) + j * 32 + fr] = acc[i][j][r];
-      }
-  if constexpr (DPT) {
-    if (tid < 160)
-      reinterpret_cast<float4*>(lds + C::LDS_BYTES + 16)[tid] = dpt_stage;
-  }
-  block_sync_lds();
-  M3S_T(t_e2);
-  tl_end.mark(3);
-
-  if constexpr (DPT) {
-    // fused DPT tail, all BN = 128 channels of a pixel (row) in the LDS tile: TPR threads
-    // per row (every thread of the block busy: 2-4 per row) each take 32 / TPR of the
-    // row's 4-channel groups — group q = (k % G) + G·h + 16·(k / G), G = 16 / TPR, so the
-    // 16 lanes of one ds_read_b128 hit 16 different bank quads — against the 1x1 weights
-    // and bias staged in LDS (broadcast reads), then the TPR partial sums meet by lane
-    // shuffle.  (One row per thread with the weights read from global memory took 8.8 us
-    // of a 27 us head.2 block in the C3 step: the block log, round 5.)
-    static_assert(BN == 128 && !SPLIT && PASSES == 1,
-                  "DPT_OUT needs the full 128-channel row in one tile");
-    constexpr int TPR = NT >= BM ? NT / BM : 1;
-    static_assert(TPR == 1 || TPR == 2 || TPR == 4 || TPR == 8, "threads per row");
-    constexpr int G = 16 / (TPR > 16 ? 16 : TPR);
-    const int gw = a.wmod > 0 ? g % a.wmod : g;
-    const float* b4 = a.dpt_b4 + (int64_t)gw * 4;
-    const float b40 = b4[0], b41 = b4[1], b42 = b4[2], b43 = b4[3];
-    const float* wl = reinterpret_cast<const float*>(lds + C::LDS_BYTES + 16);
-    const float* bl = wl + 512;
-    const int h = tid % TPR;
-    for (int row = tid / TPR; row < BM; row += NT / TPR) {
-      const int m = m0 + row;
-      float o4[4] = {0.f, 0.f, 0.f, 0.f};
-      const float* src = cs + row * C::CST;
-#pragma unroll 8
-      for (int k = 0; k < 32 / TPR; k++) {
-        const int c = 4 * ((k % G) + G * h + 16 * (k / G));
-        float4 x = *reinterpret_cast<const float4*>(src + c);
-        if constexpr ((EPI & M3S_EPI_BIAS) != 0) {
-          const float4 bb = *reinterpret_cast<const float4*>(bl + c);
-          x.x += bb.x;
-          x.y += bb.y;
-          x.z += bb.z;
-          x.w += bb.w;
-        }
-        x.x = fmaxf(x.x, 0.f);
-        x.y = fmaxf(x.y, 0.f);
-        x.z = fmaxf(x.z, 0.f);
-        x.w = fmaxf(x.w, 0.f);
-#pragma unroll
-        for (int oo = 0; oo < 4; oo++) {
-          const float4 w = *reinterpret_cast<const float4*>(wl + oo * 128 + c);
-          o4[oo] += w.x * x.x + w.y * x.y + w.z * x.z + w.w * x.w;
-        }
-      }
-#pragma unroll
-      for (int off = 1; off < TPR; off <<= 1)
-#pragma unroll
-        for (int oo = 0; oo < 4; oo++) o4[oo] += __shfl_xor(o4[oo], off, 64);
-      if (h == 0 && m < a.M) {
-        o4[0] += b40;
-        o4[1] += b41;
-        o4[2] += b42;
-        o4[3] += b43;
-        // reg_dense_depth('exp') + conf ('exp', conf_min): as dpt_out_kernel (vit_misc.hip)
-        const float d = sqrtf(o4[0] * o4[0] + o4[1] * o4[1] + o4[2] * o4[2]);
-        const float sc = expm1f(d) / fmaxf(d, 1e-8f);
-        float* P = a.dpt_pts + ((int64_t)g * a.M + m) * 3;
-        P[0] = o4[0] * sc;
-        P[1] = o4[1] * sc;
-        P[2] = o4[2] * sc;
-        a.dpt_conf[(int64_t)g * a.M + m] = a.dpt_conf_min + expf(o4[3]);
-      }
-    }
-    return;
-  }
-
-  if constexpr (SPLIT) {
-    // publish this split's partial tile; the tile's last split sums them all
-    int& s_last = *reinterpret_cast<int*>(lds + C::LDS_BYTES);
-    const int64_t per_b = (int64_t)a.M * a.N;
-    float* P = a.ws + (int64_t)zz * per_b;
-#pragma unroll 4
-    for (int v = 0; v < NV; v++) {
-      const int idx = v * NT + tid;
-      const int row = idx / VPR, c = (idx % VPR) * 8;
-      const int m = m0 + row, n = n0 + c;
-      if (m >= a.M || n >= a.N) continue;
-      const float* src = cs + row * C::CST + c;
-      float* dst = P + (int64_t)m * a.N + n;
-      if (vec) {
-        *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
-        *reinterpret_cast<float4*>(dst + 4) = *reinterpret_cast<const float4*>(src + 4);
-      } else {
-        for (int t = 0; t < 8 && n + t < a.N; t++) dst[t] = src[t];
-      }
-    }
-    if (!a.fused) {  // splitk_reduce_kernel follows
-      M3S_STAMP_EARLY();
-      return;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      // the fence's own wait can be dropped by the compiler: wait here, before the ticket
-      // (cdna_hip_programming.md Guideline 16, Pitfall 12)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      int* ctr = a.cnt + (int64_t)g * nwg + wgid;
-      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = old == a.splits - 1;
-      if (s_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!s_last) {
-      M3S_STAMP_EARLY();
-      return;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    ln_setup();
-    epi_setup(true);
-    const float* P0 = a.ws + (int64_t)g * a.splits * per_b;
-    // slab by slab, all of this thread's vectors of a slab in flight at once (one L2
-    // round trip per slab instead of one per vector); the sum stays in split order
-    float xs[NV][8];
-#pragma unroll
-    for (int v = 0; v < NV; v++)
-#pragma unroll
-      for (int t = 0; t < 8; t++) xs[v][t] = 0.f;
-    for (int k = 0; k < a.splits; k++) {
-      float ys[NV][8];
-#pragma unroll
-      for (int v = 0; v < NV; v++) {
-        const int idx = v * NT + tid;
-        const int row = idx / VPR, c = (idx % VPR) * 8;
-        const int m = m0 + row, n = n0 + c;
-        const float* src = cs + row * C::CST + c;
-        if (k == split) {  // this workgroup's own partial is still in LDS
-          *reinterpret_cast<float4*>(&ys[v][0]) = *reinterpret_cast<const float4*>(src);
-          *reinterpret_cast<float4*>(&ys[v][4]) = *reinterpret_cast<const float4*>(src + 4);
-        } else if (m < a.M && vec && n < a.N) {
-          const float* q = P0 + k * per_b + (int64_t)m * a.N + n;
-          *reinterpret_cast<float4*>(&ys[v][0]) = *reinterpret_cast<const float4*>(q);
-          *reinterpret_cast<float4*>(&ys[v][4]) = *reinterpret_cast<const float4*>(q + 4);
-        } else {
-          const float* q = P0 + k * per_b + (int64_t)m * a.N + n;
-#pragma unroll
-          for (int t = 0; t < 8; t++) ys[v][t] = (m < a.M && n + t < a.N) ? q[t] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int v = 0; v < NV; v++)
-#pragma unroll
-        for (int t = 0; t < 8; t++) xs[v][t] += ys[v][t];
-    }
-    block_sync_lds();  // every own-slab LDS read above is done before the overwrite
-#pragma unroll
-    for (int v = 0; v < NV; v++) {
-      const int idx = v * NT + tid;
-      const int row = idx / VPR, c = (idx % VPR) * 8;
-      float* dst = cs + row * C::CST + c;
-      *reinterpret_cast<float4*>(dst) = make_float4(xs[v][0], xs[v][1], xs[v][2], xs[v][3]);
-      *reinterpret_cast<float4*>(dst + 4) = make_float4(xs[v][4], xs[v][5], xs[v][6], xs[v][7]);
-    }
-    block_sync_lds();
-  }
-  if (vec_path) {
-    const float sg = (en & 16) ? 1.f : -1.f;
-    const bool has_res = fl & (M3S_EPI_RES_F32 | M3S_EPI_RES_BF16);
-    const bool rope_now = e_rope && !has_res;
-    // per group: all LDS reads first, then the math and the global stores (a ds_read issued
-    // after a global store waits for that store: the compiler cannot prove it does not
-    // alias the LDS-DMA ring — one such wait per group instead of one per vector)
-#pragma unroll
-    for (int v0 = 0; v0 < NV; v0 += EG) {
-      if (v0 > 0) e_prefetch(v0);
-      float xv[EG][8], pv[EG][8];
-#pragma unroll
-      for (int u = 0; u < EG; u++) {
-        const int row = er0 + (v0 + u) * RSTEP;
-        const float* src = cs + row * C::CST + ec;
-        *reinterpret_cast<float4*>(&xv[u][0]) = *reinterpret_cast<const float4*>(src);
-        *reinterpret_cast<float4*>(&xv[u][4]) = *reinterpret_cast<const float4*>(src + 4);
-        if (rope_now) {
-          const float* psrc = cs + row * C::CST + (ec ^ 16);
-          *reinterpret_cast<float4*>(&pv[u][0]) = *reinterpret_cast<const float4*>(psrc);
-          *reinterpret_cast<float4*>(&pv[u][4]) = *reinterpret_cast<const float4*>(psrc + 4);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < EG; u++) {
-        const int m = m0 + rb + er0 + (v0 + u) * RSTEP;
-        if (m >= a.M) continue;
-        float* x = xv[u];
-        if (fl & M3S_EPI_LN_FOLD) {  // LN(x) W^T + b = rstd (acc - mean c1) + c2
-#pragma unroll
-          for (int t = 0; t < 8; t++) x[t] = fmaf(e_rs[u], fmaf(-e_mu[u], e_c1[t], x[t]), e_b[t]);
-          if (rope_now) {  // the partner columns' final values
-#pragma unroll
-            for (int t = 0; t < 8; t++)
-              pv[u][t] = fmaf(e_rs[u], fmaf(-e_mu[u], e_pc1[t], pv[u][t]), e_pb[t]);
-          }
-        } else {
-#pragma unroll
-          for (int t = 0; t < 8; t++) x[t] += e_b[t];
-          if (rope_now) {
-#pragma unroll
-            for (int t = 0; t < 8; t++) pv[u][t] += e_pb[t];
-          }
-        }
-        if (fl & M3S_EPI_GELU) {
-#pragma unroll
-          for (int t = 0; t < 8; t++) x[t] = gelu_erf(x[t]);
-        }
-        if (rope_now) {
-#pragma unroll
-          for (int t = 0; t < 8; t++)
-            x[t] = x[t] * e_x[u][t] + sg * pv[u][t] * e_x[u][8 + t];
-        }
-        if (has_res) {
-#pragma unroll
-          for (int t = 0; t < 8; t++) x[t] += e_x[u][t];
-        }
-        if (fl & M3S_EPI_RELU) {
-#pragma unroll
-          for (int t = 0; t < 8; t++) x[t] = fmaxf(x[t], 0.f);
-        }
-        int co;
-        const int64_t off = out_offset(e, m, en, co);
-        if (fl & M3S_EPI_OUT_F32) {
-          float* cp = reinterpret_cast<float*>(e.C) + off;
-          *reinterpret_cast<float4*>(cp) = make_float4(x[0], x[1], x[2], x[3]);
-          *reinterpret_cast<float4*>(cp + 4) = make_float4(x[4], x[5], x[6], x[7]);
-          if (fl & M3S_EPI_LN_STATS) {  // the next LayerNorm's input: bf16 copy + row stats
-            store_bf16x8(a.C2 + (int64_t)g * a.sC + off, x);
-            ln_group_stats(a, g, m, en, x);
-          }
-        } else if (fl & M3S_EPI_OUT_FP8) {
-          *reinterpret_cast<uint2*>(e.C + off) = make_uint2(pack4_fp8(x[0], x[1], x[2], x[3]),
-                                                            pack4_fp8(x[4], x[5], x[6], x[7]));
-        } else {
-          bf16x8 o;
-#pragma unroll
-          for (int t = 0; t < 8; t++) o[t] = f2bf(x[t]);
-          *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16_t*>(e.C) + off) = o;
-        }
-      }
-    }
-  } else if (!vec) {
-    const bool rope = fl & M3S_EPI_ROPE;
-    for (int v = 0; v < NV; v++) {
-      const int idx = v * NT + tid;
-      const int row = idx / VPR, c = (idx % VPR) * 8;
-      const int m = m0 + rb + row, n = n0 + c;
-      if (m >= a.M || n >= a.N) continue;
-      const float* src = cs + row * C::CST + c;
-      const float* psrc = cs + row * C::CST + (c ^ 16);
-      for (int t = 0; t < 8 && n + t < a.N; t++) epi_one(e, src[t], rope ? psrc[t] : 0.f, m, n + t);
-    }
-  }
-  if (pass + 1 == PASSES) {
+            for (int r = 0; r < 16; r++) {
+              const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh - rb;
+              if (C::PASSES == 1 || wm == pass)
+                cs[row * C::CST + wn * (BN / WN) + j * 32 + fr] = acc[i][j][r];
+            }
+      });
+  if (stored) {
     M3S_STAMP_OUT();
+  } else {
+    M3S_STAMP_EARLY();
   }
-  }  // pass (the next pass's first barrier orders these LDS reads before its writes)
 }
 
 // Unfused split-K: sum the partials (fixed order) and apply the epilogue; 8 columns per
@@ -1153,6 +1176,307 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
   }
 }
 
+// Tile order of a launch (block_tile): the operand bytes an XCD's L2 must fetch for its
+// contiguous chunk of T tiles — M-major touches ceil(T / tiles_n) A bands and min(T,
+// tiles_n) B columns, N-major ceil(T / tiles_m) B columns and min(T, tiles_m) A bands, a
+// grouped order G bands x ceil(T / G) columns; the cheapest line order, or the grouped one
+// if ≥ 10 % below it.  Implicit convs keep M-major.
+inline void set_order(Args& a, int BM, int BN, int64_t groups) {
+  a.nmajor = 0;
+  a.group_m = 0;
+  if (a.mode != 0) return;
+  const int64_t T = ((int64_t)a.tiles_m * a.tiles_n * groups + 7) / 8;
+  const double band = (double)BM * a.K * 2, col = (double)BN * a.K * 2;
+  const double costM = band * std::min<int64_t>(a.tiles_m, (T + a.tiles_n - 1) / a.tiles_n + 1) +
+                       col * std::min<int64_t>(T, a.tiles_n);
+  const double costN = col * std::min<int64_t>(a.tiles_n, (T + a.tiles_m - 1) / a.tiles_m + 1) +
+                       band * std::min<int64_t>(T, a.tiles_m);
+  a.nmajor = costN < costM;
+  double best = std::min(costM, costN);
+  for (int G = 2; G < a.tiles_m && G <= 16; G++) {
+    if (T > (int64_t)G * a.tiles_n) break;
+    const double c = band * G + col * (double)((T + G - 1) / G);
+    if (c < 0.9 * best) {
+      best = c;
+      a.group_m = G;
+    }
+  }
+  if (const char* e = getenv("M3S_GEMM_ORDER")) {  // tuning override: 0 / 1 / -G
+    const int v = atoi(e);
+    a.nmajor = v == 1;
+    a.group_m = v < 0 ? -v : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// T256PP: 256x256 tiles, 8 waves in two ping-pong groups (round 6)
+// ---------------------------------------------------------------------------------------
+// cdna_hip_programming.md §5's 256² 8-phase structure, derived for this library's operand
+// layout (tools/gemm_pp_dev.hip is the isolated main loop; 4096³: 1.51 PF/s vs 1.36 for
+// hipBLASLt on the same box, profiles/r06_gemm_pp_dev.txt):
+//  * LDS: 2 K-tile buffers x 4 half-tile slots {A rows 0-127, A rows 128-255, B cols 0-127,
+//    B cols 128-255} of 128 x 64 bf16 (16 KB), filled by LDS-DMA with the chunk swizzle of
+//    gemm_kernel (chunk ^ ((row >> 1) & 7)).
+//  * A K-tile is 4 phases; phase p computes block quadrant (QM, QN) = (0,0), (0,1), (1,1),
+//    (1,0) over K = 64: each wave its 64 x 32 share (16 v_mfma_f32_16x16x32_bf16 — the
+//    16x16 shape holds a higher clock than 32x32x16 under load, MI355X_MICROARCH.md 'DVFS
+//    give-back' 7).  Fragments are read only where the quadrant changes them (A0+B0, B1,
+//    A1, B0: 28 ds_read_b128 per wave per K-tile) into one register set.
+//  * Phase p also issues half-tile p of K-tile t+1 (A0, B0, B1, A1) into the other buffer
+//    and waits vmcnt(4) (the half-tile issued two phases earlier is retired).  Phases are
+//    [reads, DMA, wait] barrier [16 MFMAs] barrier; waves 4-7 run one barrier behind waves
+//    0-3, so on each SIMD one wave's MFMA segment runs beside its partner's read / DMA
+//    segment, and the younger group holds s_setprio 1 (§5.5 T5 static form).
+//  * Ordering (phase index P = 4t + p; group 0 reads phase P before global barrier 2P, group
+//    1 before 2P + 1): a half-tile issued at phase I may be read at phase Q ≥ I + 3 (both
+//    groups' covering waits precede a barrier the reader has passed) and a slot read last
+//    at phase Q may be refilled at I ≥ Q + 2 (every read of phase Q has completed before
+//    barrier 2Q + 2).  The order above meets both with one slack phase: (t+1, A0) issued
+//    at 4t reads 4t+4, last read of (t-1, A0) 4t-4; B0 4t+1 / 4t+4, 4t-1; B1 4t+2 / 4t+5,
+//    4t-3; A1 4t+3 / 4t+6, 4t-2.
+//  * The last K-tile issues nothing (its phases wait vmcnt(2), then 0).
+// Implicit conv (MODE 1 / 2) as gemm_kernel: the tap and channel offset are block-uniform
+// per K-tile (Cin % 64 == 0), ReLU (MODE 2) on the A fragments.  Unsplit; the epilogue is
+// gemm_epilogue's, in two 128-row passes (QM = 0, then 1).
+template <int MODE, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(Args a) {
+  constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+  constexpr int HB = 128 * BK * 2;       // half-tile bytes
+  constexpr int BUFB = 4 * HB;           // one K-tile
+  constexpr int RING = 2 * BUFB;
+  constexpr int EPIB = 128 * (BN + 4) * 4;
+  constexpr int LDS_BYTES = EPIB > RING ? EPIB : RING;
+  static_assert(EPI < 0 || (EPI & (M3S_EPI_DPT_OUT | M3S_EPI_OUT_FP8)) == 0, "not on T256PP");
+  m3s_tl_begin(a.tl);
+  M3sTlEnd tl_end{a.tl};
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES + 16];
+  const int nwg = a.tiles_m * a.tiles_n;
+  int zz, wgid, tm, tn;
+  block_tile(a, zz, wgid, tm, tn);
+  const int g = zz;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;   // ping-pong group, column of the quadrant
+
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(a.A + (int64_t)(g ^ a.a_xor) * a.sA), (short)0, NUM_RECORDS, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(a.B + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sB), (short)0,
+      NUM_RECORDS, 0x00020000);
+
+  // DMA: a half-tile is 128 rows x 8 chunks of 16 B; thread chunk q = i*512 + tid lands at
+  // row q >> 3, slot q & 7 and carries logical chunk slot ^ ((row >> 1) & 7).  off[h][i]:
+  // byte offset of row (h & 1)·128 + (q >> 3) of slot h (A0 A1 B0 B1) at k = 0 (GEMM rows;
+  // conv rows keep their input pixel instead)
+  uint32_t off[4][2];
+  int kc[2], a_iy[2][2], a_ix[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int q = i * NT + tid;
+    const int r = q >> 3, p = q & 7;
+    kc[i] = (p ^ ((r >> 1) & 7)) * 8;
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+      const int row = (h & 1) * 128 + r;
+      if (h < 2) {
+        const int m = m0 + row;
+        if (MODE == 0) {
+          off[h][i] = m < a.M ? (uint32_t)(((int64_t)m * a.lda + kc[i]) * 2) : OOB;
+        } else {
+          const int oy = m / a.Wout, ox = m - oy * a.Wout;
+          a_iy[h][i] = m < a.M ? oy * a.stride - 1 : -(1 << 20);
+          a_ix[h][i] = ox * a.stride - 1;
+          off[h][i] = 0;
+        }
+      } else {
+        const int n = n0 + row;
+        off[h][i] = n < a.N ? (uint32_t)(((int64_t)n * a.ldb + kc[i]) * 2) : OOB;
+      }
+    }
+  }
+  const int nk = (a.K + BK - 1) / BK;
+  // half-tile h of K-tile t into its slot of buffer t & 1
+  auto issue = [&](int t, int h) {
+    char* dst = lds + (t & 1) * BUFB + h * HB + wid * 64 * 16;
+    const int k0 = t * BK;
+    int ky = 0, kx = 0, ci0 = 0;
+    if (MODE != 0 && h < 2) {
+      const int tap = k0 / a.Cin;
+      ci0 = k0 - tap * a.Cin;
+      ky = tap / 3;
+      kx = tap - ky * 3;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      uint32_t vo;
+      if (MODE != 0 && h < 2) {
+        const int iy = a_iy[h][i] + ky, ix = a_ix[h][i] + kx;
+        const bool ok = (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+        vo = ok ? (uint32_t)((((int64_t)iy * a.Win + ix) * a.Cin + ci0 + kc[i]) * 2) : OOB;
+      } else {
+        vo = (k0 + kc[i] < a.K) ? off[h][i] + (uint32_t)k0 * 2 : OOB;
+      }
+      glds16(h < 2 ? rA : rB, dst + i * NT * 16, vo);
+    }
+  };
+
+  // fragments: lane reads row (lane & 15) of a 16-row tile, chunk 4s + (lane >> 4),
+  // swizzled by ((row >> 1) & 7) = (lane & 15) >> 1 (tile bases are multiples of 16 rows)
+  const int fr = lane & 15, fc = lane >> 4, sw = fr >> 1;
+  const int lo0 = fr * 128 + ((fc ^ sw) << 4);
+  const int lo1 = fr * 128 + (((fc ^ sw) ^ 4) << 4);
+  bf16x8 af[4][2], bfr[2][2];
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int x = 0; x < 2; x++)
+#pragma unroll
+    for (int y = 0; y < 2; y++)
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto read_a = [&](const char* slot) {
+    const char* base = slot + wr * 64 * 128;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      af[i][0] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + lo0);
+      af[i][1] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + lo1);
+      if (MODE == 2) {
+        af[i][0] = relu_frag(af[i][0]);
+        af[i][1] = relu_frag(af[i][1]);
+      }
+    }
+  };
+  auto read_b = [&](const char* slot) {
+    const char* base = slot + wc * 32 * 128;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      bfr[j][0] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + lo0);
+      bfr[j][1] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + lo1);
+    }
+  };
+  auto mfmas = [&](f32x4 (&c)[4][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; s++)
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], c[i][j], 0, 0, 0);
+  };
+  auto bar = []() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: K-tile 0 into buffer 0; A0 and B0 retired before the first reads
+  if (nk > 0) {
+    issue(0, 0);
+    issue(0, 2);
+    issue(0, 3);
+    issue(0, 1);
+  }
+  tl_end.mark(0);
+  vm_wait<4>();
+  bar();
+  if (wr == 1) {
+    bar();                          // the stagger
+    __builtin_amdgcn_s_setprio(1);  // the younger group wins VALU / LDS arbitration
+  }
+  tl_end.mark(1);
+#define M3S_PP_PHASE(READS, ISSUE, WAIT, QM, QN) \
+  READS;                                         \
+  ISSUE;                                         \
+  vm_wait<WAIT>();                               \
+  bar();                                         \
+  mfmas(acc[QM][QN]);                            \
+  bar();
+  int t = 0;
+  for (; t < nk - 1; t++) {
+    const char* cur = lds + (t & 1) * BUFB;
+    M3S_PP_PHASE((read_a(cur), read_b(cur + 2 * HB)), issue(t + 1, 0), 4, 0, 0)
+    M3S_PP_PHASE(read_b(cur + 3 * HB), issue(t + 1, 2), 4, 0, 1)
+    M3S_PP_PHASE(read_a(cur + HB), issue(t + 1, 3), 4, 1, 1)
+    M3S_PP_PHASE(read_b(cur + 2 * HB), issue(t + 1, 1), 4, 1, 0)
+  }
+  if (nk > 0) {   // the last K-tile: nothing to issue (phase 0 retires B1, phase 1 A1)
+    const char* cur = lds + (t & 1) * BUFB;
+    M3S_PP_PHASE((read_a(cur), read_b(cur + 2 * HB)), (void)0, 2, 0, 0)
+    M3S_PP_PHASE(read_b(cur + 3 * HB), (void)0, 0, 0, 1)
+    M3S_PP_PHASE(read_a(cur + HB), (void)0, 0, 1, 1)
+    M3S_PP_PHASE(read_b(cur + 2 * HB), (void)0, 0, 1, 0)
+  }
+#undef M3S_PP_PHASE
+  if (wr == 1) __builtin_amdgcn_s_setprio(0);
+  else bar();                       // re-align the groups
+  vm_wait<0>();
+  tl_end.mark(2);
+  (void)gemm_epilogue<BM, BN, NT, 2, LDS_BYTES, false, EPI>(
+      a, lds, g, zz, nwg, wgid, 0, m0, n0, tl_end, [&](int pass, float* cs) {
+#pragma unroll
+        for (int qn = 0; qn < 2; qn++)
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++)
+#pragma unroll
+              for (int r = 0; r < 4; r++) {
+                const int row = wr * 64 + i * 16 + fc * 4 + r;
+                const int col = qn * 128 + wc * 32 + j * 16 + fr;
+                cs[row * (BN + 4) + col] = pass == 0 ? acc[0][qn][i][j][r] : acc[1][qn][i][j][r];
+              }
+      });
+}
+
+template <int MODE, int E>
+bool try_epi_pp(Args& a, dim3 grid, hipStream_t s, int key, bool biased_only = false) {
+  if (key == E && !biased_only) {
+    hipLaunchKernelGGL((gemm_pp_kernel<MODE, E>), grid, dim3(512), 0, s, a);
+    return true;
+  }
+  if (key == (E | M3S_EPI_BIAS)) {
+    hipLaunchKernelGGL((gemm_pp_kernel<MODE, E | M3S_EPI_BIAS>), grid, dim3(512), 0, s, a);
+    return true;
+  }
+  return false;
+}
+
+// T256PP launcher (unsplit): the epilogue sets of launch_main as straight-line variants,
+// the run-time-flag epilogue otherwise
+template <int MODE>
+int launch_pp(Args& a, int batch, hipStream_t s) {
+  a.tiles_m = (a.M + 255) / 256;
+  a.tiles_n = (a.N + 255) / 256;
+  if ((int64_t)a.tiles_m * a.tiles_n * batch >= (1ll << 31)) return M3S_ERR_TOO_LARGE;
+  const dim3 grid((unsigned)(a.tiles_m * a.tiles_n * batch));
+  a.splits = 1;
+  set_order(a, 256, 256, batch);
+  const int key = (a.flags & ~(M3S_PRO_RELU | (a.bias ? 0 : M3S_EPI_BIAS)));
+  bool done = false;
+  if (a.vec) {
+    if constexpr (MODE == 0) {
+      constexpr int LF = M3S_EPI_LN_FOLD, LS = M3S_EPI_LN_STATS;
+      done = try_epi_pp<0, 0>(a, grid, s, key) || try_epi_pp<0, M3S_EPI_ROPE>(a, grid, s, key) ||
+             try_epi_pp<0, M3S_EPI_GELU>(a, grid, s, key) ||
+             try_epi_pp<0, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32>(a, grid, s, key) ||
+             try_epi_pp<0, M3S_EPI_OUT_F32>(a, grid, s, key) ||
+             try_epi_pp<0, LF | M3S_EPI_ROPE>(a, grid, s, key, true) ||
+             try_epi_pp<0, LF | M3S_EPI_GELU>(a, grid, s, key, true) ||
+             try_epi_pp<0, LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32>(a, grid, s, key, true) ||
+             try_epi_pp<0, LS | M3S_EPI_OUT_F32>(a, grid, s, key, true);
+    } else {
+      done = try_epi_pp<MODE, 0>(a, grid, s, key) ||
+             try_epi_pp<MODE, M3S_EPI_RES_BF16>(a, grid, s, key) ||
+             try_epi_pp<MODE, M3S_EPI_RELU>(a, grid, s, key);
+    }
+  }
+  if (!done) hipLaunchKernelGGL((gemm_pp_kernel<MODE, -1>), grid, dim3(512), 0, s, a);
+  M3S_LAUNCH_CHECK();
+  return M3S_OK;
+}
+
 // ---------------------------------------------------------------------------------------
 // tile configurations
 // ---------------------------------------------------------------------------------------
@@ -1175,8 +1499,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
 // cycles ≈ 0.5, the shape of cdna_hip_programming.md §5's 256² template — the most MFMA
 // work per staged byte, for launches that can spend fewer CUs (large-M convs, the local-
 // feature MLP, GEMMs sharing the chip with other chains)
+// T256PP: 256x256, the 8-wave ping-pong kernel above (round 6)
 enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7, T96 = 8, T96O2 = 9,
-               T64D = 10, T128D = 11, T128W8 = 12, T256W8 = 13, T256SQ = 14 };
+               T64D = 10, T128D = 11, T128W8 = 12, T256W8 = 13, T256SQ = 14, T256PP = 15 };
 
 // Epilogue flag sets compiled as straight-line variants (8-wide vector path), per mode:
 //   GEMM: bf16 out, +RoPE, +GELU, f32 residual → f32, f32 out;  conv: bf16 out, +bf16
@@ -1299,37 +1624,7 @@ int launch(Args& a, int batch, hipStream_t s) {
   const int64_t groups = (int64_t)batch * (split ? a.splits : 1);
   if ((int64_t)a.tiles_m * a.tiles_n * groups >= (1ll << 31)) return M3S_ERR_TOO_LARGE;
   dim3 grid((unsigned)(a.tiles_m * a.tiles_n * groups));
-  // tile order: the operand bytes an XCD's L2 must fetch for its contiguous chunk of T
-  // tiles — M-major touches ceil(T / tiles_n) A bands and min(T, tiles_n) B columns,
-  // N-major ceil(T / tiles_m) B columns and min(T, tiles_m) A bands; take the smaller
-  if (a.mode == 0) {
-    const int64_t T = ((int64_t)a.tiles_m * a.tiles_n * groups + 7) / 8;
-    const double band = (double)BM * a.K * 2, col = (double)BN * a.K * 2;
-    const double costM = band * std::min<int64_t>(a.tiles_m, (T + a.tiles_n - 1) / a.tiles_n + 1) +
-                         col * std::min<int64_t>(T, a.tiles_n);
-    const double costN = col * std::min<int64_t>(a.tiles_n, (T + a.tiles_m - 1) / a.tiles_m + 1) +
-                         band * std::min<int64_t>(T, a.tiles_m);
-    a.nmajor = costN < costM;
-    // grouped order: a chunk of T tiles as G bands x ceil(T / G) columns
-    double best = std::min(costM, costN);
-    a.group_m = 0;
-    for (int G = 2; G < a.tiles_m && G <= 16; G++) {
-      if (T > (int64_t)G * a.tiles_n) break;
-      const double c = band * G + col * (double)((T + G - 1) / G);
-      if (c < 0.9 * best) {
-        best = c;
-        a.group_m = G;
-      }
-    }
-    if (const char* e = getenv("M3S_GEMM_ORDER")) {  // tuning override: 0 / 1 / -G
-      const int v = atoi(e);
-      a.nmajor = v == 1;
-      a.group_m = v < 0 ? -v : 0;
-    }
-  } else {
-    a.nmajor = 0;
-    a.group_m = 0;
-  }
+  set_order(a, BM, BN, groups);
   if (split) {
     // split-K (fused last-split epilogue): 128^2 GEMM tiles, 64x128 GEMM / conv tiles
     constexpr bool CAN = !F8 && ((BM == 128 && BN == 128 && BK == 64) ||

@@ -267,6 +267,17 @@ HEAD_FP8 = ("head0", "head2")
 FP8_ACT_HEADROOM = 2.0   # calibrated amax maps to 448 / 2: test frames may run hotter
 
 
+def _assign_params(old, new):
+    """`new` written into the tensors of dict `old` when every key, shape and dtype match
+    (the tensors a captured graph reads stay the same), else `new` itself."""
+    if (old.keys() != new.keys() or
+            any(old[k].shape != new[k].shape or old[k].dtype != new[k].dtype for k in new)):
+        return new
+    for k in new:
+        old[k].copy_(new[k])
+    return old
+
+
 def _fp8_shifted_params(W, cal):
     """Calibrated fp8 parameter copies (PairModel.calibrate_fp8): cal[(site, layer)] = the
     per-channel mean of that e4m3 operand ([C] for the encoder, [Z, C] per decoder problem;
@@ -570,8 +581,13 @@ class PairModel:
         0.99936 (mono 512x512).  images: calibration frames [n >= 2, 3, H, W] in [-1, 1]
         (frames of the target domain with real checkpoints) instead of the noise frames."""
         W, dev = self.w, self.dev
-        was = self.fp8
+        was, was_convs = self.fp8, self.fp8_convs
+        old = (W.fp8_shift_enc, W.fp8_shift_dec)
+        bufs_before = set(self._bufs)
         self.fp8 = True
+        # the heads run their bf16 convs while calibrating: the amax of an e4m3 upsample
+        # output would be its largest byte code, not its largest activation (ADVICE r5)
+        self.fp8_convs = False
         W.fp8_shift_enc, W.fp8_shift_dec = {}, [{} for _ in W.dec]   # plain biases first
         self._cal = {}
         try:
@@ -588,19 +604,39 @@ class PairModel:
             f = feat.reshape(frames, gh * gw, self.a.enc_dim)
             # pairs (frame k, frame k+1): both models, both sides
             hooks = self.decode_multi(f.contiguous(), f.roll(1, 0).contiguous(), gh, gw)
-            # the heads (bf16 convs until calibrated) for the upsample outputs' amax
+            # the heads (bf16 convs) for the upsample outputs' amax
             self.heads(hooks, gh, gw, hw[0], hw[1])
             torch.cuda.synchronize(dev)
             amax = {k: float(v) for k, v in self._cal.items() if k[0] == "amax"}
             cal = {k: v[0] / v[1] for k, v in self._cal.items() if k[0] != "amax"}
+            enc, dec = _fp8_shifted_params(W, cal)
+        except BaseException:
+            # a failed calibration leaves the previous parameters in force
+            W.fp8_shift_enc, W.fp8_shift_dec = old
+            raise
         finally:
             self._cal = None
-            self.fp8 = was
-        W.fp8_shift_enc, W.fp8_shift_dec = _fp8_shifted_params(W, cal)
+            self.fp8, self.fp8_convs = was, was_convs
+            # calibration scratch (frame-count / size-specific buffers) is not kept: only
+            # the buffers this call created are dropped, so graphs captured before it stay
+            # valid (> 1 GB held for good after set_fp8)
+            for k in set(self._bufs) - bufs_before:
+                del self._bufs[k]
+        # new values written into the tensors already in use where the layout matches, so
+        # a graph captured in fp8 mode before a re-calibration replays the new parameters
+        # (a changed layout allocates afresh: re-capture after a re-calibration then)
+        W.fp8_shift_enc = _assign_params(old[0], enc)
+        W.fp8_shift_dec = [_assign_params(o, n) for o, n in zip(old[1], dec)] \
+            if len(old[1]) == len(dec) else dec
         for k in HEAD_FP8:
-            s = max(amax[("amax", k)], 1e-30) * FP8_ACT_HEADROOM / 448.0
-            W.h8_inv[k] = 1.0 / s
-            W.h8_cs[k] = (W.h8[k][1] * s).contiguous()
+            sc = max(amax[("amax", k)], 1e-30) * FP8_ACT_HEADROOM / 448.0
+            W.h8_inv[k] = 1.0 / sc
+            cs = (W.h8[k][1] * sc).contiguous()
+            prev = W.h8_cs.get(k)
+            if prev is not None and prev.shape == cs.shape and prev.dtype == cs.dtype:
+                prev.copy_(cs)
+            else:
+                W.h8_cs[k] = cs
         W.fp8_calibrated = True
 
     def _calib(self, site, i, t, z=None):
@@ -620,6 +656,8 @@ class PairModel:
 
     def _calib_amax(self, name, t):
         if getattr(self, "_cal", None) is not None:
+            if t.dtype == torch.uint8:   # e4m3 bytes: not an activation range
+                raise RuntimeError(f"calibrate_fp8: {name} is an e4m3 tensor")
             prev = self._cal.get(("amax", name), 0.0)
             self._cal[("amax", name)] = max(prev, float(t.float().abs().max()))
 

@@ -76,14 +76,15 @@ def test_gemm_rope_epilogue(ops, dev, split_k):
     assert _rel(out, ref.reshape(B * S, 3 * C)) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [None, 14])
+@pytest.mark.parametrize("tile", [None, 14, 15])
 @pytest.mark.parametrize("H,W,cin,cout,stride,relu_in,res", [
     (24, 32, 256, 256, 1, True, True), (12, 16, 768, 768, 2, False, False),
     (96, 128, 96, 256, 1, False, False), (7, 9, 64, 32, 1, True, False),
     (48, 64, 256, 256, 1, False, True)])
 def test_conv3x3_implicit_gemm(ops, dev, monkeypatch, H, W, cin, cout, stride, relu_in, res,
                                tile):
-    """tile 14: the 256x256 configuration (two-pass epilogue) on the same convs."""
+    """tile 14: the 256x256 configuration (two-pass epilogue) on the same convs; 15: the
+    256x256 ping-pong kernel (T256PP, round 6)."""
     from monst3r_slam_amd import _lib
     if tile:
         monkeypatch.setenv("M3S_GEMM_TILE", str(tile))
@@ -668,6 +669,106 @@ def test_fp8_mono_512_vs_fp32_restatement(dev, parity_log):
     assert stats["X_med"] < 0.10 and stats["C_med"] < 0.08, stats
 
 
+def _fp8_pair_stats(m, sdm, am, sdM, aM, img_i, img_j):
+    """fp8 pair inference vs the fp32 restatement: the statistics the pair bars read."""
+    from oracle import vit_ref as V
+    out = m.pair(img_i, img_j=img_j)
+    out = {k: out[k].clone() for k in ("X", "C", "D", "Q")}
+    X, C, D, Q, _, _ = V.asymmetric_inference(sdm, am, sdM, aM, img_i, img_j)
+    rel_X = ((out["X"] - X).norm(dim=-1) / X.norm(dim=-1).clamp_min(1e-6))
+    cos_D = _cos(out["D"], D)
+    return dict(X_med=float(rel_X.median()), C_med=float(((out["C"] - C).abs() / C.abs()).median()),
+                D_cos_med=float(cos_D.median()), D_cos_min=float(cos_D.min()),
+                Q_med=float(((out["Q"] - Q).abs() / Q.abs()).median()))
+
+
+def _fp8_mono_stats(m, sdm, am, img):
+    from oracle import vit_ref as V
+    feat = m.encode(img)[0].clone()
+    X, C = m.mono(feat, img.shape[-2], img.shape[-1])
+    X, C = X[0].clone(), C[0].clone()
+    f_ref, pos = V.encode(sdm, am, img)
+    Xr, Cr = V.inference_mono(sdm, am, f_ref, pos, img.shape[-2], img.shape[-1])
+    Xr, Cr = Xr.reshape(X.shape), Cr.reshape(C.shape)
+    cos_f = _cos(feat.reshape(-1, am.enc_dim), f_ref.reshape(-1, am.enc_dim))
+    return dict(feat_cos_med=float(cos_f.median()),
+                X_med=float(((X - Xr).norm(dim=-1) / Xr.norm(dim=-1).clamp_min(1e-6)).median()),
+                C_med=float(((C - Cr).abs() / Cr.abs()).median()))
+
+
+def test_fp8_calibration_out_of_distribution(dev, parity_log):
+    """the fp8 calibration (calibrate_fp8) must not be fitted to the
+    test distribution.  Both directions, the C5 bars unchanged (pair X < 6 %, C < 8 %,
+    descriptor cosine median > 0.97 / min > 0.98; mono X < 10 %, C < 8 %, feature cosine
+    > 0.998):
+      noise-calibrated (the default: two uniform-noise frames, seeds 100/101) → tested on
+        512x512 frames of the rendered room (sequence.SyntheticSequence);
+      room-calibrated (calibrate_fp8(images=) on two other room frames) → tested on the
+        uniform-noise frames of the in-distribution tests above (seeds 3, 9)."""
+    from monst3r_slam_amd import model as Mdl
+    from monst3r_slam_amd import sequence as S
+    m, (sdm, am, sdM, aM) = Mdl.build(dev)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    sdm = {k: v.to(dev) for k, v in sdm.items()}
+    sdM = {k: v.to(dev) for k, v in sdM.items()}
+    seq = S.SyntheticSequence(24, 512, 512, device=dev, seed=5, period=48)
+    room = seq.img[:, 0]                     # [24, 3, 512, 512] in [-1, 1]
+    gen = torch.Generator(device=dev).manual_seed(3)
+    noise_i = torch.rand(1, 3, 512, 512, device=dev, generator=gen) * 2 - 1
+    noise_j = torch.rand(1, 3, 512, 512, device=dev, generator=gen) * 2 - 1
+    gen = torch.Generator(device=dev).manual_seed(9)
+    noise_mono = torch.rand(1, 3, 512, 512, device=dev, generator=gen) * 2 - 1
+    cases = []
+    m.set_fp8(True)                          # noise calibration
+    cases.append(("noise-cal/room-test", room[0:1], room[6:7], room[3:4]))
+    results = {}
+    for tag, a, b, mono in cases:
+        results[tag] = (_fp8_pair_stats(m, sdm, am, sdM, aM, a, b), _fp8_mono_stats(m, sdm, am, mono))
+    m.calibrate_fp8(images=room[15:17])      # room calibration, frames no test uses
+    tag = "room-cal/noise-test"
+    results[tag] = (_fp8_pair_stats(m, sdm, am, sdM, aM, noise_i, noise_j),
+                    _fp8_mono_stats(m, sdm, am, noise_mono))
+    m.set_fp8(False)
+    for tag, (ps, ms) in results.items():
+        print(tag, ps, ms)
+        parity_log("fp8-ood-pair-" + tag, **ps)
+        parity_log("fp8-ood-mono-" + tag, **ms)
+    for tag, (ps, ms) in results.items():
+        assert ps["X_med"] < 0.06 and ps["C_med"] < 0.08, (tag, ps)
+        assert ps["D_cos_med"] > 0.97 and ps["D_cos_min"] > 0.98, (tag, ps)
+        assert ms["X_med"] < 0.10 and ms["C_med"] < 0.08 and ms["feat_cos_med"] > 0.998, (tag, ms)
+
+
+def test_fp8_recalibration_with_convs_keeps_scales(dev):
+    """calibrating again with the fp8 head convs on measures the heads' bf16
+    activations (not e4m3 byte codes): the activation scales h8_inv and the calibrated
+    biases come out as the first calibration's, written into the same tensors (a graph
+    captured before the re-calibration keeps reading valid parameters); a failed
+    calibration keeps the previous parameters; the calibration scratch is released."""
+    from monst3r_slam_amd import model as Mdl
+    m, _ = Mdl.build(dev, small=True)
+    n0 = len(m._bufs)
+    m.set_fp8(True, convs=True)
+    assert len(m._bufs) == n0
+    W = m.w
+    inv0 = dict(W.h8_inv)
+    cs_ptr = {k: v.data_ptr() for k, v in W.h8_cs.items()}
+    enc_ptr = {k: v.data_ptr() for k, v in W.fp8_shift_enc.items()}
+    enc0 = {k: v.clone() for k, v in W.fp8_shift_enc.items()}
+    m.calibrate_fp8()
+    for k in inv0:
+        assert W.h8_inv[k] == pytest.approx(inv0[k], rel=1e-6), (k, W.h8_inv[k], inv0[k])
+        assert W.h8_cs[k].data_ptr() == cs_ptr[k]
+    for k, v in W.fp8_shift_enc.items():
+        assert v.data_ptr() == enc_ptr[k]
+        assert torch.allclose(v, enc0[k], rtol=1e-6, atol=1e-7), k
+    with pytest.raises(ValueError):
+        m.calibrate_fp8(images=torch.zeros(1, 3, 64, 64, device=dev))
+    assert W.fp8_calibrated and W.fp8_shift_enc["qkv_b"].data_ptr() == enc_ptr["qkv_b"]
+    assert m.fp8 and m.fp8_convs
+    m.set_fp8(False)
+
+
 def test_split_heads_match_batched(dev):
     """pair(split_heads=True): MASt3R DPT heads as their own 2-problem set on a side stream
     (joined), MonST3R heads as another — same outputs as the 4-problem batched heads up
@@ -697,7 +798,7 @@ def _ln_stats_ref(x):
 
 @pytest.mark.parametrize("M,N,K,batch,split_k", [(768, 768, 3072, 4, 1), (768, 1024, 1024, 1, 2),
                                                  (768, 1024, 4096, 1, 0), (200, 256, 96, 2, 1)])
-@pytest.mark.parametrize("tile", [None, 12, 13, 14])
+@pytest.mark.parametrize("tile", [None, 12, 13, 14, 15])
 def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k, tile):
     """LN_STATS: the residual GEMM also stores bf16(x) and per-128-column (mean, M2) of the
     stored f32 rows — in the main epilogue and in the split-K reduce (split_k 2 / auto);
@@ -727,7 +828,7 @@ def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k, tile):
                                                   (768, 4096, 1024, 1, 0, "gelu"),
                                                   (200, 384, 256, 2, 1, "none")])
 @pytest.mark.parametrize("split", ["0", "3"])
-@pytest.mark.parametrize("tile", ["0", "12", "13", "14"])
+@pytest.mark.parametrize("tile", ["0", "12", "13", "14", "15"])
 def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi, split, tile):
     """LN_FOLD: LN(x) Wᵀ + b computed as rstd (bf16(x) (W∘γ)ᵀ − mean c1) + c2 from the
     producer's statistics, vs torch fp32 LayerNorm → Linear (→ RoPE / GELU) on x of
@@ -777,7 +878,7 @@ def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi,
     assert _rel(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("epi", ["gelu", "res", "tail"])
 def test_gemm_every_tile_config(ops, dev, monkeypatch, tile, epi):
     """Every tile configuration (M3S_GEMM_TILE override) on a 768-row problem, straight-
@@ -804,6 +905,46 @@ def test_gemm_every_tile_config(ops, dev, monkeypatch, tile, epi):
         ops.gemm(A, B, C, M, N, K, b, sA=M * K, sB=N * K, sC=M * N, bias=bias, sBias=N, R=R,
                  sR=M * N, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, split_k=1)
         assert _rel(C, ref + R) < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K,batch,wmod,epi", [
+    (4096, 4096, 4096, 1, 0, "bf16"), (6144, 3072, 768, 4, 0, "gelu"),
+    (768, 6400, 7168, 2, 0, "f32"), (1536, 2304, 1024, 8, 4, "bias"),
+    (300, 520, 72, 3, 0, "relu"), (256, 256, 64, 1, 0, "bf16"), (257, 264, 40, 2, 2, "res")])
+def test_gemm_pingpong_t256pp(ops, dev, monkeypatch, M, N, K, batch, wmod, epi):
+    """T256PP (M3S_GEMM_TILE=15): the 256x256 8-wave ping-pong kernel against torch fp32 on
+    the shapes it is routed to (4096³, the restacked keyframe-graph projections, the
+    local-feature fc2) and on edges: a weight stack shared by batch g % wmod, ragged M / N,
+    K tails (K % 64 ≠ 0), one K-tile (K ≤ 64), the run-time-flag epilogue (ReLU, no
+    straight-line variant), bias-less bf16 output, f32 out + f32 residual."""
+    from monst3r_slam_amd import _lib
+    monkeypatch.setenv("M3S_GEMM_TILE", "15")
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    A = (torch.rand(batch, M, K, device=dev, generator=g) * 2 - 1).bfloat16()
+    nw = wmod if wmod else batch
+    Bw = ((torch.rand(nw, N, K, device=dev, generator=g) * 2 - 1) / K ** 0.5).bfloat16()
+    bias = torch.randn(nw, N, device=dev, generator=g)
+    idx = torch.arange(batch, device=dev) % nw
+    ref = torch.bmm(A.float(), Bw.float()[idx].transpose(1, 2))
+    kw = dict(sA=M * K, sB=N * K, sC=M * N, wmod=wmod)
+    if epi == "bf16":
+        C = torch.empty(batch, M, N, device=dev, dtype=torch.bfloat16)
+        ops.gemm(A, Bw, C, M, N, K, batch, **kw)
+        want = ref
+    elif epi in ("gelu", "bias", "relu"):
+        C = torch.empty(batch, M, N, device=dev, dtype=torch.bfloat16)
+        fl = {"gelu": _lib.EPI_GELU, "bias": 0, "relu": _lib.EPI_RELU}[epi]
+        ops.gemm(A, Bw, C, M, N, K, batch, bias=bias, sBias=N, flags=fl, **kw)
+        want = ref + bias[idx][:, None]
+        want = F.gelu(want) if epi == "gelu" else F.relu(want) if epi == "relu" else want
+    else:
+        R = torch.randn(batch, M, N, device=dev, generator=g) if epi == "res" else None
+        C = torch.empty(batch, M, N, device=dev)
+        fl = _lib.EPI_OUT_F32 | (_lib.EPI_RES_F32 if R is not None else 0)
+        ops.gemm(A, Bw, C, M, N, K, batch, R=R, sR=M * N, flags=fl, bias=bias, sBias=N, **kw)
+        want = ref + bias[idx][:, None] + (R if R is not None else 0)
+    tol = 1e-3 if C.dtype == torch.float32 else 1e-2
+    assert _rel(C, want) < tol, (_rel(C, want), tol)
 
 
 def test_cross_attention_kv_batch_xor(ops, dev):
