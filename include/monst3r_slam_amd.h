@@ -49,7 +49,9 @@ int m3s_device_count(void);
  * in s_memrealtime ticks of 100 MHz, block b stamping pair b % 64; the launch spans
  * [min of the starts, max of the ends]; the caller fills every pair with {UINT64_MAX, 0}
  * before a run; then a 4-u64 header {block-log buffer or 0, pointer to its u32 record
- * counter, capacity in records, 0}: when set, the first wave of every block appends
+ * counter, capacity in records, 0}, zeroed by m3s_timeline_set (call it outside any stream
+ * capture; it synchronises the device) and filled by the caller afterwards: when set, the
+ * first wave of every block appends
  * {start, end, slot address, HW_ID | XCC_ID << 32, 4 phase marks} (8 u64) at the counter — the busy
  * intervals of every CU).  A null d_buf
  * disarms it (later launches carry no slot).  m3s_timeline_count() = slots taken since the
@@ -73,6 +75,16 @@ int m3s_iter_proj(const float* d_rays_img_with_grad, const float* d_pts_3d_norm,
                   const float* d_p_init, float* d_p_new, uint8_t* d_converged,
                   int64_t b, int64_t h, int64_t w, int64_t n,
                   int max_iter, float lambda_init, float cost_thresh, void* stream);
+
+/* m3s_iter_proj under the FMA-contracted numeric model (opt-in): the products fused into
+ * the adds that consume them as nvcc's default --fmad=true contraction does under LLVM's
+ * rules (sums of products as fma chains, a*b - c*d as fma(a, b, -(c*d)), r*inv - pts and
+ * u + det_inv*(...) fused).  Bit-exact to oracle/matching_ref.c ref_iter_proj_fma; same
+ * arguments and errors as m3s_iter_proj.  DESIGN §2 records how far the models differ. */
+int m3s_iter_proj_fma(const float* d_rays_img_with_grad, const float* d_pts_3d_norm,
+                      const float* d_p_init, float* d_p_new, uint8_t* d_converged,
+                      int64_t b, int64_t h, int64_t w, int64_t n,
+                      int max_iter, float lambda_init, float cost_thresh, void* stream);
 
 /* Replaces mast3r_slam_backends.refine_matches (gn.cpp:101-114 → matching_kernels.cu:84-116,
  * kernel :25-81).  D11 f16[b,h,w,fdim], D21 f16[b,n,fdim] (raw IEEE half bits),
@@ -150,7 +162,7 @@ int m3s_gauss_newton_points(float* d_Twc, const float* d_Xs, const float* d_Cs,
                             void* d_workspace, int* h_status_out, void* stream);
 
 /* Diagnostic: 1 = run every backend GN solve on the global-memory dense path instead of the
- * LDS-resident one used while 7(P-1) <= 126 (both give bit-identical poses; tests compare
+ * LDS-resident one used while 7(P-1) <= 140 (both give bit-identical poses; tests compare
  * them).  Not thread-scoped; returns M3S_OK. */
 int m3s_gn_force_global_solve(int on);
 

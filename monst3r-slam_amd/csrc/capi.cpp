@@ -43,6 +43,15 @@ unsigned long long* m3s_timeline_take(int kind, double flops, int64_t d0, int64_
 
 extern "C" int m3s_timeline_set(void* d_buf, int capacity) {
   if (d_buf && capacity <= 0) return M3S_ERR_INVALID_ARG;
+  if (d_buf) {
+    // every slot's 4-u64 header (block-log pointer, counter, capacity) starts zeroed: a
+    // caller that fills only the stamp pairs (or allocates the slots uninitialised) gets no
+    // block log instead of a garbage pointer dereferenced inside a captured step
+    if (hipMemset2D(reinterpret_cast<char*>(d_buf) + 128 * 8, 132 * 8, 0,
+                    4 * 8, (size_t)capacity) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
+      return M3S_ERR_INVALID_ARG;
+  }
   std::lock_guard<std::mutex> lk(g_tl_mu);
   g_tl = reinterpret_cast<unsigned long long*>(d_buf);
   g_tl_cap = d_buf ? capacity : 0;

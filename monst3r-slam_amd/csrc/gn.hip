@@ -608,7 +608,8 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_kernel(
 //    triangular solves by one wave with the right-hand side in registers (no barriers,
 //    each panel's operands read ahead of its dependent chain), retraction and the
 //    convergence test as before.
-constexpr int kLdsN = 126;            // P <= 19
+constexpr int kLdsN = 140;            // P <= 21 (sA 153 KB of the 160 KB LDS)
+constexpr int kLdsP = kLdsN / 7 + 1;
 constexpr int kEB = 56;               // per edge: A (49) then v (7), f64
 
 // LDS written by some lanes of a wave, then read by others of the same wave: wait for the
@@ -699,7 +700,7 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
   //     gn_solve_kernel step 1, same order), T = M G, A = T Mᵀ, v = M v'
   // per-wave scratch for two edges at a time, in sA past the poses' M: edge h's G at
   // 147 h, T at 147 h + 49, v' at 147 h + 98
-  double* scr = sA + 1024 + wv * 294;  // P * 49 <= 1024; 1024 + 16 * 294 <= kLdsN^2
+  double* scr = sA + 49 * kLdsP + wv * 294;  // past the poses' M; + 16 * 294 <= kLdsN^2
   const bool tl = lane < 49, vl = lane >= 56 && lane < 63;  // T / A lanes; v lanes
   const int r_l = tl ? lane / 7 : lane - 56, c_l = tl ? lane % 7 : 0;
   // pose ranks of this wave's edges k0 .. k0 + 63 (its k-th edge is wv + NW k), one per lane,
@@ -864,12 +865,14 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
   bool fail = false;
   if (tid == 0) s_fail = 0;
   auto factor_panel = [&](int c0) {  // wave 0
-    const int i0 = c0 + lane, i1 = c0 + 64 + lane;  // n - c0 <= 126 rows
-    double a0[7], a1[7];
+    // rows c0 + lane + 64 t, t < 3: n - c0 <= 140 rows (the third only for the first panels)
+    const int i0 = c0 + lane, i1 = c0 + 64 + lane, i2 = c0 + 128 + lane;
+    double a0[7], a1[7], a2[7];
 #pragma unroll
     for (int c = 0; c < 7; c++) {
       a0[c] = i0 < n ? sA[i0 * n + c0 + c] : 0.0;
       a1[c] = i1 < n ? sA[i1 * n + c0 + c] : 0.0;
+      a2[c] = i2 < n ? sA[i2 * n + c0 + c] : 0.0;
     }
     bool f = false;
 #pragma unroll
@@ -881,15 +884,17 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
         break;
       }
       const double rpiv = 1.0 / sqrt(d);
-      const double l0 = a0[c] * rpiv, l1 = a1[c] * rpiv;
+      const double l0 = a0[c] * rpiv, l1 = a1[c] * rpiv, l2 = a2[c] * rpiv;
       if (i0 > k && i0 < n) sA[k * n + i0] = l0;
       if (i1 > k && i1 < n) sA[k * n + i1] = l1;
+      if (i2 < n) sA[k * n + i2] = l2;
       if (lane == 0) sR[k] = rpiv;
 #pragma unroll
       for (int c2 = c + 1; c2 < 7; c2++) {
         const double lj = bcast_f64(l0, c2);        // L[c0 + c2][k]
         if (i0 >= c0 + c2) a0[c2] -= l0 * lj;
         if (i1 >= c0 + c2) a1[c2] -= l1 * lj;
+        if (i2 < n) a2[c2] -= l2 * lj;
       }
     }
     if (lane == 0 && f) s_fail = 1;
@@ -918,9 +923,9 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
       factor_panel(t0);
     } else {  // panel p applied to columns t0 + 7 .. i of row i = t0 + 7 + ri
       const int t1 = t0 + 7;
-      const int ri = (tid - 64) >> 3, cg = tid & 7;
-      const int i = t1 + ri;
-      if (i < n) {
+      const int cg = tid & 7;
+      // 120 rows per pass (waves 1..15, 8 lanes a row); a second pass past row t1 + 119
+      for (int i = t1 + ((tid - 64) >> 3); i < n; i += (kSolveThreads - 64) / 8) {
         double li[7];
 #pragma unroll
         for (int c = 0; c < 7; c++) li[c] = sA[(c0 + c) * n + i];
@@ -953,30 +958,36 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
   }
 
   M3S_GS(3)
-  // 4) L y = b, Lᵀ x = y by wave 0, rows i = lane + 64 t in registers (t < 2: n <= 128);
+  // 4) L y = b, Lᵀ x = y by wave 0, rows i = lane + 64 t in registers (t < 3: n <= 192);
   //    the solved unknown goes to every lane by v_readlane (the owner lane is uniform).  The
-  //    unknowns of rows < 64 and >= 64 are swept by separate loops, so the owner's register
-  //    is known at compile time (a select between the two was on every step's dependent
-  //    chain), and each group of 8 steps reads its columns of L and 1 / L[j][j] (clamped,
-  //    unconditional LDS loads; masked lanes do not use them) ahead of its chain; the masked
-  //    updates are selects, so the compiler does not sink those loads into branches.
+  //    unknowns of rows [0, 64), [64, 128) and [128, n) are swept by separate loops, so the
+  //    owner's register is known at compile time (a select between them was on every step's
+  //    dependent chain), and each group of 8 steps reads its columns of L and 1 / L[j][j]
+  //    (clamped, unconditional LDS loads; masked lanes do not use them) ahead of its chain;
+  //    the masked updates are selects, so the compiler does not sink those loads into
+  //    branches.  Every x_i receives x_i -= L[i][j] y_j (j increasing), then
+  //    x_i -= L[j][i] x_j (j decreasing) — gn_solve_kernel's order.
   if (wv == 0 && !fail) {
     constexpr int G8 = 8;
-    const int lc = min(lane, n - 1), lc1 = min(lane + 64, n - 1), n0 = min(n, 64);
+    const int lc = min(lane, n - 1), lc1 = min(lane + 64, n - 1), lc2 = min(lane + 128, n - 1);
+    const int n0 = min(n, 64), n1 = min(n, 128);
     double x0 = lane < n ? sb[lane] : 0.0, x1 = lane + 64 < n ? sb[lane + 64] : 0.0;
+    double x2 = lane + 128 < n ? sb[lane + 128] : 0.0;
     for (int jb = 0; jb < n0; jb += G8) {       // forward, unknowns j < 64 (x0 of lane j)
-      double c0[G8], c1[G8], rr[G8];
+      double c0[G8], c1[G8], c2[G8], rr[G8];
 #pragma unroll
       for (int u = 0; u < G8; u++) {
         const int j = min(jb + u, n - 1);
         c0[u] = sA[j * n + lc];
         c1[u] = sA[j * n + lc1];
+        c2[u] = sA[j * n + lc2];
         rr[u] = sR[j];
       }
 #pragma unroll
       for (int u = 0; u < G8; u++) {
         pin_vgpr(c0[u]);
         pin_vgpr(c1[u]);
+        pin_vgpr(c2[u]);
         pin_vgpr(rr[u]);
       }
 #pragma unroll
@@ -987,31 +998,85 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
         if (lane == j) x0 = yj;
         x0 = lane > j && lane < n ? x0 - c0[u] * yj : x0;
         x1 = lane + 64 < n ? x1 - c1[u] * yj : x1;
+        x2 = lane + 128 < n ? x2 - c2[u] * yj : x2;
       }
     }
-    for (int jb = 64; jb < n; jb += G8) {       // forward, unknowns j >= 64 (x1 of lane j - 64)
-      double c1[G8], rr[G8];
+    for (int jb = 64; jb < n1; jb += G8) {      // forward, unknowns 64 <= j < 128 (x1)
+      double c1[G8], c2[G8], rr[G8];
 #pragma unroll
       for (int u = 0; u < G8; u++) {
         const int j = min(jb + u, n - 1);
         c1[u] = sA[j * n + lc1];
+        c2[u] = sA[j * n + lc2];
         rr[u] = sR[j];
       }
 #pragma unroll
       for (int u = 0; u < G8; u++) {
         pin_vgpr(c1[u]);
+        pin_vgpr(c2[u]);
+        pin_vgpr(rr[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = jb + u;
+        if (j >= n1) break;
+        const double yj = bcast_f64(x1 * rr[u], j - 64);
+        if (lane == j - 64) x1 = yj;
+        x1 = lane + 64 > j && lane + 64 < n ? x1 - c1[u] * yj : x1;
+        x2 = lane + 128 < n ? x2 - c2[u] * yj : x2;
+      }
+    }
+    for (int jb = 128; jb < n; jb += G8) {      // forward, unknowns j >= 128 (x2)
+      double c2[G8], rr[G8];
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = min(jb + u, n - 1);
+        c2[u] = sA[j * n + lc2];
+        rr[u] = sR[j];
+      }
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        pin_vgpr(c2[u]);
         pin_vgpr(rr[u]);
       }
 #pragma unroll
       for (int u = 0; u < G8; u++) {
         const int j = jb + u;
         if (j >= n) break;
-        const double yj = bcast_f64(x1 * rr[u], j - 64);
-        if (lane == j - 64) x1 = yj;
-        x1 = lane + 64 > j && lane + 64 < n ? x1 - c1[u] * yj : x1;
+        const double yj = bcast_f64(x2 * rr[u], j - 128);
+        if (lane == j - 128) x2 = yj;
+        x2 = lane + 128 > j && lane + 128 < n ? x2 - c2[u] * yj : x2;
       }
     }
-    for (int jt = n - 1; jt >= 64; jt -= G8) {  // backward, unknowns j >= 64
+    for (int jt = n - 1; jt >= 128; jt -= G8) { // backward, unknowns j >= 128 (x2)
+      double c0[G8], c1[G8], c2[G8], rr[G8];
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = max(jt - u, 0);
+        c0[u] = sA[lc * n + j];
+        c1[u] = sA[lc1 * n + j];
+        c2[u] = sA[lc2 * n + j];
+        rr[u] = sR[j];
+      }
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        pin_vgpr(c0[u]);
+        pin_vgpr(c1[u]);
+        pin_vgpr(c2[u]);
+        pin_vgpr(rr[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < G8; u++) {
+        const int j = jt - u;
+        if (j < 128) break;
+        const double xj = bcast_f64(x2 * rr[u], j - 128);
+        if (lane == j - 128) x2 = xj;
+        x0 = lane < j ? x0 - c0[u] * xj : x0;
+        x1 = lane + 64 < j ? x1 - c1[u] * xj : x1;
+        x2 = lane + 128 < j ? x2 - c2[u] * xj : x2;
+      }
+    }
+    for (int jt = n1 - 1; jt >= 64; jt -= G8) { // backward, unknowns 64 <= j < 128 (x1)
       double c0[G8], c1[G8], rr[G8];
 #pragma unroll
       for (int u = 0; u < G8; u++) {
@@ -1060,6 +1125,7 @@ __global__ __launch_bounds__(kSolveThreads) void gn_solve_lds_kernel(
     }
     if (lane < n) sb[lane] = x0;
     if (lane + 64 < n) sb[lane + 64] = x1;
+    if (lane + 128 < n) sb[lane + 128] = x2;
   }
   __syncthreads();
   M3S_GS(4)

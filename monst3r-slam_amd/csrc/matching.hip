@@ -44,7 +44,7 @@ __device__ __forceinline__ Bilin bilin_weights(float u, float v) {
 
 // r[j] = w11*r11[j] + w12*r12[j] + w21*r21[j] + w22*r22[j], pixels opposite the area
 // (matching_kernels.cu:154-158).  img points at the (b) image, row stride w*C floats.
-template <int C, int NCH>
+template <int C, int NCH, bool FMA = false>
 __device__ __forceinline__ void bilin_sample(const float* __restrict__ img, int w,
                                              const Bilin& bw, float* out) {
   const float* r22 = img + ((int64_t)bw.v11 * w + bw.u11) * C;        // top left
@@ -53,15 +53,32 @@ __device__ __forceinline__ void bilin_sample(const float* __restrict__ img, int 
   const float* r11 = r12 + C;                                          // bottom right
 #pragma unroll
   for (int j = 0; j < NCH; j++) {
-    float s = bw.w11 * r11[j];
-    s = s + bw.w12 * r12[j];
-    s = s + bw.w21 * r21[j];
-    s = s + bw.w22 * r22[j];
-    out[j] = s;
+    if (FMA) {   // the contracted model (iter_proj_kernel<C, true>)
+      out[j] = __builtin_fmaf(bw.w22, r22[j],
+                              __builtin_fmaf(bw.w21, r21[j],
+                                             __builtin_fmaf(bw.w11, r11[j], bw.w12 * r12[j])));
+    } else {
+      float s = bw.w11 * r11[j];
+      s = s + bw.w12 * r12[j];
+      s = s + bw.w21 * r21[j];
+      s = s + bw.w22 * r22[j];
+      out[j] = s;
+    }
   }
 }
 
-template <int C>
+// a0*b0 + a1*b1 + a2*b2: uncontracted, or as LLVM contracts it (the first product fused
+// into the second add, the third into the result: oracle/matching_ref.c ref_iter_proj_fma)
+template <bool FMA>
+__device__ __forceinline__ float dot3(float a0, float a1, float a2, float b0, float b1, float b2) {
+  if (FMA) return __builtin_fmaf(a2, b2, __builtin_fmaf(a0, b0, a1 * b1));
+  return a0 * b0 + a1 * b1 + a2 * b2;
+}
+
+// FMA = false: the reference source taken literally (every product / sum rounded);
+// FMA = true: the FMA-contracted model of nvcc's default --fmad=true (opt-in,
+// m3s_iter_proj_fma; oracle/matching_ref.c ref_iter_proj_fma).
+template <int C, bool FMA>
 __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
     const float* __restrict__ rays_img, const float* __restrict__ pts_3d_norm,
     const float* __restrict__ p_init, float* __restrict__ p_new,
@@ -88,36 +105,47 @@ __global__ __launch_bounds__(kBlock) void iter_proj_kernel(
   for (int it = 0; it < max_iter; it++) {
     float s[9];
     Bilin bw = bilin_weights(u, v);
-    bilin_sample<C, 9>(img, w, bw, s);
+    bilin_sample<C, 9, FMA>(img, w, bw, s);
     // normalise ray (:173-178); 1.0/r_norm is a double division in the reference
-    float r_norm = sqrtf(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+    float r_norm = sqrtf(dot3<FMA>(s[0], s[1], s[2], s[0], s[1], s[2]));
     float r_norm_inv = (float)(1.0 / (double)r_norm);
-    const float r0 = s[0] * r_norm_inv, r1 = s[1] * r_norm_inv, r2 = s[2] * r_norm_inv;
-    const float e0 = r0 - t0, e1 = r1 - t1, e2 = r2 - t2;
-    const float cost = e0 * e0 + e1 * e1 + e2 * e2;
+    // err = r * inv - pts (contracted: fma(r, inv, -pts))
+    const float e0 = FMA ? __builtin_fmaf(s[0], r_norm_inv, -t0) : s[0] * r_norm_inv - t0;
+    const float e1 = FMA ? __builtin_fmaf(s[1], r_norm_inv, -t1) : s[1] * r_norm_inv - t1;
+    const float e2 = FMA ? __builtin_fmaf(s[2], r_norm_inv, -t2) : s[2] * r_norm_inv - t2;
+    const float cost = dot3<FMA>(e0, e1, e2, e0, e1, e2);
     // J^T J + lambda I, -J^T r  (:187-197)
-    float A00 = s[3] * s[3] + s[4] * s[4] + s[5] * s[5];
-    const float A01 = s[3] * s[6] + s[4] * s[7] + s[5] * s[8];
-    float A11 = s[6] * s[6] + s[7] * s[7] + s[8] * s[8];
-    const float b0 = -(e0 * s[3] + e1 * s[4] + e2 * s[5]);
-    const float b1 = -(e0 * s[6] + e1 * s[7] + e2 * s[8]);
+    float A00 = dot3<FMA>(s[3], s[4], s[5], s[3], s[4], s[5]);
+    const float A01 = dot3<FMA>(s[3], s[4], s[5], s[6], s[7], s[8]);
+    float A11 = dot3<FMA>(s[6], s[7], s[8], s[6], s[7], s[8]);
+    const float b0 = -dot3<FMA>(e0, e1, e2, s[3], s[4], s[5]);
+    const float b1 = -dot3<FMA>(e0, e1, e2, s[6], s[7], s[8]);
     A00 = A00 + lambda;
     A11 = A11 + lambda;
-    const float det_inv = (float)(1.0 / (double)(A00 * A11 - A01 * A01));
-    const float delta_u = det_inv * (A11 * b0 - A01 * b1);
-    const float delta_v = det_inv * (-A01 * b0 + A00 * b1);
-    float u_new = clamp_ref(u + delta_u, 1.0f, umax);
-    float v_new = clamp_ref(v + delta_v, 1.0f, vmax);
+    float u_new, v_new;
+    if (FMA) {
+      const float det_inv = (float)(1.0 / (double)__builtin_fmaf(A00, A11, -(A01 * A01)));
+      u_new = __builtin_fmaf(det_inv, __builtin_fmaf(A11, b0, -(A01 * b1)), u);
+      v_new = __builtin_fmaf(det_inv, __builtin_fmaf(-A01, b0, A00 * b1), v);
+    } else {
+      const float det_inv = (float)(1.0 / (double)(A00 * A11 - A01 * A01));
+      const float delta_u = det_inv * (A11 * b0 - A01 * b1);
+      const float delta_v = det_inv * (-A01 * b0 + A00 * b1);
+      u_new = u + delta_u;
+      v_new = v + delta_v;
+    }
+    u_new = clamp_ref(u_new, 1.0f, umax);
+    v_new = clamp_ref(v_new, 1.0f, vmax);
     // re-evaluate cost at the candidate (:200-228); only the ray channels are needed
     float s2[3];
     Bilin bw2 = bilin_weights(u_new, v_new);
-    bilin_sample<C, 3>(img, w, bw2, s2);
-    r_norm = sqrtf(s2[0] * s2[0] + s2[1] * s2[1] + s2[2] * s2[2]);
+    bilin_sample<C, 3, FMA>(img, w, bw2, s2);
+    r_norm = sqrtf(dot3<FMA>(s2[0], s2[1], s2[2], s2[0], s2[1], s2[2]));
     r_norm_inv = (float)(1.0 / (double)r_norm);
-    const float f0 = s2[0] * r_norm_inv - t0;
-    const float f1 = s2[1] * r_norm_inv - t1;
-    const float f2 = s2[2] * r_norm_inv - t2;
-    const float new_cost = f0 * f0 + f1 * f1 + f2 * f2;
+    const float f0 = FMA ? __builtin_fmaf(s2[0], r_norm_inv, -t0) : s2[0] * r_norm_inv - t0;
+    const float f1 = FMA ? __builtin_fmaf(s2[1], r_norm_inv, -t1) : s2[1] * r_norm_inv - t1;
+    const float f2 = FMA ? __builtin_fmaf(s2[2], r_norm_inv, -t2) : s2[2] * r_norm_inv - t2;
+    const float new_cost = dot3<FMA>(f0, f1, f2, f0, f1, f2);
     if (new_cost < cost) {
       u = u_new;
       v = v_new;
@@ -547,20 +575,42 @@ __global__ __launch_bounds__(kBlock) void pixel_to_lin_kernel(const int64_t* __r
 
 }  // namespace
 
-extern "C" int m3s_iter_proj(const float* d_rays, const float* d_pts, const float* d_p_init,
-                             float* d_p_new, uint8_t* d_conv, int64_t b, int64_t h, int64_t w,
-                             int64_t n, int max_iter, float lambda_init, float cost_thresh,
-                             void* stream) {
+namespace {
+int iter_proj_launch(bool fma, const float* d_rays, const float* d_pts, const float* d_p_init,
+                     float* d_p_new, uint8_t* d_conv, int64_t b, int64_t h, int64_t w, int64_t n,
+                     int max_iter, float lambda_init, float cost_thresh, void* stream) {
   if (b < 0 || n < 0 || h < 3 || w < 3) return M3S_ERR_INVALID_ARG;
   if (b == 0 || n == 0) return M3S_OK;
   if (!d_rays || !d_pts || !d_p_init || !d_p_new || !d_conv) return M3S_ERR_INVALID_ARG;
   if (b > 65535) return M3S_ERR_TOO_LARGE;
   dim3 grid(m3s_div_up(n, kBlock), (unsigned)b);
-  hipLaunchKernelGGL(iter_proj_kernel<9>, grid, dim3(kBlock), 0, m3s_stream(stream), d_rays,
-                     d_pts, d_p_init, d_p_new, d_conv, (int)h, (int)w, n, max_iter, lambda_init,
-                     cost_thresh);
+  if (fma)
+    hipLaunchKernelGGL((iter_proj_kernel<9, true>), grid, dim3(kBlock), 0, m3s_stream(stream),
+                       d_rays, d_pts, d_p_init, d_p_new, d_conv, (int)h, (int)w, n, max_iter,
+                       lambda_init, cost_thresh);
+  else
+    hipLaunchKernelGGL((iter_proj_kernel<9, false>), grid, dim3(kBlock), 0, m3s_stream(stream),
+                       d_rays, d_pts, d_p_init, d_p_new, d_conv, (int)h, (int)w, n, max_iter,
+                       lambda_init, cost_thresh);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
+}
+}  // namespace
+
+extern "C" int m3s_iter_proj(const float* d_rays, const float* d_pts, const float* d_p_init,
+                             float* d_p_new, uint8_t* d_conv, int64_t b, int64_t h, int64_t w,
+                             int64_t n, int max_iter, float lambda_init, float cost_thresh,
+                             void* stream) {
+  return iter_proj_launch(false, d_rays, d_pts, d_p_init, d_p_new, d_conv, b, h, w, n, max_iter,
+                          lambda_init, cost_thresh, stream);
+}
+
+extern "C" int m3s_iter_proj_fma(const float* d_rays, const float* d_pts, const float* d_p_init,
+                                 float* d_p_new, uint8_t* d_conv, int64_t b, int64_t h, int64_t w,
+                                 int64_t n, int max_iter, float lambda_init, float cost_thresh,
+                                 void* stream) {
+  return iter_proj_launch(true, d_rays, d_pts, d_p_init, d_p_new, d_conv, b, h, w, n, max_iter,
+                          lambda_init, cost_thresh, stream);
 }
 
 extern "C" int m3s_refine_matches(const uint16_t* d_D11, const uint16_t* d_D21,

@@ -30,6 +30,7 @@ SIGNATURES = {
     "m3s_timeline_count": (_I, []),
     "m3s_timeline_meta": (_I, [_P, _P, _P, _I]),
     "m3s_iter_proj": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _F, _F, _P]),
+    "m3s_iter_proj_fma": (_I, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I, _F, _F, _P]),
     "m3s_refine_matches": (_I, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I, _I, _P]),
     "m3s_match_prep": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P]),
     "m3s_match_occlusion": (_I, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _F, _P]),

@@ -55,10 +55,12 @@ def match_iterative_proj(X11, X21, D11, D21, idx_1_to_2_init=None, cfg=None, idx
     rwg, pts, p_init = prep_for_iter_proj(X11, X21, idx_1_to_2_init)
     p = torch.empty((b, n, 2), dtype=torch.float32, device=dev)
     conv = torch.empty((b, n), dtype=torch.uint8, device=dev)
-    _lib.check(lib.m3s_iter_proj(_lib.ptr(rwg), _lib.ptr(pts), _lib.ptr(p_init), _lib.ptr(p),
-                                 _lib.ptr(conv), b, h, w, n, int(cfg["max_iter"]),
-                                 float(cfg["lambda_init"]), float(cfg["convergence_thresh"]), s),
-               "iter_proj")
+    # cfg["iter_proj_fma"] (opt-in): the FMA-contracted numeric model of the reference
+    # binary's nvcc --fmad=true build instead of its source taken literally
+    ip = lib.m3s_iter_proj_fma if cfg.get("iter_proj_fma", False) else lib.m3s_iter_proj
+    _lib.check(ip(_lib.ptr(rwg), _lib.ptr(pts), _lib.ptr(p_init), _lib.ptr(p), _lib.ptr(conv), b,
+                  h, w, n, int(cfg["max_iter"]), float(cfg["lambda_init"]),
+                  float(cfg["convergence_thresh"]), s), "iter_proj")
     p1 = torch.empty((b, n, 2), dtype=torch.int64, device=dev)
     valid = torch.empty((b, n), dtype=torch.uint8, device=dev)
     _lib.check(lib.m3s_match_occlusion(_lib.ptr(X11), _lib.ptr(X21), _lib.ptr(p), _lib.ptr(conv),

@@ -170,6 +170,102 @@ void ref_iter_proj(const float* rays, const float* pts, const float* p_init, flo
   }
 }
 
+/* ---- iter_proj, contracted model ----------------------
+ * The reference is built by nvcc -O3 (setup.py:29-36), whose default --fmad=true lets the
+ * compiler fuse a product into the add / subtract that consumes it.  This variant applies
+ * the fusions LLVM's DAG combiner (NVPTX enables aggressive FMA fusion, no reassociation)
+ * makes on matching_kernels.cu:154-228 as written — a sum of products a0*b0 + a1*b1 + ...
+ * becomes fma(a_k, b_k, ... fma(a1, b1, a0*b0)) with the FIRST product fused into the
+ * second add (fadd(fmul N0, fmul N1) -> fma(N0.x, N0.y, N1)), a difference of products
+ * fma(x, y, -(z*w)), and the consumer of a single-use product is fused with it:
+ *   bilinear   fma(w22,r22, fma(w21,r21, fma(w11,r11, w12*r12)))
+ *   |r|^2      fma(r2,r2, fma(r0,r0, r1*r1))            (also cost, A00, A01, A11, b0, b1)
+ *   err_j      fma(r_j, r_norm_inv, -pts_j)               (r *= inv then r - pts)
+ *   det        fma(A00, A11, -(A01*A01))
+ *   delta      fma(A11, b0, -(A01*b1)), fma(-A01, b0, A00*b1)
+ *   u + delta  fma(det_inv, (A11 b0 - A01 b1), u)         (delta_u = det_inv * (...))
+ * The f64 sub-expressions stay f64 (1.0/x, (1.0-du)*dv: a product of a difference, no
+ * fusion).  Which fusions the proprietary nvcc front end actually emits cannot be checked
+ * here (no CUDA toolkit); DESIGN §2 records how far the two models' results differ. */
+static float dot3c(const float* a, const float* b) {
+  return fmaf(a[2], b[2], fmaf(a[0], b[0], a[1] * b[1]));
+}
+
+static void bilinear_c(const float* img, int w, int C, float u, float v, int nch, float* out) {
+  int u11 = (int)floorf(u);
+  int v11 = (int)floorf(v);
+  float du = u - (float)u11;
+  float dv = v - (float)v11;
+  float w11 = du * dv;
+  float w12 = (float)((1.0 - (double)du) * (double)dv);
+  float w21 = (float)((double)du * (1.0 - (double)dv));
+  float w22 = (float)((1.0 - (double)du) * (1.0 - (double)dv));
+  const float* r11 = img + ((int64_t)(v11 + 1) * w + (u11 + 1)) * C;
+  const float* r12 = img + ((int64_t)(v11 + 1) * w + u11) * C;
+  const float* r21 = img + ((int64_t)v11 * w + (u11 + 1)) * C;
+  const float* r22 = img + ((int64_t)v11 * w + u11) * C;
+  for (int j = 0; j < nch; j++)
+    out[j] = fmaf(w22, r22[j], fmaf(w21, r21[j], fmaf(w11, r11[j], w12 * r12[j])));
+}
+
+void ref_iter_proj_fma(const float* rays, const float* pts, const float* p_init, float* p_new,
+                       uint8_t* converged, int64_t b, int64_t h, int64_t w, int64_t n, int C,
+                       int max_iter, float lambda_init, float cost_thresh) {
+  for (int64_t bi = 0; bi < b; bi++) {
+    const float* img = rays + bi * h * w * C;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+    for (int64_t i = 0; i < n; i++) {
+      const int64_t q = bi * n + i;
+      const float* t = pts + 3 * q;
+      float u = clampf_ref(p_init[2 * q], 1.0f, (float)(w - 2));
+      float v = clampf_ref(p_init[2 * q + 1], 1.0f, (float)(h - 2));
+      float lambda = lambda_init;
+      uint8_t conv = 0;
+      for (int it = 0; it < max_iter; it++) {
+        float s[9], err[3], r[3];
+        bilinear_c(img, (int)w, C, u, v, 9, s);
+        float r_norm = sqrtf(dot3c(s, s));
+        float r_norm_inv = (float)(1.0 / (double)r_norm);
+        for (int j = 0; j < 3; j++) err[j] = fmaf(s[j], r_norm_inv, -t[j]);
+        float cost = dot3c(err, err);
+        const float* gx = s + 3;
+        const float* gy = s + 6;
+        float A00 = dot3c(gx, gx);
+        float A01 = dot3c(gx, gy);
+        float A11 = dot3c(gy, gy);
+        float b0 = -dot3c(err, gx);
+        float b1 = -dot3c(err, gy);
+        A00 += lambda;
+        A11 += lambda;
+        float det_inv = (float)(1.0 / (double)fmaf(A00, A11, -(A01 * A01)));
+        float u_new = fmaf(det_inv, fmaf(A11, b0, -(A01 * b1)), u);
+        float v_new = fmaf(det_inv, fmaf(-A01, b0, A00 * b1), v);
+        u_new = clampf_ref(u_new, 1.0f, (float)(w - 2));
+        v_new = clampf_ref(v_new, 1.0f, (float)(h - 2));
+        bilinear_c(img, (int)w, C, u_new, v_new, 3, r);
+        r_norm = sqrtf(dot3c(r, r));
+        r_norm_inv = (float)(1.0 / (double)r_norm);
+        for (int j = 0; j < 3; j++) err[j] = fmaf(r[j], r_norm_inv, -t[j]);
+        float new_cost = dot3c(err, err);
+        if (new_cost < cost) {
+          u = u_new;
+          v = v_new;
+          lambda = (float)((double)lambda * 0.1);
+          conv = new_cost < cost_thresh;
+        } else {
+          lambda = (float)((double)lambda * 10.0);
+          conv = cost < cost_thresh;
+        }
+      }
+      p_new[2 * q] = u;
+      p_new[2 * q + 1] = v;
+      converged[q] = conv;
+    }
+  }
+}
+
 /* ---- refine_matches (matching_kernels.cu:25-81) --------------------------- */
 static void refine_soft(const uint16_t* D11, const uint16_t* D21, const int64_t* p1,
                         int64_t* p1_new, int64_t b, int64_t h, int64_t w, int64_t n,

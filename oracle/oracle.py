@@ -36,6 +36,8 @@ def lib():
         L.ref_iter_proj.argtypes = [P, P, P, P, P, i64, i64, i64, i64, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_float, ctypes.c_float]
         L.ref_iter_proj.restype = None
+        L.ref_iter_proj_fma.argtypes = L.ref_iter_proj.argtypes
+        L.ref_iter_proj_fma.restype = None
         L.ref_refine_matches.argtypes = [P, P, P, P, i64, i64, i64, i64, i64, ctypes.c_int,
                                          ctypes.c_int]
         L.ref_refine_matches.restype = None
@@ -72,8 +74,10 @@ def _c(a, dtype):
 # --------------------------------------------------------------------------
 # matching
 # --------------------------------------------------------------------------
-def iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, cost_thresh):
-    """matching_kernels.cu:119-316 restated (oracle/matching_ref.c)."""
+def iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, cost_thresh,
+              contract=False):
+    """matching_kernels.cu:119-316 restated (oracle/matching_ref.c).  contract=True: the
+    FMA-contracted model of nvcc's default --fmad=true (ref_iter_proj_fma)."""
     rays = _c(rays_img_with_grad, np.float32)
     pts = _c(pts_3d_norm, np.float32)
     pin = _c(p_init, np.float32)
@@ -81,8 +85,9 @@ def iter_proj(rays_img_with_grad, pts_3d_norm, p_init, max_iter, lambda_init, co
     n = pts.shape[1]
     p_new = np.zeros((b, n, 2), np.float32)
     conv = np.zeros((b, n), np.uint8)
-    lib().ref_iter_proj(_p(rays), _p(pts), _p(pin), _p(p_new), _p(conv), b, h, w, n, c,
-                        int(max_iter), float(lambda_init), float(cost_thresh))
+    fn = lib().ref_iter_proj_fma if contract else lib().ref_iter_proj
+    fn(_p(rays), _p(pts), _p(pin), _p(p_new), _p(conv), b, h, w, n, c, int(max_iter),
+       float(lambda_init), float(cost_thresh))
     return p_new, conv.astype(bool)
 
 
@@ -127,19 +132,22 @@ def match_occlusion(X11, X21, p, conv, dist_thresh):
     return p1, valid.astype(bool)
 
 
-def match(X11, X21, D11, D21, idx_init=None, cfg=None):
-    """matching.match_iterative_proj (matching.py:52-90) restated on the CPU."""
+def match(X11, X21, D11, D21, idx_init=None, cfg=None, contract=False, stages=False):
+    """matching.match_iterative_proj (matching.py:52-90) restated on the CPU.  contract: the
+    FMA-contracted iter_proj model; stages: also return the intermediate (p, converged)."""
     cfg = cfg or dict(max_iter=10, lambda_init=1e-8, convergence_thresh=1e-6, dist_thresh=1e-1,
                       radius=3, dilation_max=5)
     b, h, w = X21.shape[:3]
     rwg, pts, p_init = prep_for_iter_proj(X11, X21, idx_init)
-    p, valid = iter_proj(rwg, pts, p_init, cfg["max_iter"], cfg["lambda_init"],
-                         cfg["convergence_thresh"])
-    p1, valid = match_occlusion(X11, X21, p, valid, cfg["dist_thresh"])
+    p, conv = iter_proj(rwg, pts, p_init, cfg["max_iter"], cfg["lambda_init"],
+                        cfg["convergence_thresh"], contract=contract)
+    p1, valid = match_occlusion(X11, X21, p, conv, cfg["dist_thresh"])
     if cfg["radius"] > 0:
         p1 = refine_matches(D11.astype(np.float16), D21.reshape(b, h * w, -1).astype(np.float16),
                             p1, cfg["radius"], cfg["dilation_max"])
     idx = p1[..., 0] + w * p1[..., 1]
+    if stages:
+        return idx, valid[..., None], p, conv
     return idx, valid[..., None]
 
 

@@ -37,12 +37,14 @@ def test_gn_rays_parity(oracle, dev, P, h, w, iters):
     np.testing.assert_allclose(dx.cpu().numpy(), ref["dx"], atol=POSE_TOL, rtol=0)
 
 
-@pytest.mark.parametrize("P", [2, 19, 20, 24])
+@pytest.mark.parametrize("P", [2, 19, 20, 21, 22, 24])
 def test_gn_rays_solve_paths(oracle, dev, P):
     """The fp64 solve runs LDS-resident (system assembled by block row in edge order,
-    Cholesky in LDS, one-wave triangular solves) while n = 7(P - 1) <= 126 and in global
-    memory beyond: both paths, at the LDS capacity edge (P = 19, n = 126) and past it, vs
-    the oracle's dense Cholesky."""
+    Cholesky in LDS, one-wave triangular solves) while n = 7(P - 1) <= 140 and in global
+    memory beyond: both paths — the round-5 edge (P = 19, n = 126: two row registers per
+    lane), rows past 128 (P = 20, 21: a third row register in the panel factor and the
+    triangular solves, the wide update's second row pass) and past the LDS capacity (P = 22,
+    24) — vs the oracle's dense Cholesky."""
     import mast3r_slam_backends as mb
     g = syn.keyframe_graph(P=P, h=24, w=32, seed=P)
     for iters in (1, 3):
@@ -67,7 +69,7 @@ def test_gn_rays_solve_paths(oracle, dev, P):
             np.testing.assert_allclose(Twc.cpu().numpy(), Twc_ref, atol=POSE_TOL, rtol=5e-5)
 
 
-@pytest.mark.parametrize("P", [2, 16, 19])
+@pytest.mark.parametrize("P", [2, 16, 19, 20, 21])
 def test_gn_lds_solve_equals_global_solve(dev, P):
     """The LDS-resident solve (block-row assembly in edge order, look-ahead LDS Cholesky,
     one-wave triangular solves) performs the global-memory solve's operations in the same order:

@@ -41,6 +41,36 @@ def test_iter_proj_ragged_tail(oracle, dev):
     np.testing.assert_array_equal(c_gpu.cpu().numpy(), c_ref)
 
 
+@pytest.mark.parametrize("b,h,w", [(1, 384, 512), (2, 224, 224), (1, 30, 41)])
+def test_iter_proj_fma_bit_exact_to_contracted_model(oracle, dev, b, h, w):
+    """m3s_iter_proj_fma (opt-in) vs the oracle's FMA-contracted model (ref_iter_proj_fma):
+    bit-exact p and converged; and end to end through match_iterative_proj with
+    cfg["iter_proj_fma"]: indices and valid masks equal the oracle's contracted match."""
+    from monst3r_slam_amd import _lib
+    from monst3r_slam_amd import matching as M
+    from monst3r_slam_amd.config import config
+    X11, X21, D11, D21 = syn.pointmap_pair_batch(b, h, w, seed=b * 7 + h)
+    rwg, pts, p_init = oracle.prep_for_iter_proj(X11, X21)
+    rng = np.random.default_rng(1)
+    p_init = (p_init + rng.uniform(-3, 3, p_init.shape)).astype(np.float32)
+    n = h * w
+    p_ref, c_ref = oracle.iter_proj(rwg, pts, p_init, 10, 1e-8, 1e-6, contract=True)
+    p = torch.empty((b, n, 2), dtype=torch.float32, device=dev)
+    conv = torch.empty((b, n), dtype=torch.uint8, device=dev)
+    rt, pt, pit = _t(rwg, dev), _t(pts, dev), _t(p_init, dev)
+    _lib.check(_lib.load().m3s_iter_proj_fma(_lib.ptr(rt), _lib.ptr(pt), _lib.ptr(pit),
+                                             _lib.ptr(p), _lib.ptr(conv), b, h, w, n, 10, 1e-8,
+                                             1e-6, _lib.stream(dev)), "iter_proj_fma")
+    np.testing.assert_array_equal(p.cpu().numpy(), p_ref)
+    np.testing.assert_array_equal(conv.cpu().numpy().astype(bool), c_ref)
+    cfg = dict(config["matching"], iter_proj_fma=True)
+    idx_ref, valid_ref = oracle.match(X11, X21, D11, D21, contract=True)
+    idx, valid = M.match_iterative_proj(_t(X11, dev), _t(X21, dev), _t(D11, dev), _t(D21, dev),
+                                        cfg=cfg)
+    np.testing.assert_array_equal(idx.cpu().numpy(), idx_ref)
+    np.testing.assert_array_equal(valid.cpu().numpy(), valid_ref)
+
+
 @pytest.mark.parametrize("b,h,w", [(1, 384, 512), (2, 96, 128), (1, 31, 37)])
 def test_refine_matches_bit_exact(oracle, dev, b, h, w):
     import mast3r_slam_backends as mb

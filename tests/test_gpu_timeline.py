@@ -32,12 +32,13 @@ def test_timeline_records_every_launch(dev):
     nlog = 1 << 16
     blog = torch.zeros((nlog, 8), dtype=torch.int64, device=dev)
     bcnt = torch.zeros(2, dtype=torch.int32, device=dev)
+    slot[:, 128:] = 7                    # garbage headers: m3s_timeline_set zeroes them
+    m.ops.record = []
+    _lib.check(lib.m3s_timeline_set(P(buf), cap), "timeline_set")
+    assert int(slot[:, 128:].abs().sum()) == 0
     slot[:, 128] = blog.data_ptr()
     slot[:, 129] = bcnt.data_ptr()
     slot[:, 130] = nlog
-    slot[:, 131] = 0
-    m.ops.record = []
-    _lib.check(lib.m3s_timeline_set(P(buf), cap), "timeline_set")
     try:
         m.pair(img, feat_j=feat_k)
         torch.cuda.synchronize()

@@ -121,3 +121,29 @@ def test_refine_f16c_path_equals_software_half(oracle, monkeypatch, flush):
     monkeypatch.setenv("ORACLE_SOFT_HALF", "0")
     fast = oracle.refine_matches(E11[None].astype(np.float16), E21.reshape(1, -1, 24), p, 3, 5)
     assert np.array_equal(soft, fast)
+
+
+def test_iter_proj_contracted_model(oracle):
+    """The FMA-contracted model (ref_iter_proj_fma): the same known
+    answers as the literal model (sub-pixel shift recovered, identity kept), and on the
+    C3-sized 384x512 field of test_match_end_to_end_bit_exact the two models' final match
+    indices differ for a few percent of the pixels (DESIGN §2 records the counts: p 105,539,
+    converged 1, idx 10,122, valid 1 of 196,608)."""
+    sx, sy = 1.5, -0.75
+    X11, X21, _, _ = syn.pair(96, 128, seed=2, shift_px=(sx, sy), noise=0.0)
+    rwg, pts, p_init = oracle.prep_for_iter_proj(X11[None], X21[None])
+    p, conv = oracle.iter_proj(rwg, pts, p_init, 10, 1e-8, 1e-6, contract=True)
+    yy, xx = np.meshgrid(np.arange(96), np.arange(128), indexing="ij")
+    inner = ((xx > 4) & (xx < 120) & (yy > 4) & (yy < 90)).reshape(-1)
+    exp = np.stack([xx + sx, yy + sy], -1).reshape(-1, 2)
+    assert np.median(np.abs(p[0, inner] - exp[inner])) < 0.05
+    assert conv[0, inner].mean() > 0.9
+    X11, X21, D11, D21 = syn.pointmap_pair_batch(1, 384, 512, seed=11)
+    i0, v0, p0, c0 = oracle.match(X11, X21, D11, D21, stages=True)
+    i1, v1, p1, c1 = oracle.match(X11, X21, D11, D21, contract=True, stages=True)
+    n = 384 * 512
+    dp = int((p0 != p1).any(-1).sum())
+    di = int((i0 != i1).sum())
+    assert 0.2 * n < dp < 0.8 * n, dp          # the low bits of p move for most pixels
+    assert 0 < di < 0.1 * n, di                 # truncation + refine: a few percent of idx
+    assert int((v0 != v1).sum()) < 0.001 * n

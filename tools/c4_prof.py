@@ -1,0 +1,20 @@
+"""Run only bench.py's configs[3] leg (keyframe graph: symmetric re-inference + matching +
+GN over the retrieval-built graph), for rocprofv3 / A-B timing.
+Usage: python tools/c4_prof.py [steps]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "monst3r-slam_amd")]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from monst3r_slam_amd import model as Mdl  # noqa: E402
+
+dev = torch.device("cuda:0")
+m, _ = Mdl.build(dev)
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+r = bench.keyframe_graph_bench(m, dev, 1, steps)
+print(json.dumps({k: r[k] for k in ("pairs", "keyframes", "pairs_per_s", "ms_per_graph",
+                                    "tflops_achieved", "gn", "valid_match_frac")}), flush=True)

@@ -57,6 +57,9 @@ def capture(fn, st, timeline=False):
     gr = torch.cuda.CUDAGraph()
     if timeline:
         _lib.check(lib.m3s_timeline_set(P(slot), cap_slots), "timeline_set")
+        slot[:, 128] = blog.data_ptr()      # the headers, zeroed by the set
+        slot[:, 129] = bcnt.data_ptr()
+        slot[:, 130] = nlog
     try:
         with torch.cuda.graph(gr, stream=st):
             fn()

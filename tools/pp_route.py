@@ -1,0 +1,87 @@
+"""Which recorded GEMM launch classes the 256x256 ping-pong kernel (T256PP, tile 15) should
+take: every launch class of the pair inference (+ the split-heads pair, the mono and
+symmetric decodes with --graph, the C5 frame's bf16 launches with --c5) is replayed back to
+back in a HIP graph under the current choice (table / heuristic) and under T256PP (unsplit),
+timed with HIP events (tools/gemm_autotune.py's method).  Prints per class, and with
+--write writes gpurun_out/gemm_table_pp.inc: the current table with the classes where T256PP
+wins by > --min-gain switched to it (copy to monst3r-slam_amd/csrc/gemm_table.inc).
+
+  python tools/pp_route.py [--graph] [--c5] [--split-heads] [--write] [--min-m 512]
+"""
+import argparse
+import json
+import os
+import re
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tools"), os.path.join(ROOT, "monst3r-slam_amd")]
+import gemm_autotune as GA  # noqa: E402
+from monst3r_slam_amd import model as Mdl  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--c5", action="store_true")
+    ap.add_argument("--split-heads", action="store_true")
+    ap.add_argument("--write", action="store_true")
+    ap.add_argument("--min-gain", type=float, default=0.03)
+    ap.add_argument("--min-m", type=int, default=0)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pp_route.json"))
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    m, _ = Mdl.build(dev)
+    for k in ("M3S_GEMM_TILE", "M3S_GEMM_SPLITS", "M3S_GEMM_FUSED"):
+        os.environ.pop(k, None)
+    groups = GA.record(m, dev, args.graph, args.split_heads, args.c5, False)
+    rows = []
+    for key, lst in groups.items():
+        M, N, K, batch, flags, mode = key
+        if M < args.min_m:
+            continue
+        base = min(GA.time_group(m, dev, lst, {}) for _ in range(2))
+        pp = min(GA.time_group(m, dev, lst, {"M3S_GEMM_TILE": 15, "M3S_GEMM_SPLITS": 1,
+                                               "M3S_GEMM_FUSED": 0}) for _ in range(2))
+        fl = sum(f for _, f in lst) / len(lst)
+        rows.append(dict(M=M, N=N, K=K, batch=batch, flags=flags, mode=mode, launches=len(lst),
+                         base_us=round(base, 2), pp_us=round(pp, 2),
+                         base_tflops=fl / base / 1e6, pp_tflops=fl / pp / 1e6))
+        print(f"{str(key):44s} n={len(lst):3d} current {base:8.2f} us ({fl / base / 1e6:6.1f} "
+              f"TF/s)  T256PP {pp:8.2f} us ({fl / pp / 1e6:6.1f} TF/s)"
+              f"{'  <- PP' if pp < (1 - args.min_gain) * base else ''}", flush=True)
+    tb = sum(r["base_us"] * r["launches"] for r in rows)
+    tp = sum(min(r["base_us"], r["pp_us"]) * r["launches"] for r in rows)
+    print(f"GEMM per recorded run: current {tb:.1f} us, with T256PP where it wins {tp:.1f} us")
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    json.dump(dict(rows=rows, total_current_us=tb, total_with_pp_us=tp), open(args.out, "w"),
+              indent=1)
+    if args.write:
+        src = os.path.join(ROOT, "monst3r-slam_amd", "csrc", "gemm_table.inc")
+        lines = open(src).read().splitlines()
+        keyre = re.compile(r"^\{(\d+), (\d+), (\d+), (\d+), (\d+), (\d+),")
+        wins = {(r["M"], r["N"], r["K"], r["batch"], r["flags"], r["mode"]): r for r in rows
+                if r["pp_us"] < (1 - args.min_gain) * r["base_us"]}
+        out, seen = [], set()
+        for ln in lines:
+            mt = keyre.match(ln)
+            k = tuple(int(v) for v in mt.groups()) if mt else None
+            if k in wins:
+                r = wins[k]
+                ln = (f"{{{k[0]}, {k[1]}, {k[2]}, {k[3]}, {k[4]}, {k[5]}, 15, 1, 0}},  // "
+                      f"{r['base_us']:.1f} -> {r['pp_us']:.1f} us (T256PP, round 6)")
+                seen.add(k)
+            out.append(ln)
+        for k, r in wins.items():
+            if k not in seen:
+                out.append(f"{{{k[0]}, {k[1]}, {k[2]}, {k[3]}, {k[4]}, {k[5]}, 15, 1, 0}},  // "
+                           f"{r['base_us']:.1f} -> {r['pp_us']:.1f} us (T256PP, round 6)")
+        path = os.path.join(os.path.dirname(args.out), "gemm_table_pp.inc")
+        open(path, "w").write("\n".join(out) + "\n")
+        print("wrote", path, len(wins), "classes to T256PP")
+
+
+if __name__ == "__main__":
+    main()
