@@ -1453,6 +1453,14 @@ int launch_pp(Args& a, int batch, hipStream_t s) {
   const dim3 grid((unsigned)(a.tiles_m * a.tiles_n * batch));
   a.splits = 1;
   set_order(a, 256, 256, batch);
+  // large grids (both tile dimensions >= 8, GEMM mode): the 32 tiles an XCD runs at once as
+  // 4 A bands x 8 B columns instead of one band x 32 columns — set_order's whole-panel
+  // model stops grouping once an XCD's share exceeds a group, but at one 256^2 block per CU
+  // what the L2 holds is the concurrent tiles' current K-slices (8192^3: 1271 -> 1486
+  // TF/s, profiles/r06_pp_bench_order.txt)
+  if (a.mode == 0 && a.group_m == 0 && a.tiles_m >= 8 && a.tiles_n >= 8 &&
+      !getenv("M3S_GEMM_ORDER"))
+    a.group_m = 4;
   const int key = (a.flags & ~(M3S_PRO_RELU | (a.bias ? 0 : M3S_EPI_BIAS)));
   bool done = false;
   if (a.vec) {
