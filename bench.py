@@ -494,6 +494,14 @@ def roofline_entry(tl, roof, pmc, mfma, step_ms):
                                    "an implicit 3x3 conv reads its input image once: M·K/9 "
                                    "for A)")
     if mfma:
+        # the PMC pass ran on the box that committed it (its own untraced step time), this
+        # line may run on another: both step times, and the utilisation at each
+        mfma = dict(mfma)
+        busy = mfma.get("mfma_busy_cycles_per_step")
+        mfma["pmc_box_step_ms"] = mfma.get("untraced_step_ms")
+        mfma["this_line_step_ms"] = step_ms
+        if busy:
+            mfma["mfma_util_at_this_line_step"] = busy / (1024.0 * 2.4e9 * step_ms * 1e-3)
         e["mfma_busy"] = mfma
         hb = (mfma.get("hbm") or {}).get("gemm")
         if hb:   # the step's own GEMM HBM bytes (PMC passes over the replayed step)
@@ -620,7 +628,7 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
         geo[3, b] = (Tgt[j].inv() * Tgt[i]).act(Xs_d[i].reshape(-1, 3)).reshape(H, W, 3)
     real_sym = model.symmetric
 
-    def sym(fi, fj, Hh, Ww, chunk=4):
+    def sym(fi, fj, Hh, Ww, chunk=None):
         out = real_sym(fi, fj, Hh, Ww, chunk=chunk)
         out["X"].copy_(geo[:, :out["X"].shape[1]])
         return out

@@ -542,6 +542,7 @@ class PairModel:
         self._wbase = 0       # first head-weight stack of that set
         self._wm = 4
         self._ev_heads = None
+        self.sym_chunk = 7    # most pairs per symmetric() launch set (8 problems each)
 
     def set_fp8(self, on=True, calibrate=True, convs=None):
         """fp8 mode: the encoder / decoder transformer GEMMs take OCP e4m3
@@ -1438,10 +1439,14 @@ class PairModel:
         return pts, conf
 
     # ---- monst3r_decode_symmetric_batch (monst3r_utils.py:141-184) ----
-    def symmetric(self, feat_i, feat_j, H, W, chunk=4):
+    def symmetric(self, feat_i, feat_j, H, W, chunk=None):
         """B keyframe pairs (i_b, j_b), both directions, both models.  feat_i/feat_j bf16
         [B,S,E].  The reference loops over b and runs 4 decoder calls + 8 heads per pair
-        sequentially; here `chunk` pairs (8 x chunk problems) go through every launch.
+        sequentially; here `chunk` pairs (8 x chunk problems) go through every launch —
+        by default the B pairs in ceil(B / 7) near-equal chunks of at most 7 (round 6: at 7
+        pairs the M = 768 decoder GEMMs' 256x256 tile grids end on nearly full waves —
+        [768,768,768,56] 504 tiles, [768,768,3072,56] 504 — where 4 pairs left 288 tiles,
+        1.1 waves).
         Returns fresh tensors in the reference's [4,B,...] order (Xii, Xji, Xjj, Xij):
         X f32 [4,B,H,W,3], C [4,B,H,W] (MonST3R), D f32 [4,B,H,W,24], D16 f16, Q [4,B,H,W]
         (MASt3R)."""
@@ -1455,8 +1460,13 @@ class PairModel:
         D = torch.empty((4, B, H, W, 24), dtype=F32, device=self.dev)
         D16 = torch.empty((4, B, H, W, 24), dtype=torch.float16, device=self.dev)
         Q = torch.empty((4, B, H, W), dtype=F32, device=self.dev)
-        for b0 in range(0, B, chunk):
-            nb = min(chunk, B - b0)
+        if chunk is None:   # ceil(B / sym_chunk) chunks, sizes differing by at most one
+            c = max(1, -(-B // self.sym_chunk))
+            sizes = [B // c + (1 if i < B % c else 0) for i in range(c)]
+        else:
+            sizes = [min(chunk, B - b0) for b0 in range(0, B, chunk)]
+        b0 = 0
+        for nb in sizes:
             # directed pairs g = b*2 + d: d = 0 → (i, j), d = 1 → (j, i)
             f1 = torch.stack([fi[b0:b0 + nb], fj[b0:b0 + nb]], 1).reshape(2 * nb, S, E)
             f2 = torch.stack([fj[b0:b0 + nb], fi[b0:b0 + nb]], 1).reshape(2 * nb, S, E)
@@ -1470,6 +1480,7 @@ class PairModel:
             D[:, b0:b0 + nb] = d32.view(nb, 4, H, W, 24).transpose(0, 1)
             D16[:, b0:b0 + nb] = d16.view(nb, 4, H, W, 24).transpose(0, 1)
             Q[:, b0:b0 + nb] = dq.view(nb, 4, H, W).transpose(0, 1)
+            b0 += nb
         return dict(X=X, C=C, D=D, D16=D16, Q=Q)
 
 

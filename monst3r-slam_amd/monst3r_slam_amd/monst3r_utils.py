@@ -361,9 +361,10 @@ def monst3r_symmetric_inference(mast3r, monst3r, frame_i, frame_j):
 
 @torch.inference_mode()
 def monst3r_decode_symmetric_batch(mast3r, monst3r, feat_i, pos_i, feat_j, pos_j, shape_i,
-                                   shape_j, chunk=4):
+                                   shape_j, chunk=None):
     """:141-184 ("Assumes img shape the same") → X, C, D, Q [4,B,H,W(,c)].  The reference
-    loops over b; here `chunk` pairs = 8·chunk decoder/head problems share every launch."""
+    loops over b; here `chunk` pairs = 8·chunk decoder/head problems share every launch
+    (None: PairModel.symmetric's near-equal chunks of at most `sym_chunk` pairs)."""
     pm = monst3r.pair_model()
     H, W = _hw(shape_i[0])
     out = pm.symmetric(feat_i.to(Mdl.BF16), feat_j.to(Mdl.BF16), H, W, chunk=chunk)

@@ -52,9 +52,12 @@ def small(dev):
     return m, g
 
 
-@pytest.mark.parametrize("chunk", [2, 4])
-def test_symmetric_batch_vs_reference_goldens(small, chunk):
+@pytest.mark.parametrize("chunk,sym_chunk", [(2, 7), (4, 7), (None, 7), (None, 2)])
+def test_symmetric_batch_vs_reference_goldens(small, chunk, sym_chunk):
+    """chunk None: PairModel.symmetric's near-equal chunks of at most sym_chunk pairs
+    (B = 3: one chunk of 3; sym_chunk 2: chunks of 2 + 1)."""
     m, g = small
+    m.sym_chunk = sym_chunk
     H, W = g["imgs"].shape[-2:]
     feats = [m.encode(g["imgs"][k])[0].clone() for k in range(g["imgs"].shape[0])]
     pi = [int(p[0]) for p in g["pairs"]]

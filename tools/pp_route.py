@@ -31,12 +31,32 @@ def main():
     ap.add_argument("--min-gain", type=float, default=0.03)
     ap.add_argument("--min-m", type=int, default=0)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pp_route.json"))
+    ap.add_argument("--sym-pairs", type=lambda v: [int(x) for x in v.split(",") if x],
+                    default=[], help="also symmetric decodes of these pair counts (one chunk)")
+    ap.add_argument("--encode-batch", type=int, default=0, help="also a batched encode")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     m, _ = Mdl.build(dev)
     for k in ("M3S_GEMM_TILE", "M3S_GEMM_SPLITS", "M3S_GEMM_FUSED"):
         os.environ.pop(k, None)
     groups = GA.record(m, dev, args.graph, args.split_heads, args.c5, False)
+    # extra launch classes: symmetric decodes of other chunk sizes (the keyframe graph's
+    # near-equal chunks) and a batched keyframe encode (the C4 leg's shard_keyframe_features)
+    extra = []
+    img = torch.rand(1, 3, 384, 512, device=dev) * 2 - 1
+    feat = m.encode(img)[0].clone()
+    m.ops.record = []
+    for nb in args.sym_pairs:
+        f = feat.expand(nb, -1, -1).contiguous()
+        m.symmetric(f, f, 384, 512, chunk=nb)
+    if args.encode_batch:
+        m.encode(torch.rand(args.encode_batch, 3, 384, 512, device=dev) * 2 - 1)
+    torch.cuda.synchronize()
+    extra, m.ops.record = m.ops.record, None
+    for d, fl, f8 in extra:
+        if f8:
+            continue
+        groups.setdefault((d.M, d.N, d.K, d.batch, d.flags, d.mode), []).append((d, fl))
     rows = []
     for key, lst in groups.items():
         M, N, K, batch, flags, mode = key
