@@ -1103,8 +1103,15 @@ def main():
                         ms_per_frame=el200 / SEQ_FRAMES * 1e3)
         tl = None if (args.eager or args.no_timeline) else step_timeline(
             loop, dev, out_path=args.timeline_out)
-        g_pair = None if args.eager else capture(
-            lambda: model.pair(loop.img_cur, feat_j=tr.kf.feat), dev)
+        # C2 (configs[1]): one pair inference — frame encoder, both decoders (one chain per
+        # model), all four DPT heads and the local features — with the MASt3R heads on a
+        # side stream beside the MonST3R heads (split_heads) and joined before the graph
+        # ends: every output of the serial pair, computed concurrently
+        def c2_pair():
+            model.pair(loop.img_cur, feat_j=tr.kf.feat, split_heads=True)
+            model.join()
+
+        g_pair = None if args.eager else capture(c2_pair, dev)
         pair_ms = time_replays(g_pair, dev, 20) if g_pair else None
         del g_pair
         res = loop.step(0)                       # eager: buffers of one frame for the rooflines

@@ -37,7 +37,13 @@ def record(m, dev, graph, split_heads=False, c5=False, fp8=False):
     if split_heads:  # the C3 step's head launches (MonST3R / MASt3R heads as two batch-2 sets)
         m.pair(img, feat_j=feat, split_heads=True)
     if c5:  # the configs[4] 512x512 frame's bf16 launches (heads) beside its fp8 ViT
+        # (set_fp8 calibrates on two frames through scratch buffers it frees afterwards: its
+        # launches are not recorded — replaying their descriptors would touch freed memory;
+        # round 6: a recorded calibration conv replayed after the scratch was released
+        # faulted with an illegal address)
+        rec, m.ops.record = m.ops.record, None
         m.set_fp8(True)
+        m.ops.record = rec
         img5 = torch.rand(1, 3, 512, 512, device=dev) * 2 - 1
         f5 = m.encode(img5)[0].clone()
         feat_i, pos = m.encode(img5)

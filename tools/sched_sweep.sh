@@ -12,5 +12,5 @@ for spec in "$@"; do
   env "${envs[@]}" timeout -k 10 150 python -u bench.py --no-graph --no-c5 --no-retrieval \
       --no-cpu-baseline --no-timeline --steps 200 "${flags[@]}" \
       > gpurun_out/sched_sweep.json 2> gpurun_out/sched_sweep.err || { tail -20 gpurun_out/sched_sweep.err; exit 1; }
-  python -c "import json;d=json.loads(open('gpurun_out/sched_sweep.json').read().strip().splitlines()[-1]);print(repr('$spec'), round(d['value'],1), 'fps', round(d['ms_per_step'],3), 'ms')"
+  python -c "import json;d=json.loads(open('gpurun_out/sched_sweep.json').read().strip().splitlines()[-1]);print(repr('$spec'), round(d['value'],1), 'fps', round(d['ms_per_step'],3), 'ms', 'pair', round(d['pair_inference_ms'] or 0,3), 'ms')"
 done
