@@ -54,6 +54,9 @@ extern template int launch<256, 256, 64, 2, 4, 2, 1>(Args&, int, hipStream_t);
 extern template int launch_pp<0>(Args&, int, hipStream_t);
 extern template int launch_pp<1>(Args&, int, hipStream_t);
 extern template int launch_pp<2>(Args&, int, hipStream_t);
+extern template int launch_pp<0, 192>(Args&, int, hipStream_t);
+extern template int launch_pp<1, 192>(Args&, int, hipStream_t);
+extern template int launch_pp<2, 192>(Args&, int, hipStream_t);
 }  // namespace m3s_gemm
 #endif
 
@@ -260,7 +263,7 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     // (96-row tiles, 768 tokens = 8 bands, measured faster launch by launch but slower in
     // the pipelined step: 182 vs 184.6 frames/s, DESIGN §2 — reachable by tile hint only)
   }
-  if (cfg < 1 || cfg > 15 || cfg == 4 || cfg == 5) cfg = T128;
+  if (cfg < 1 || cfg > 16 || cfg == 4 || cfg == 5) cfg = T128;
   if (conv && (cfg == T64D || cfg == T128D)) cfg = T64;
   if (conv && d->Cin % 64 != 0) cfg = T128K32;  // tap-uniform K-tiles need Cin % BK == 0
   if (!conv && cfg == T128K32) cfg = T128;
@@ -282,7 +285,8 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   // fused split-K: 128^2 GEMM tiles or 64x128 GEMM / conv tiles, a workspace for the f32
   // partials and one zeroed counter per (batch, tile)
   const int bm = (cfg == T64 || cfg == T64D) ? 64
-                 : (cfg == T256 || cfg == T256W8 || cfg == T256SQ || cfg == T256PP) ? 256 : 128;
+                 : (cfg == T256 || cfg == T256W8 || cfg == T256SQ || cfg == T256PP) ? 256
+                 : cfg == T192PP ? 192 : 128;
   const int64_t tiles_cfg = (int64_t)((d->M + bm - 1) / bm) * ((d->N + 127) / 128) * d->batch;
   const bool split_cfg = (!conv && (cfg == T128 || cfg == T128O2 || cfg == T64 || cfg == T64D ||
                                     cfg == T128D || cfg == T128W8 || cfg == T256 ||
@@ -334,6 +338,13 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
         return launch<256, 128, 64, 4, 2, 3, 1>(a, d->batch, s);
       if (!conv) return launch_pp<0>(a, d->batch, s);
       return (d->flags & M3S_PRO_RELU) ? launch_pp<2>(a, d->batch, s) : launch_pp<1>(a, d->batch, s);
+    // 192x256 ping-pong: the grids a 256-row tile leaves on a partial wave (same fallbacks)
+    case T192PP:
+      if (a.splits > 1 || (d->flags & (M3S_EPI_DPT_OUT | M3S_EPI_CONVT | M3S_EPI_OUT_FP8)))
+        return launch<256, 128, 64, 4, 2, 3, 1>(a, d->batch, s);
+      if (!conv) return launch_pp<0, 192>(a, d->batch, s);
+      return (d->flags & M3S_PRO_RELU) ? launch_pp<2, 192>(a, d->batch, s)
+                                       : launch_pp<1, 192>(a, d->batch, s);
     default: return launch<64, 128, 64, 2, 2, 3, 2>(a, d->batch, s);
   }
 }

@@ -1238,14 +1238,25 @@ inline void set_order(Args& a, int BM, int BN, int64_t groups) {
 // Implicit conv (MODE 1 / 2) as gemm_kernel: the tap and channel offset are block-uniform
 // per K-tile (Cin % 64 == 0), ReLU (MODE 2) on the A fragments.  Unsplit; the epilogue is
 // gemm_epilogue's, in two 128-row passes (QM = 0, then 1).
-template <int MODE, int EPI>
+// BM = 192 (T192PP, round 6): the same schedule on 192 x 256 tiles — A half-tiles of 96
+// rows (each wave group's share 48 rows = 3 MFMA row tiles); a half-tile still takes two
+// 16-B DMA chunks per thread (the vmcnt counts assume it): the 256 chunks past row 96 go
+// to a 4-KB junk area with out-of-range offsets (zeros, no memory read).  For grids that a
+// 256-row tile leaves on a partial wave (M = 768: 4 row tiles instead of 3).
+template <int MODE, int EPI, int BM = 256>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(Args a) {
-  constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
-  constexpr int HB = 128 * BK * 2;       // half-tile bytes
-  constexpr int BUFB = 4 * HB;           // one K-tile
+  static_assert(BM == 256 || BM == 192, "T256PP / T192PP");
+  constexpr int BN = 256, BK = 64, NT = 512;
+  constexpr int HA = BM / 2;             // A half-tile rows
+  constexpr int FA = HA / 32;            // 16-row MFMA tiles per wave group per half
+  constexpr int HBA = HA * BK * 2;       // A half-tile bytes
+  constexpr int HB = 128 * BK * 2;       // B half-tile bytes
+  constexpr int SOFF[4] = {0, HBA, 2 * HBA, 2 * HBA + HB};   // slots A0 A1 B0 B1
+  constexpr int BUFB = 2 * HBA + 2 * HB; // one K-tile
   constexpr int RING = 2 * BUFB;
-  constexpr int EPIB = 128 * (BN + 4) * 4;
-  constexpr int LDS_BYTES = EPIB > RING ? EPIB : RING;
+  constexpr int JUNK = HA == 128 ? 0 : 4 * 1024;
+  constexpr int EPIB = HA * (BN + 4) * 4;
+  constexpr int LDS_BYTES = EPIB > RING + JUNK ? EPIB : RING + JUNK;
   static_assert(EPI < 0 || (EPI & (M3S_EPI_DPT_OUT | M3S_EPI_OUT_FP8)) == 0, "not on T256PP");
   m3s_tl_begin(a.tl);
   M3sTlEnd tl_end{a.tl};
@@ -1278,9 +1289,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(Args a) {
     kc[i] = (p ^ ((r >> 1) & 7)) * 8;
 #pragma unroll
     for (int h = 0; h < 4; h++) {
-      const int row = (h & 1) * 128 + r;
+      const int row = (h & 1) * (h < 2 ? HA : 128) + r;
       if (h < 2) {
-        const int m = m0 + row;
+        const int m = r < HA ? m0 + row : a.M;   // chunks past the A half-tile: junk
         if (MODE == 0) {
           off[h][i] = m < a.M ? (uint32_t)(((int64_t)m * a.lda + kc[i]) * 2) : OOB;
         } else {
@@ -1298,7 +1309,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(Args a) {
   const int nk = (a.K + BK - 1) / BK;
   // half-tile h of K-tile t into its slot of buffer t & 1
   auto issue = [&](int t, int h) {
-    char* dst = lds + (t & 1) * BUFB + h * HB + wid * 64 * 16;
+    char* dst = lds + (t & 1) * BUFB + SOFF[h] + wid * 64 * 16;
     const int k0 = t * BK;
     int ky = 0, kx = 0, ci0 = 0;
     if (MODE != 0 && h < 2) {
@@ -1317,7 +1328,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(Args a) {
       } else {
         vo = (k0 + kc[i] < a.K) ? off[h][i] + (uint32_t)k0 * 2 : OOB;
       }
-      glds16(h < 2 ? rA : rB, dst + i * NT * 16, vo);
+      // (T192PP: waves 4-7's second A chunk lands in the junk area, out of range)
+      char* d = (JUNK && h < 2 && i == 1 && wid >= 4) ? lds + RING + (wid - 4) * 64 * 16
+                                                      : dst + i * NT * 16;
+      if (JUNK && h < 2 && i == 1 && wid >= 4) vo = OOB;
+      glds16(h < 2 ? rA : rB, d, vo);
     }
   };
 
@@ -1326,20 +1341,20 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(Args a) {
   const int fr = lane & 15, fc = lane >> 4, sw = fr >> 1;
   const int lo0 = fr * 128 + ((fc ^ sw) << 4);
   const int lo1 = fr * 128 + (((fc ^ sw) ^ 4) << 4);
-  bf16x8 af[4][2], bfr[2][2];
-  f32x4 acc[2][2][4][2];
+  bf16x8 af[FA][2], bfr[2][2];
+  f32x4 acc[2][2][FA][2];
 #pragma unroll
   for (int x = 0; x < 2; x++)
 #pragma unroll
     for (int y = 0; y < 2; y++)
 #pragma unroll
-      for (int i = 0; i < 4; i++)
+      for (int i = 0; i < FA; i++)
 #pragma unroll
         for (int j = 0; j < 2; j++) acc[x][y][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto read_a = [&](const char* slot) {
-    const char* base = slot + wr * 64 * 128;
+    const char* base = slot + wr * (HA / 2) * 128;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < FA; i++) {
       af[i][0] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + lo0);
       af[i][1] = *reinterpret_cast<const bf16x8*>(base + i * 16 * 128 + lo1);
       if (MODE == 2) {
@@ -1356,11 +1371,11 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(Args a) {
       bfr[j][1] = *reinterpret_cast<const bf16x8*>(base + j * 16 * 128 + lo1);
     }
   };
-  auto mfmas = [&](f32x4 (&c)[4][2]) {
+  auto mfmas = [&](f32x4 (&c)[FA][2]) {
 #pragma unroll
     for (int s = 0; s < 2; s++)
 #pragma unroll
-      for (int i = 0; i < 4; i++)
+      for (int i = 0; i < FA; i++)
 #pragma unroll
         for (int j = 0; j < 2; j++)
           c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], c[i][j], 0, 0, 0);
@@ -1396,17 +1411,17 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(Args a) {
   int t = 0;
   for (; t < nk - 1; t++) {
     const char* cur = lds + (t & 1) * BUFB;
-    M3S_PP_PHASE((read_a(cur), read_b(cur + 2 * HB)), issue(t + 1, 0), 4, 0, 0)
-    M3S_PP_PHASE(read_b(cur + 3 * HB), issue(t + 1, 2), 4, 0, 1)
-    M3S_PP_PHASE(read_a(cur + HB), issue(t + 1, 3), 4, 1, 1)
-    M3S_PP_PHASE(read_b(cur + 2 * HB), issue(t + 1, 1), 4, 1, 0)
+    M3S_PP_PHASE((read_a(cur), read_b(cur + SOFF[2])), issue(t + 1, 0), 4, 0, 0)
+    M3S_PP_PHASE(read_b(cur + SOFF[3]), issue(t + 1, 2), 4, 0, 1)
+    M3S_PP_PHASE(read_a(cur + SOFF[1]), issue(t + 1, 3), 4, 1, 1)
+    M3S_PP_PHASE(read_b(cur + SOFF[2]), issue(t + 1, 1), 4, 1, 0)
   }
   if (nk > 0) {   // the last K-tile: nothing to issue (phase 0 retires B1, phase 1 A1)
     const char* cur = lds + (t & 1) * BUFB;
-    M3S_PP_PHASE((read_a(cur), read_b(cur + 2 * HB)), (void)0, 2, 0, 0)
-    M3S_PP_PHASE(read_b(cur + 3 * HB), (void)0, 0, 0, 1)
-    M3S_PP_PHASE(read_a(cur + HB), (void)0, 0, 1, 1)
-    M3S_PP_PHASE(read_b(cur + 2 * HB), (void)0, 0, 1, 0)
+    M3S_PP_PHASE((read_a(cur), read_b(cur + SOFF[2])), (void)0, 2, 0, 0)
+    M3S_PP_PHASE(read_b(cur + SOFF[3]), (void)0, 0, 0, 1)
+    M3S_PP_PHASE(read_a(cur + SOFF[1]), (void)0, 0, 1, 1)
+    M3S_PP_PHASE(read_b(cur + SOFF[2]), (void)0, 0, 1, 0)
   }
 #undef M3S_PP_PHASE
   if (wr == 1) __builtin_amdgcn_s_setprio(0);
@@ -1418,26 +1433,26 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(Args a) {
 #pragma unroll
         for (int qn = 0; qn < 2; qn++)
 #pragma unroll
-          for (int i = 0; i < 4; i++)
+          for (int i = 0; i < FA; i++)
 #pragma unroll
             for (int j = 0; j < 2; j++)
 #pragma unroll
               for (int r = 0; r < 4; r++) {
-                const int row = wr * 64 + i * 16 + fc * 4 + r;
+                const int row = wr * (HA / 2) + i * 16 + fc * 4 + r;
                 const int col = qn * 128 + wc * 32 + j * 16 + fr;
                 cs[row * (BN + 4) + col] = pass == 0 ? acc[0][qn][i][j][r] : acc[1][qn][i][j][r];
               }
       });
 }
 
-template <int MODE, int E>
+template <int MODE, int E, int BM>
 bool try_epi_pp(Args& a, dim3 grid, hipStream_t s, int key, bool biased_only = false) {
   if (key == E && !biased_only) {
-    hipLaunchKernelGGL((gemm_pp_kernel<MODE, E>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((gemm_pp_kernel<MODE, E, BM>), grid, dim3(512), 0, s, a);
     return true;
   }
   if (key == (E | M3S_EPI_BIAS)) {
-    hipLaunchKernelGGL((gemm_pp_kernel<MODE, E | M3S_EPI_BIAS>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((gemm_pp_kernel<MODE, E | M3S_EPI_BIAS, BM>), grid, dim3(512), 0, s, a);
     return true;
   }
   return false;
@@ -1445,14 +1460,14 @@ bool try_epi_pp(Args& a, dim3 grid, hipStream_t s, int key, bool biased_only = f
 
 // T256PP launcher (unsplit): the epilogue sets of launch_main as straight-line variants,
 // the run-time-flag epilogue otherwise
-template <int MODE>
+template <int MODE, int BM = 256>
 int launch_pp(Args& a, int batch, hipStream_t s) {
-  a.tiles_m = (a.M + 255) / 256;
+  a.tiles_m = (a.M + BM - 1) / BM;
   a.tiles_n = (a.N + 255) / 256;
   if ((int64_t)a.tiles_m * a.tiles_n * batch >= (1ll << 31)) return M3S_ERR_TOO_LARGE;
   const dim3 grid((unsigned)(a.tiles_m * a.tiles_n * batch));
   a.splits = 1;
-  set_order(a, 256, 256, batch);
+  set_order(a, BM, 256, batch);
   // large grids (both tile dimensions >= 8, GEMM mode): the 32 tiles an XCD runs at once as
   // 4 A bands x 8 B columns instead of one band x 32 columns — set_order's whole-panel
   // model stops grouping once an XCD's share exceeds a group, but at one 256^2 block per CU
@@ -1466,21 +1481,22 @@ int launch_pp(Args& a, int batch, hipStream_t s) {
   if (a.vec) {
     if constexpr (MODE == 0) {
       constexpr int LF = M3S_EPI_LN_FOLD, LS = M3S_EPI_LN_STATS;
-      done = try_epi_pp<0, 0>(a, grid, s, key) || try_epi_pp<0, M3S_EPI_ROPE>(a, grid, s, key) ||
-             try_epi_pp<0, M3S_EPI_GELU>(a, grid, s, key) ||
-             try_epi_pp<0, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32>(a, grid, s, key) ||
-             try_epi_pp<0, M3S_EPI_OUT_F32>(a, grid, s, key) ||
-             try_epi_pp<0, LF | M3S_EPI_ROPE>(a, grid, s, key, true) ||
-             try_epi_pp<0, LF | M3S_EPI_GELU>(a, grid, s, key, true) ||
-             try_epi_pp<0, LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32>(a, grid, s, key, true) ||
-             try_epi_pp<0, LS | M3S_EPI_OUT_F32>(a, grid, s, key, true);
+      done = try_epi_pp<0, 0, BM>(a, grid, s, key) ||
+             try_epi_pp<0, M3S_EPI_ROPE, BM>(a, grid, s, key) ||
+             try_epi_pp<0, M3S_EPI_GELU, BM>(a, grid, s, key) ||
+             try_epi_pp<0, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, BM>(a, grid, s, key) ||
+             try_epi_pp<0, M3S_EPI_OUT_F32, BM>(a, grid, s, key) ||
+             try_epi_pp<0, LF | M3S_EPI_ROPE, BM>(a, grid, s, key, true) ||
+             try_epi_pp<0, LF | M3S_EPI_GELU, BM>(a, grid, s, key, true) ||
+             try_epi_pp<0, LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, BM>(a, grid, s, key, true) ||
+             try_epi_pp<0, LS | M3S_EPI_OUT_F32, BM>(a, grid, s, key, true);
     } else {
-      done = try_epi_pp<MODE, 0>(a, grid, s, key) ||
-             try_epi_pp<MODE, M3S_EPI_RES_BF16>(a, grid, s, key) ||
-             try_epi_pp<MODE, M3S_EPI_RELU>(a, grid, s, key);
+      done = try_epi_pp<MODE, 0, BM>(a, grid, s, key) ||
+             try_epi_pp<MODE, M3S_EPI_RES_BF16, BM>(a, grid, s, key) ||
+             try_epi_pp<MODE, M3S_EPI_RELU, BM>(a, grid, s, key);
     }
   }
-  if (!done) hipLaunchKernelGGL((gemm_pp_kernel<MODE, -1>), grid, dim3(512), 0, s, a);
+  if (!done) hipLaunchKernelGGL((gemm_pp_kernel<MODE, -1, BM>), grid, dim3(512), 0, s, a);
   M3S_LAUNCH_CHECK();
   return M3S_OK;
 }
@@ -1507,9 +1523,10 @@ int launch_pp(Args& a, int batch, hipStream_t s) {
 // cycles ≈ 0.5, the shape of cdna_hip_programming.md §5's 256² template — the most MFMA
 // work per staged byte, for launches that can spend fewer CUs (large-M convs, the local-
 // feature MLP, GEMMs sharing the chip with other chains)
-// T256PP: 256x256, the 8-wave ping-pong kernel above (round 6)
+// T256PP: 256x256, the 8-wave ping-pong kernel above (round 6); T192PP: its 192x256 form
 enum TileCfg { T128 = 1, T64 = 2, T128K32 = 3, T256 = 6, T128O2 = 7, T96 = 8, T96O2 = 9,
-               T64D = 10, T128D = 11, T128W8 = 12, T256W8 = 13, T256SQ = 14, T256PP = 15 };
+               T64D = 10, T128D = 11, T128W8 = 12, T256W8 = 13, T256SQ = 14, T256PP = 15,
+               T192PP = 16 };
 
 // Epilogue flag sets compiled as straight-line variants (8-wide vector path), per mode:
 //   GEMM: bf16 out, +RoPE, +GELU, f32 residual → f32, f32 out;  conv: bf16 out, +bf16

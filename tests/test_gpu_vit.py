@@ -76,7 +76,7 @@ def test_gemm_rope_epilogue(ops, dev, split_k):
     assert _rel(out, ref.reshape(B * S, 3 * C)) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [None, 14, 15])
+@pytest.mark.parametrize("tile", [None, 14, 15, 16])
 @pytest.mark.parametrize("H,W,cin,cout,stride,relu_in,res", [
     (24, 32, 256, 256, 1, True, True), (12, 16, 768, 768, 2, False, False),
     (96, 128, 96, 256, 1, False, False), (7, 9, 64, 32, 1, True, False),
@@ -798,7 +798,7 @@ def _ln_stats_ref(x):
 
 @pytest.mark.parametrize("M,N,K,batch,split_k", [(768, 768, 3072, 4, 1), (768, 1024, 1024, 1, 2),
                                                  (768, 1024, 4096, 1, 0), (200, 256, 96, 2, 1)])
-@pytest.mark.parametrize("tile", [None, 12, 13, 14, 15])
+@pytest.mark.parametrize("tile", [None, 12, 13, 14, 15, 16])
 def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k, tile):
     """LN_STATS: the residual GEMM also stores bf16(x) and per-128-column (mean, M2) of the
     stored f32 rows — in the main epilogue and in the split-K reduce (split_k 2 / auto);
@@ -828,7 +828,7 @@ def test_gemm_ln_stats_producer(ops, dev, M, N, K, batch, split_k, tile):
                                                   (768, 4096, 1024, 1, 0, "gelu"),
                                                   (200, 384, 256, 2, 1, "none")])
 @pytest.mark.parametrize("split", ["0", "3"])
-@pytest.mark.parametrize("tile", ["0", "12", "13", "14", "15"])
+@pytest.mark.parametrize("tile", ["0", "12", "13", "14", "15", "16"])
 def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi, split, tile):
     """LN_FOLD: LN(x) Wᵀ + b computed as rstd (bf16(x) (W∘γ)ᵀ − mean c1) + c2 from the
     producer's statistics, vs torch fp32 LayerNorm → Linear (→ RoPE / GELU) on x of
@@ -878,7 +878,7 @@ def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi,
     assert _rel(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 @pytest.mark.parametrize("epi", ["gelu", "res", "tail"])
 def test_gemm_every_tile_config(ops, dev, monkeypatch, tile, epi):
     """Every tile configuration (M3S_GEMM_TILE override) on a 768-row problem, straight-
@@ -911,14 +911,17 @@ def test_gemm_every_tile_config(ops, dev, monkeypatch, tile, epi):
     (4096, 4096, 4096, 1, 0, "bf16"), (6144, 3072, 768, 4, 0, "gelu"),
     (768, 6400, 7168, 2, 0, "f32"), (1536, 2304, 1024, 8, 4, "bias"),
     (300, 520, 72, 3, 0, "relu"), (256, 256, 64, 1, 0, "bf16"), (257, 264, 40, 2, 2, "res")])
-def test_gemm_pingpong_t256pp(ops, dev, monkeypatch, M, N, K, batch, wmod, epi):
-    """T256PP (M3S_GEMM_TILE=15): the 256x256 8-wave ping-pong kernel against torch fp32 on
+@pytest.mark.parametrize("tile", ["15", "16"])
+def test_gemm_pingpong_t256pp(ops, dev, monkeypatch, M, N, K, batch, wmod, epi, tile):
+    """T256PP (M3S_GEMM_TILE=15): the 256x256 8-wave ping-pong kernel — and T192PP (16), its
+    192x256 form (96-row A half-tiles, a junk area for the DMA chunks past them) — against
+    torch fp32 on
     the shapes it is routed to (4096³, the restacked keyframe-graph projections, the
     local-feature fc2) and on edges: a weight stack shared by batch g % wmod, ragged M / N,
     K tails (K % 64 ≠ 0), one K-tile (K ≤ 64), the run-time-flag epilogue (ReLU, no
     straight-line variant), bias-less bf16 output, f32 out + f32 residual."""
     from monst3r_slam_amd import _lib
-    monkeypatch.setenv("M3S_GEMM_TILE", "15")
+    monkeypatch.setenv("M3S_GEMM_TILE", tile)
     g = torch.Generator(device=dev).manual_seed(M + N + K)
     A = (torch.rand(batch, M, K, device=dev, generator=g) * 2 - 1).bfloat16()
     nw = wmod if wmod else batch

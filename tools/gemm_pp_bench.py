@@ -32,7 +32,7 @@ shapes = [(4096, 4096, 4096, 1), (8192, 8192, 8192, 1), (768, 6400, 7168, 2),
           (6144, 3840, 768, 4), (6144, 768, 768, 4)]
 if len(sys.argv) > 1:
     shapes = [tuple(int(v) for v in a.split("x")) for a in sys.argv[1:]]
-cfgs = [("table", None), ("T256SQ", "14"), ("T256PP", "15")]
+cfgs = [("table", None), ("T256SQ", "14"), ("T256PP", "15"), ("T192PP", "16")]
 ORDERS = [o for o in os.environ.get("PP_ORDERS", "").split(",") if o]   # e.g. -4,-8,0
 for o in ORDERS:
     cfgs.append((f"T256PP/o{o}", "15:" + o))

@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--sym-pairs", type=lambda v: [int(x) for x in v.split(",") if x],
                     default=[], help="also symmetric decodes of these pair counts (one chunk)")
     ap.add_argument("--encode-batch", type=int, default=0, help="also a batched encode")
+    ap.add_argument("--t192", action="store_true", help="also try T192PP (tile 16)")
+    ap.add_argument("--only-batch", type=lambda v: [int(x) for x in v.split(",") if x],
+                    default=[], help="only launch classes of these batch sizes")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     m, _ = Mdl.build(dev)
@@ -60,17 +63,24 @@ def main():
     rows = []
     for key, lst in groups.items():
         M, N, K, batch, flags, mode = key
-        if M < args.min_m:
+        if M < args.min_m or (args.only_batch and batch not in args.only_batch):
             continue
         base = min(GA.time_group(m, dev, lst, {}) for _ in range(2))
-        pp = min(GA.time_group(m, dev, lst, {"M3S_GEMM_TILE": 15, "M3S_GEMM_SPLITS": 1,
-                                               "M3S_GEMM_FUSED": 0}) for _ in range(2))
+        # the ping-pong tiles: T256PP (15) and, with --t192, T192PP (16)
+        best_pp, pp_cfg = None, 15
+        for cfg in ([15, 16] if args.t192 else [15]):
+            t = min(GA.time_group(m, dev, lst, {"M3S_GEMM_TILE": cfg, "M3S_GEMM_SPLITS": 1,
+                                                "M3S_GEMM_FUSED": 0}) for _ in range(2))
+            if best_pp is None or t < best_pp:
+                best_pp, pp_cfg = t, cfg
+        pp = best_pp
         fl = sum(f for _, f in lst) / len(lst)
         rows.append(dict(M=M, N=N, K=K, batch=batch, flags=flags, mode=mode, launches=len(lst),
-                         base_us=round(base, 2), pp_us=round(pp, 2),
+                         base_us=round(base, 2), pp_us=round(pp, 2), pp_cfg=pp_cfg,
                          base_tflops=fl / base / 1e6, pp_tflops=fl / pp / 1e6))
+        name = "T256PP" if pp_cfg == 15 else "T192PP"
         print(f"{str(key):44s} n={len(lst):3d} current {base:8.2f} us ({fl / base / 1e6:6.1f} "
-              f"TF/s)  T256PP {pp:8.2f} us ({fl / pp / 1e6:6.1f} TF/s)"
+              f"TF/s)  {name} {pp:8.2f} us ({fl / pp / 1e6:6.1f} TF/s)"
               f"{'  <- PP' if pp < (1 - args.min_gain) * base else ''}", flush=True)
     tb = sum(r["base_us"] * r["launches"] for r in rows)
     tp = sum(min(r["base_us"], r["pp_us"]) * r["launches"] for r in rows)
@@ -90,14 +100,16 @@ def main():
             k = tuple(int(v) for v in mt.groups()) if mt else None
             if k in wins:
                 r = wins[k]
-                ln = (f"{{{k[0]}, {k[1]}, {k[2]}, {k[3]}, {k[4]}, {k[5]}, 15, 1, 0}},  // "
-                      f"{r['base_us']:.1f} -> {r['pp_us']:.1f} us (T256PP, round 6)")
+                ln = (f"{{{k[0]}, {k[1]}, {k[2]}, {k[3]}, {k[4]}, {k[5]}, {r['pp_cfg']}, 1, 0}},  "
+                      f"// {r['base_us']:.1f} -> {r['pp_us']:.1f} us "
+                      f"({'T256PP' if r['pp_cfg'] == 15 else 'T192PP'}, round 6)")
                 seen.add(k)
             out.append(ln)
         for k, r in wins.items():
             if k not in seen:
-                out.append(f"{{{k[0]}, {k[1]}, {k[2]}, {k[3]}, {k[4]}, {k[5]}, 15, 1, 0}},  // "
-                           f"{r['base_us']:.1f} -> {r['pp_us']:.1f} us (T256PP, round 6)")
+                out.append(f"{{{k[0]}, {k[1]}, {k[2]}, {k[3]}, {k[4]}, {k[5]}, {r['pp_cfg']}, 1, "
+                           f"0}},  // {r['base_us']:.1f} -> {r['pp_us']:.1f} us "
+                           f"({'T256PP' if r['pp_cfg'] == 15 else 'T192PP'}, round 6)")
         path = os.path.join(os.path.dirname(args.out), "gemm_table_pp.inc")
         open(path, "w").write("\n".join(out) + "\n")
         print("wrote", path, len(wins), "classes to T256PP")
