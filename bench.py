@@ -715,14 +715,16 @@ def keyframe_graph_bench(model, dev, world, steps, warmup=1):
                         f"({P.keyframe_record_bytes(n) / 1e6:.1f} MB)"}
 
 
-def c5_bench(model, dev, steps, modes=("fp8", "fp8_convs", "bf16")):
+def c5_bench(model, dev, steps, modes=("fp8", "fp8_convs", "bf16", "fp8_unfolded")):
     """configs[4], one GPU: the per-frame inference of dynamic-mask tracking
     at 512x512 with the fp8 transformer path — MonST3R encoder (new frame), MonST3R-only
     mono decode + both heads (depth for the ego flow), ego flow + flow-error mask (the RAFT
     flow is an input: synthetic here, RAFT is absent code), MonST3R+MASt3R pair decode + 4
     heads + local features vs the cached keyframe, apply_dynamic_mask on C/Q/D.  Graph
-    captured; timed for fp8 and for the bf16 path on the same inputs.  Multi-GPU: frames
-    are sequential per sequence → replicas (the 1→8 curve is the replica sweep)."""
+    captured; timed for fp8 and for the bf16 path on the same inputs (and fp8 with the
+    round-5 separate e4m3 LayerNorm launches instead of the fold: fp8_unfolded).
+    Multi-GPU: frames are sequential per sequence → replicas (the 1→8 curve is the replica
+    sweep)."""
     from monst3r_slam_amd import monst3r_utils as U
     from monst3r_slam_amd import synthetic as syn
     H5 = W5 = 512
@@ -737,6 +739,7 @@ def c5_bench(model, dev, steps, modes=("fp8", "fp8_convs", "bf16")):
     res = {}
     for mode in modes:
         model.set_fp8(mode != "bf16", convs=mode == "fp8_convs")
+        model.fp8_fold = mode != "fp8_unfolded"
         feat_k = model.encode(img_k)[0].clone()
 
         def step():
@@ -762,17 +765,22 @@ def c5_bench(model, dev, steps, modes=("fp8", "fp8_convs", "bf16")):
         torch.cuda.synchronize(dev)
         gph = capture(step, dev)
         res[mode] = time_replays(gph, dev, steps)
-        if mode == "fp8" and len(modes) == 3:
+        if mode == "fp8" and "fp8_convs" in modes and "bf16" in modes:
             rep = gemm_replay(model, step, dev)
         del gph
     model.set_fp8(False, convs=False)
-    if len(res) < 3:                  # a subset of the modes (tools/c5_prof.py)
+    model.fp8_fold = True
+    if not all(k in res for k in ("fp8", "fp8_convs", "bf16")):   # a subset (tools/c5_prof.py)
         return {"ms_per_frame": res}
     return {"workload": "configs[4]: 512x512 frame, fp8 encoder+decoders, mono decode + ego "
                         "flow + flow-error mask (on a side stream) beside pair decode/heads, "
                         "then apply_dynamic_mask",
             "ms_per_frame_fp8": res["fp8"], "ms_per_frame_bf16": res["bf16"],
             "frames_per_s_fp8": 1e3 / res["fp8"], "speedup_vs_bf16": res["bf16"] / res["fp8"],
+            "ms_per_frame_fp8_unfolded": res.get("fp8_unfolded"),
+            "lnfold": "fp8 modes fold every block LayerNorm into the e4m3 projections (the "
+                      "residual GEMMs write a shifted e4m3 copy of x + row statistics, "
+                      "_fp8_fold_params); fp8_unfolded: separate e4m3 LayerNorm launches",
             "ms_per_frame_fp8_convs": res["fp8_convs"],
             "speedup_fp8_convs_vs_bf16": res["bf16"] / res["fp8_convs"],
             "fp8_convs": "opt-in set_fp8(convs=True): head.0 / head.2 on the fp8 MFMA (pair X "

@@ -299,7 +299,9 @@ enum {
                              epilogue forms LN(x) W^T + b = rstd (acc - mean c1[n]) + c2[n]
                              with mean / rstd from the producer's stats (Chan's combination
                              of the groups, fixed order), c1 = ln_c1 (row sums of B) and
-                             bias = c2 = b + W beta.  GEMM mode; no fp8 */
+                             bias = c2 = b + W beta.  GEMM mode.  On e4m3 operands (IN_FP8,
+                             ABI 0.5) A is the producer's shifted e4m3 copy (ln_shift) and
+                             ln_c3 restores the shift before the fold                 */
 };
 
 typedef struct {
@@ -343,6 +345,16 @@ typedef struct {
                                               tile configuration (vit_gemm_kern.h TileCfg) with
                                               split_k (0 → 1) — a caller that knows the launch
                                               shares the chip (the prefetched encoder) */
+  /* ABI 0.5: the LayerNorm fold on e4m3 operands (fp8 mode) */
+  const float* ln_c3;                      /* LN_FOLD + IN_FP8: f32 [N] per weight batch
+                                              (strideBias) added to the dequantised accumulator
+                                              before the fold: Σ_k shift[k] B[n][k] for an A
+                                              copy written with ln_shift                    */
+  const float* ln_shift;                   /* LN_STATS: null → C2 is the bf16 copy; else C2 is
+                                              e4m3((C[m][n] − shift[n]) · ln_qscale[g]), shift
+                                              f32 [N] per weight batch (strideBias)          */
+  const float* ln_qscale;                  /* LN_STATS with ln_shift: f32 e4m3 scale per weight
+                                              batch (device memory, > 0)                    */
 } m3s_gemm_desc;
 
 /* C = epilogue(A · Bᵀ), batched over desc->batch.  K % 8 == 0; conv: Cin % 32 == 0.

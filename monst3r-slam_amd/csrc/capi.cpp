@@ -16,7 +16,7 @@ extern "C" const char* m3s_status_string(int status) {
   }
 }
 
-extern "C" int m3s_version(void) { return (0 << 16) | (4 << 8) | 0; }
+extern "C" int m3s_version(void) { return (0 << 16) | (5 << 8) | 0; }
 
 // ---- step timeline (common.h) ----
 #define M3S_TL_SUB_HOST 64   // = M3S_TL_SUB: stamp pairs per slot

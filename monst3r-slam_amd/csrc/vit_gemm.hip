@@ -180,16 +180,29 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   a.a_xor = 0;
   a.ln_c1 = d->ln_c1;
   a.ln_eps = d->ln_eps;
+  a.ln_groups = d->stats_groups;
+  a.ln_c3 = d->ln_c3;
+  a.ln_shift = d->ln_shift;
+  a.ln_qscale = d->ln_qscale;
   const bool ln_stats = d->flags & M3S_EPI_LN_STATS, ln_fold = d->flags & M3S_EPI_LN_FOLD;
   if (ln_stats || ln_fold) {
-    // GEMM mode, bf16 operands, biased, 128-column groups, 16-B aligned row vectors
-    if (d->mode != 0 || f8 || !d->stats || !d->bias || !(d->flags & M3S_EPI_BIAS) ||
-        (d->flags & (M3S_EPI_CONVT | M3S_EPI_OUT_FP8)) || !aligned16(d->stats))
+    // GEMM mode, biased, 128-column groups, 16-B aligned row vectors (bf16 or e4m3 operands)
+    if (d->mode != 0 || !d->stats || !d->bias || !(d->flags & M3S_EPI_BIAS) ||
+        (d->flags & M3S_EPI_CONVT) || (ln_stats && (d->flags & M3S_EPI_OUT_FP8)) ||
+        !aligned16(d->stats))
       return M3S_ERR_INVALID_ARG;
   }
   if (ln_stats && (d->N % 128 || !(d->flags & M3S_EPI_OUT_F32) || !d->C2 || !aligned16(d->C2) ||
                    (d->flags & (M3S_EPI_GELU | M3S_EPI_ROPE | M3S_EPI_RELU))))
     return M3S_ERR_INVALID_ARG;
+  // the shifted e4m3 copy (fp8 consumer) / the consumer's shift term: fp8 fold only
+  if (d->ln_shift && (!ln_stats || !aligned16(d->ln_shift) || !d->ln_qscale ||
+                      d->strideBias % 4))
+    return M3S_ERR_INVALID_ARG;
+  if (d->ln_c3 && (!ln_fold || !f8 || !aligned16(d->ln_c3)))
+    return M3S_ERR_INVALID_ARG;
+  if (!ln_stats) a.ln_shift = nullptr;
+  if (!ln_fold) a.ln_c3 = nullptr;
   if (ln_fold) {
     if (d->K % 128 || d->K / 128 != d->stats_groups || d->stats_groups > 8 || !d->ln_c1 ||
         !aligned16(d->ln_c1) || d->a_batch_xor < 0 || d->a_batch_xor > 1 ||

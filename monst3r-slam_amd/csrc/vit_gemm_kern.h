@@ -82,6 +82,11 @@ struct Args {
   int a_xor;               // LN_FOLD: A and stats of batch g ^ a_xor
   const float* ln_c1;      // LN_FOLD: row sums of the gamma-folded weight (stride sBias)
   float ln_eps;
+  int ln_groups;           // LN_FOLD: 128-column groups per stats row (LayerNorm dim / 128)
+  const float* ln_c3;      // LN_FOLD + IN_FP8: Σ_k shift[k] B[n][k], added after the dequant
+  const float* ln_shift;   // LN_STATS: non-null → C2 = e4m3((C − shift[n]) · ln_qscale[g])
+  const float* ln_qscale;  //   (one scale per weight batch, device memory: re-calibration
+                           //   in place reaches captured graphs)
   unsigned long long* tl;  // step-timeline slot or null (common.h)
 };
 
@@ -152,6 +157,35 @@ __device__ __forceinline__ void store_bf16x8(bf16_t* p, const float* x) {
 #pragma unroll
   for (int t = 0; t < 8; t++) o[t] = f2bf(x[t]);
   *reinterpret_cast<bf16x8*>(p) = o;
+}
+
+// LN_STATS: the copy of the 8 stored values [n, n+8) of row m that the LN_FOLD consumer
+// reads as A — bf16, or (ln_shift set: the fp8 consumer) e4m3 of (x − shift[n]) · qscale,
+// the per-channel calibrated shift centring each channel before the 3-bit mantissa.
+// ln_c2_operands loads a thread's 8 shifts + the scale once, ahead of the epilogue's
+// stores: a load issued between them would wait for every store before it (vmcnt counts
+// both), one memory round trip per row vector (enc fc2 15.7 → 22.8 us measured so)
+__device__ __forceinline__ void ln_c2_operands(const Args& a, int64_t g, int n, float* sh,
+                                               float& q) {
+  const int64_t gw = a.wmod > 0 ? g % a.wmod : g;
+  const float* p = a.ln_shift + gw * a.sBias + n;
+  *reinterpret_cast<float4*>(sh) = *reinterpret_cast<const float4*>(p);
+  *reinterpret_cast<float4*>(sh + 4) = *reinterpret_cast<const float4*>(p + 4);
+  q = a.ln_qscale[gw];
+}
+
+__device__ __forceinline__ void ln_store_c2(const Args& a, int64_t g, int64_t off,
+                                            const float* x, const float* sh, float q) {
+  if (a.ln_shift) {
+    uint8_t* p = reinterpret_cast<uint8_t*>(a.C2) + g * a.sC + off;
+    *reinterpret_cast<uint2*>(p) =
+        make_uint2(pack4_fp8((x[0] - sh[0]) * q, (x[1] - sh[1]) * q, (x[2] - sh[2]) * q,
+                             (x[3] - sh[3]) * q),
+                   pack4_fp8((x[4] - sh[4]) * q, (x[5] - sh[5]) * q, (x[6] - sh[6]) * q,
+                             (x[7] - sh[7]) * q));
+  } else {
+    store_bf16x8(a.C2 + g * a.sC + off, x);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -423,6 +457,7 @@ __device__ __forceinline__ bool gemm_epilogue(const Args& a, char* lds, int g, i
   const bool vec_path = vec && en < a.N;
   float e_b[8], e_pb[8], e_x[EG][16];
   float e_c1[8], e_pc1[8], e_mu[EG], e_rs[EG];  // LN_FOLD: c1 columns, row mean / rstd
+  float e_sh[8], e_q = 0.f;                     // LN_STATS e4m3 copy: shifts, scale
   // LN_FOLD: the 16 lanes of a row group own rows er0 + v·RSTEP (v < NV ≤ 16); lane v
   // combines the statistics of row v once, the others read it by lane shuffle
   float ln_mu = 0.f, ln_rs = 0.f;
@@ -430,8 +465,8 @@ __device__ __forceinline__ bool gemm_epilogue(const Args& a, char* lds, int g, i
   int rb = 0;                                 // first tile row of the epilogue pass
   auto ln_setup = [&]() {
     if ((fl & M3S_EPI_LN_FOLD) && (lane & 15) < NV)
-      ln_row_stats(a, g ^ a.a_xor, min(m0 + rb + er0 + (lane & 15) * RSTEP, a.M - 1), a.K >> 7,
-                   ln_mu, ln_rs);
+      ln_row_stats(a, g ^ a.a_xor, min(m0 + rb + er0 + (lane & 15) * RSTEP, a.M - 1),
+                   a.ln_groups, ln_mu, ln_rs);
   };
   Epi e = make_epi(a, g);
   e.flags = fl;
@@ -491,6 +526,7 @@ __device__ __forceinline__ bool gemm_epilogue(const Args& a, char* lds, int g, i
             *reinterpret_cast<const float4*>(c1 + (en ^ 16) + 4);
       }
     }
+    if ((fl & M3S_EPI_LN_STATS) && a.ln_shift) ln_c2_operands(a, g, en, e_sh, e_q);
     if (prefetch_rows) e_prefetch(0);
   };
   if (!SPLIT) epi_setup(false);   // split-K: only the tile's last split needs the operands
@@ -737,8 +773,8 @@ __device__ __forceinline__ bool gemm_epilogue(const Args& a, char* lds, int g, i
           float* cp = reinterpret_cast<float*>(e.C) + off;
           *reinterpret_cast<float4*>(cp) = make_float4(x[0], x[1], x[2], x[3]);
           *reinterpret_cast<float4*>(cp + 4) = make_float4(x[4], x[5], x[6], x[7]);
-          if (fl & M3S_EPI_LN_STATS) {  // the next LayerNorm's input: bf16 copy + row stats
-            store_bf16x8(a.C2 + (int64_t)g * a.sC + off, x);
+          if (fl & M3S_EPI_LN_STATS) {  // the next LayerNorm's input: A copy + row stats
+            ln_store_c2(a, g, off, x, e_sh, e_q);
             ln_group_stats(a, g, m, en, x);
           }
         } else if (fl & M3S_EPI_OUT_FP8) {
@@ -1093,15 +1129,27 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
   M3S_T(t_loop);
   tl_end.mark(2);
   if constexpr (F8) {  // dequant: acc(i, j) *= col_scale[n] (n = this lane's column)
-    const float* cs_g = a.cscale + (int64_t)(a.wmod > 0 ? g % a.wmod : g) * a.sCscale;
+    const int64_t gw = a.wmod > 0 ? g % a.wmod : g;
+    const float* cs_g = a.cscale + gw * a.sCscale;
+    // LN_FOLD consumer of a shifted e4m3 copy: + c3[n] = Σ_k shift[k] B[n][k] restores
+    // Σ_k x[k] B[n][k] before the epilogue's rstd (acc − mean c1) + c2
+    const float* c3_g = a.ln_c3 ? a.ln_c3 + gw * a.sBias : nullptr;
 #pragma unroll
     for (int j = 0; j < TN; j++) {
       const int n = n0 + wn * (BN / WN) + j * 32 + fr;
       const float sc = n < a.N ? cs_g[n] : 0.f;
+      if (c3_g) {
+        const float c3 = n < a.N ? c3_g[n] : 0.f;
 #pragma unroll
-      for (int i = 0; i < TM; i++)
+        for (int i = 0; i < TM; i++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) acc[i][j][r] *= sc;
+          for (int r = 0; r < 16; r++) acc[i][j][r] = fmaf(acc[i][j][r], sc, c3);
+      } else {
+#pragma unroll
+        for (int i = 0; i < TM; i++)
+#pragma unroll
+          for (int r = 0; r < 16; r++) acc[i][j][r] *= sc;
+      }
     }
   }
 
@@ -1161,7 +1209,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(Args a) {
     }
     epi_vec8(e, x, p, m, n);  // x now holds the stored values
     if (a.flags & M3S_EPI_LN_STATS) {
-      store_bf16x8(a.C2 + (int64_t)g * a.sC + (int64_t)m * a.ldc + n, x);
+      float sh[8], q = 0.f;
+      if (a.ln_shift) ln_c2_operands(a, g, n, sh, q);
+      ln_store_c2(a, g, (int64_t)m * a.ldc + n, x, sh, q);
       ln_group_stats(a, g, m, n, x);
     }
   } else {
@@ -1577,6 +1627,27 @@ void launch_main_f8(Args& a, dim3 grid, hipStream_t s) {
       if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, true>(
               a, grid, s, key))
         return;
+      // the LayerNorm fold on e4m3 operands (round 6): consumers qkv / q (+RoPE) and fc1
+      // (+GELU, e4m3 out), producers the residual GEMMs (f32 x + shifted e4m3 copy + stats)
+      constexpr int LF = M3S_EPI_LN_FOLD | M3S_EPI_BIAS, LS = M3S_EPI_LN_STATS | M3S_EPI_BIAS;
+      if (key == (LF | M3S_EPI_ROPE)) {
+        hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, false,
+                                        LF | M3S_EPI_ROPE, true>),
+                           grid, dim3(WM * WN * 64), 0, s, a);
+        return;
+      }
+      if (key == (LF | M3S_EPI_GELU | M3S_EPI_OUT_FP8)) {
+        hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, false,
+                                        LF | M3S_EPI_GELU | M3S_EPI_OUT_FP8, true>),
+                           grid, dim3(WM * WN * 64), 0, s, a);
+        return;
+      }
+      if (key == (LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32)) {
+        hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, false,
+                                        LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, true>),
+                           grid, dim3(WM * WN * 64), 0, s, a);
+        return;
+      }
     } else if constexpr (BN == 128) {
       if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, MODE, M3S_EPI_RELU | M3S_EPI_DPT_OUT, true>(
               a, grid, s, key))

@@ -115,7 +115,8 @@ class GemmDesc(ctypes.Structure):
                 ("stats_groups", ctypes.c_int32), ("a_batch_xor", ctypes.c_int32),
                 ("ln_c1", _P), ("ln_eps", ctypes.c_float),
                 ("tile_counters", _P), ("tile_counters_len", ctypes.c_int32),
-                ("tile_hint", ctypes.c_int32)]
+                ("tile_hint", ctypes.c_int32),
+                ("ln_c3", _P), ("ln_shift", _P), ("ln_qscale", _P)]
 
 
 (EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RES_F32, EPI_RES_BF16, EPI_OUT_F32, PRO_RELU, EPI_CONVT,

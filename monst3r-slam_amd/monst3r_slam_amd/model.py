@@ -90,9 +90,12 @@ class Ops:
         float8_e4m3fn / uint8), the f32 accumulator is scaled per column; out_fp8: C is
         stored as e4m3.
         ln_stats = (C2 bf16, stats f32 [batch, M, N/128, 2]): this f32-out GEMM produces a
-        LayerNorm input — also store its bf16 copy and per-128-column (mean, M2).
-        ln_fold = (stats, c1 f32, a_xor): A is the bf16 copy of a LayerNorm input and B a
-        gamma-folded weight; the epilogue applies the normalisation (bias = c2).
+        LayerNorm input — also store its bf16 copy and per-128-column (mean, M2);
+        (C2 uint8, stats, shift f32 [.., N], qscale f32 [..]): the copy is e4m3 of
+        (C − shift)·qscale instead (the fp8 consumer's A operand).
+        ln_fold = (stats, c1 f32, a_xor[, c3 f32]): A is the bf16 (or shifted e4m3) copy of a
+        LayerNorm input and B a gamma-folded weight; the epilogue applies the normalisation
+        (bias = c2); c3 = Σ_k shift[k] B[n][k] for the shifted e4m3 copy.
         tile = (tile configuration, split-K): the descriptor's tile_hint instead of the
         per-shape table (PairModel.encode(concurrent=True))."""
         if tile is None:
@@ -134,10 +137,14 @@ class Ops:
         if ln_stats is not None:
             d.flags |= _lib.EPI_LN_STATS
             d.C2, d.stats = _p(ln_stats[0]), _p(ln_stats[1])
+            if len(ln_stats) > 2 and ln_stats[2] is not None:
+                d.ln_shift, d.ln_qscale = _p(ln_stats[2]), _p(ln_stats[3])
         if ln_fold is not None:
             d.flags |= _lib.EPI_LN_FOLD
             d.stats, d.ln_c1, d.a_batch_xor = _p(ln_fold[0]), _p(ln_fold[1]), ln_fold[2]
             d.stats_groups, d.ln_eps = K // 128, LN_EPS
+            if len(ln_fold) > 3 and ln_fold[3] is not None:
+                d.ln_c3 = _p(ln_fold[3])
         if self.record is not None:  # (descriptor copy, flops, fp8) for the bench replay
             dc = _lib.GemmDesc()
             ctypes.memmove(ctypes.byref(dc), ctypes.byref(d), ctypes.sizeof(d))
@@ -264,6 +271,9 @@ DEC_FP8 = ("qkv_w", "proj_w", "q_w", "kv_w", "cproj_w", "fc1_w", "fc2_w")
 # ... and the DPT heads' two full-resolution 3x3 convs (round 5): their inputs are the
 # bilinear upsamples (path1 → head.0, head.0 → head.2), which emit e4m3 directly
 HEAD_FP8 = ("head0", "head2")
+# ... and, for the fp8 LayerNorm fold (round 6), the gamma-folded norm → projection weights
+ENC_FP8_FOLD = ("qkv_wf", "fc1_wf")
+DEC_FP8_FOLD = ("qkvkv_wf", "q_wf", "fc1_wf")
 FP8_ACT_HEADROOM = 2.0   # calibrated amax maps to 448 / 2: test frames may run hotter
 
 
@@ -321,6 +331,66 @@ def _fp8_shifted_params(W, cal):
         d["cproj_b"] = P["cproj_b"].to(f64) + mv(P["cproj_w"], mc)
         d["fc1_b"] = P["fc1_b"].to(f64) + mv(P["fc1_w"], m3)
         d["fc2_b"] = P["fc2_b"].to(f64) - mv(deq(P8["fc2_w"], P["fc2_w"]), mh)
+        dec.append({k: v.float().contiguous() for k, v in d.items()})
+    return enc, dec
+
+
+def _fp8_fold_params(W, cal, raw):
+    """Parameters of the fp8 LayerNorm fold (round 6; PairModel._f8fold) from the same
+    calibration pass as _fp8_shifted_params.  raw[(site, layer)] = (mean, max, min) per
+    channel of the raw residual stream x where a LayerNorm reads it ([C] encoder, [4, C] per
+    decoder weight stack).  The producer of that x writes e4m3((x − s)·qs) with s = the
+    channel mean and qs = 448 / (headroom · max |x − s|); the consumer (gamma-folded weight
+    W' of ln_fold, e4m3 per row with scale sw) then accumulates Σ (x − s)·W'q, dequantises
+    with col_scale = sw / qs and adds c3 = W' s, so that the epilogue's
+    rstd (acc − mean c1) + c2 is LN(x)·W'ᵀ + c2 up to the e4m3 roundings (c1, c3 from the
+    bf16 W': the weight rounding meets only the centred x − s, as in the LayerNorm path).
+    c2 of the q/k/v projections carries the attention-output shifts of _fp8_shifted_params
+    (the v columns minus that attention's calibrated output mean).  Returns (encoder dict of
+    [L, ...] stacks, decoder list of per-layer dicts of [4, ...] stacks), f32."""
+    f64 = torch.float64
+
+    def qscale(mean, mx, mn):   # one scale per (layer | stack): the largest channel range
+        amax = torch.maximum(mx - mean, mean - mn)
+        return 448.0 / (FP8_ACT_HEADROOM * amax.amax(-1).clamp_min(1e-30))
+
+    def consumer(q8, wf, s, qs):   # (col_scale, c3) of a gamma-folded e4m3 weight
+        return (q8[1].to(f64) / qs[..., None],
+                torch.einsum("...nk,...k->...n", wf.to(f64), s))
+
+    L = W.arch.enc_depth
+    P, P8 = W.enc, W.enc8
+    stk = lambda site, j: torch.stack([raw[(site, i)][j] for i in range(L)])  # noqa: E731
+    s1, s2 = stk("enc.x1", 0), stk("enc.x2", 0)
+    qs1 = qscale(s1, stk("enc.x1", 1), stk("enc.x1", 2))
+    qs2 = qscale(s2, stk("enc.x2", 1), stk("enc.x2", 2))
+    E = s1.shape[-1]
+    ma = torch.stack([cal[("enc.att", i)] for i in range(L)])
+    qkv_cs, qkv_c3 = consumer(P8["qkv_wf"], P["qkv_wf"], s1, qs1)
+    fc1_cs, fc1_c3 = consumer(P8["fc1_wf"], P["fc1_wf"], s2, qs2)
+    qkv_c2 = P["qkv_c2"].to(f64).clone()
+    qkv_c2[:, 2 * E:] -= ma
+    enc = dict(s1=s1, qs1=qs1, s2=s2, qs2=qs2, qkv_cs=qkv_cs, qkv_c3=qkv_c3, qkv_c2=qkv_c2,
+               fc1_cs=fc1_cs, fc1_c3=fc1_c3, fc1_c2=P["fc1_c2"])
+    enc = {k: v.float().contiguous() for k, v in enc.items()}
+    dec = []
+    sw = [1, 0, 3, 2]
+    for i, (P, P8) in enumerate(zip(W.dec, W.dec8)):
+        d = {}
+        for t in ("1", "2", "3"):
+            mean, mx, mn = raw[("dec.x" + t, i)]
+            d["s" + t], d["qs" + t] = mean, qscale(mean, mx, mn)
+        D = d["s1"].shape[-1]
+        d["qkvkv_cs"], d["qkvkv_c3"] = consumer(P8["qkvkv_wf"], P["qkvkv_wf"], d["s1"], d["qs1"])
+        d["q_cs"], d["q_c3"] = consumer(P8["q_wf"], P["q_wf"], d["s2"], d["qs2"])
+        d["fc1_cs"], d["fc1_c3"] = consumer(P8["fc1_wf"], P["fc1_wf"], d["s3"], d["qs3"])
+        # fused columns [q | k | k' | v | v']: v = this problem's self-attention, v' = the
+        # cross-attention values of problem z ^ 1 (PackedWeights "qkvkv")
+        c2 = P["qkvkv_c2"].to(f64).clone()
+        c2[:, 3 * D:4 * D] -= cal[("dec.att", i)]
+        c2[:, 4 * D:] -= cal[("dec.catt", i)][sw]
+        d["qkvkv_c2"] = c2
+        d["q_c2"], d["fc1_c2"] = P["q_c2"], P["fc1_c2"]
         dec.append({k: v.float().contiguous() for k, v in d.items()})
     return enc, dec
 
@@ -454,6 +524,7 @@ class PackedWeights:
         self.lf_fc2_b = f32(torch.stack([sd_mast3r[f"{h}.head_local_features.fc2.bias"] for h in lf]))
         self.enc8 = self.dec8 = None
         self.fp8_shift_enc, self.fp8_shift_dec = {}, [{} for _ in self.dec]
+        self.fp8_fold_enc, self.fp8_fold_dec = {}, [{} for _ in self.dec]
         self.fp8_calibrated = False
         self.h8, self.h8_cs, self.h8_inv = None, {}, {}
 
@@ -467,6 +538,10 @@ class PackedWeights:
             # [Cout][ky][kx][Cin] rows), per-Cout scales; their e4m3 inputs come from the
             # upsample with a calibrated per-tensor scale (h8_cs = row scale x act scale)
             self.h8 = {k: quant_e4m3(self.h[k + "_w"]) for k in HEAD_FP8}
+            # the gamma-folded projections of the LayerNorm fold (ln_fold), e4m3 per row
+            self.enc8.update({k: quant_e4m3(self.enc[k]) for k in ENC_FP8_FOLD})
+            for P, P8 in zip(self.dec, self.dec8):
+                P8.update({k: quant_e4m3(P[k]) for k in DEC_FP8_FOLD})
 
 
 # ---------------------------------------------------------------------------------------
@@ -520,6 +595,10 @@ class PairModel:
         # bf16 path: the blocks' LayerNorms folded into the following projections (ln_fold;
         # LN_STATS / LN_FOLD epilogues) instead of separate LayerNorm launches
         self.lnfold = os.environ.get("M3S_LNFOLD", "1") != "0"
+        # fp8 path: the same fold on e4m3 operands (shifted e4m3 copy of x from the residual
+        # GEMMs, calibrated shifts / scales; _fp8_fold_params) — M3S_FP8_FOLD=0: separate
+        # e4m3 LayerNorm launches as in round 5
+        self.fp8_fold = os.environ.get("M3S_FP8_FOLD", "1") != "0"
         # tile configurations (TileCfg, split-K) of the prefetched encoder's projections,
         # measured in the pipelined C3 step (encode(concurrent=True)); {} = per-shape table
         # (T128W8 residual GEMMs: 212.8 → 224.5 frames/s; with the split decoder, T256W8
@@ -609,8 +688,11 @@ class PairModel:
             self.heads(hooks, gh, gw, hw[0], hw[1])
             torch.cuda.synchronize(dev)
             amax = {k: float(v) for k, v in self._cal.items() if k[0] == "amax"}
-            cal = {k: v[0] / v[1] for k, v in self._cal.items() if k[0] != "amax"}
+            raw = {k[1:]: (v[0] / v[1], v[2], v[3]) for k, v in self._cal.items()
+                   if k[0] == "raw"}
+            cal = {k: v[0] / v[1] for k, v in self._cal.items() if k[0] not in ("amax", "raw")}
             enc, dec = _fp8_shifted_params(W, cal)
+            fenc, fdec = _fp8_fold_params(W, cal, raw)
         except BaseException:
             # a failed calibration leaves the previous parameters in force
             W.fp8_shift_enc, W.fp8_shift_dec = old
@@ -629,6 +711,9 @@ class PairModel:
         W.fp8_shift_enc = _assign_params(old[0], enc)
         W.fp8_shift_dec = [_assign_params(o, n) for o, n in zip(old[1], dec)] \
             if len(old[1]) == len(dec) else dec
+        W.fp8_fold_enc = _assign_params(W.fp8_fold_enc, fenc)
+        W.fp8_fold_dec = [_assign_params(o, n) for o, n in zip(W.fp8_fold_dec, fdec)] \
+            if len(W.fp8_fold_dec) == len(fdec) else fdec
         for k in HEAD_FP8:
             sc = max(amax[("amax", k)], 1e-30) * FP8_ACT_HEADROOM / 448.0
             W.h8_inv[k] = 1.0 / sc
@@ -654,6 +739,35 @@ class PairModel:
         key = (site, i)
         acc, n = self._cal.get(key, (0.0, 0))
         self._cal[key] = (acc + m, n + 1)
+
+    def _calib_raw(self, site, i, x, z=None):
+        """Calibration hook of the fp8 LayerNorm fold: per-channel mean, max and min of the
+        raw residual stream x (f32, rows × channels or [Z, S, C] per problem z) where a
+        LayerNorm reads it (_fp8_fold_params)."""
+        if getattr(self, "_cal", None) is None:
+            return
+        C = x.shape[-1]
+        if z is None:
+            v = x.reshape(-1, C)
+            m, mx, mn = v.double().mean(0), v.amax(0).double(), v.amin(0).double()
+        else:
+            v = x.reshape(z, -1, C)
+            m = v.double().mean(1).reshape(-1, self._wm, C).mean(0)
+            mx = v.amax(1).double().reshape(-1, self._wm, C).amax(0)
+            mn = v.amin(1).double().reshape(-1, self._wm, C).amin(0)
+        key = ("raw", site, i)
+        if key in self._cal:
+            acc, n, pmx, pmn = self._cal[key]
+            m, mx, mn = acc + m, torch.maximum(pmx, mx), torch.minimum(pmn, mn)
+        else:
+            n = 0
+        self._cal[key] = (m, n + 1, mx, mn)
+
+    def _f8fold(self):
+        """fp8 mode with the LayerNorms folded into the e4m3 projections (round 6): calibrated,
+        not calibrating, the fold on (M3S_LNFOLD) and M3S_FP8_FOLD != 0."""
+        return (self.fp8 and self.fp8_fold and self.lnfold and self.w.fp8_calibrated and
+                bool(self.w.fp8_fold_enc) and getattr(self, "_cal", None) is None)
 
     def _calib_amax(self, name, t):
         if getattr(self, "_cal", None) is not None:
@@ -793,18 +907,27 @@ class PairModel:
         lo, hi = layers if layers is not None else (0, a.enc_depth)
         patches = self._buf("enc_patch", (M, 3 * a.patch * a.patch), BF16)
         x = self._buf("enc_x", (M, E), F32)
-        fold = self.lnfold and not self.fp8 and E % 128 == 0
+        f8f = self._f8fold() and E % 128 == 0
+        fold = self.lnfold and (not self.fp8 or f8f) and E % 128 == 0
         if fold:
             # LayerNorm folded into the projections (ln_fold): every residual-stream
-            # producer also writes x in bf16 + row statistics; no LayerNorm launches
-            xb = self._buf("enc_xb", (M, E), BF16)
+            # producer also writes x in bf16 (fp8: e4m3 of x − shift, _fp8_fold_params) +
+            # row statistics; no LayerNorm launches
+            xb = self._buf("enc_xq" if f8f else "enc_xb", (M, E), U8 if f8f else BF16)
             st = self._buf("enc_stats", (M, E // 128, 2), F32)
-            R32S = dict(flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, ln_stats=(xb, st))
+            FE = self.w.fp8_fold_enc
+
+            def lns(t, i):   # ln_stats of the producer of layer i's norm<t> input
+                if not f8f:
+                    return (xb, st)
+                if i >= a.enc_depth:   # the last block's output goes to enc_norm
+                    return None
+                return (xb, st, FE["s" + t][i], FE["qs" + t][i:i + 1])
         if begin:
             img = img.to(F32).contiguous()
             o.patchify(img, patches, B, H, Wd)
             o.gemm(patches, W.patch_w, x, M, E, 3 * a.patch * a.patch, bias=W.patch_b,
-                   flags=_lib.EPI_OUT_F32, ln_stats=(xb, st) if fold else None)
+                   flags=_lib.EPI_OUT_F32, ln_stats=lns("1", 0) if fold else None)
         adt = U8 if self.fp8 else BF16   # GEMM A operands: e4m3 bytes in fp8 mode
         xn = self._buf("enc_xn", (M, E), adt)
         qkv = self._buf("enc_qkv", (M, 3 * E), BF16)
@@ -813,8 +936,28 @@ class PairModel:
         pos = self.positions(B, gh, gw)
         rt = self.rope_tab(gh, gw)
         P, P8 = W.enc, W.enc8
-        if fold:
+        R32 = _lib.EPI_OUT_F32 | _lib.EPI_RES_F32
+        for i in (range(lo, hi) if f8f else ()):
+            # the fp8 fold: e4m3 gamma-folded qkv / fc1 on the shifted e4m3 copy of x
+            o.gemm(xb, P8["qkv_wf"][0][i], qkv, M, 3 * E, E, bias=FE["qkv_c2"][i],
+                   rope=(rt, 2 * E, S), ln_fold=(st, P["qkv_c1"][i], 0, FE["qkv_c3"][i]),
+                   fp8=(FE["qkv_cs"][i], 0), tile=tiles.get("qkv"))
+            o.attn(qkv, 3 * E, S * 3 * E, qkv[:, E:], qkv[:, 2 * E:], 3 * E, S * 3 * E, att,
+                   E, S * E, B, a.enc_heads, S, S)
+            w, kw = self._wt(P, P8, "proj_w", i)
+            o.gemm(att, w, x, M, E, E, bias=self._pb(P, "proj_b", i), R=x, flags=R32,
+                   ln_stats=lns("2", i), tile=tiles.get("proj"), **kw)
+            o.gemm(xb, P8["fc1_wf"][0][i], hid, M, a.mlp_ratio * E, E, bias=FE["fc1_c2"][i],
+                   flags=_lib.EPI_GELU, out_fp8=True,
+                   ln_fold=(st, P["fc1_c1"][i], 0, FE["fc1_c3"][i]), fp8=(FE["fc1_cs"][i], 0),
+                   tile=tiles.get("fc1"))
+            w, kw = self._wt(P, P8, "fc2_w", i)
+            o.gemm(hid, w, x, M, E, a.mlp_ratio * E, bias=self._pb(P, "fc2_b", i), R=x,
+                   flags=R32, ln_stats=lns("1", i + 1), tile=tiles.get("fc2"), **kw)
+            yield i
+        if fold and not f8f:
             hot = _exp_hot_weights("enc")
+            R32S = dict(flags=R32, ln_stats=(xb, st))
             for i in range(lo, hi):
                 j = 0 if hot else i
                 o.gemm(xb, P["qkv_wf"][j], qkv, M, 3 * E, E, bias=P["qkv_c2"][j],
@@ -830,6 +973,7 @@ class PairModel:
                 yield i
         pb = self._pb
         for i in (range(lo, hi) if not fold else ()):
+            self._calib_raw("enc.x1", i, x)
             o.ln(x, P["ln1_g"][i], pb(P, "ln1_b", i), xn, M, E)
             self._calib("enc.ln1", i, xn)
             # qkv projection with RoPE2D on q and k fused into the epilogue
@@ -841,6 +985,7 @@ class PairModel:
             w, kw = self._wt(P, P8, "proj_w", i)
             o.gemm(att, w, x, M, E, E, bias=pb(P, "proj_b", i), R=x,
                    flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, **kw)
+            self._calib_raw("enc.x2", i, x)
             o.ln(x, P["ln2_g"][i], pb(P, "ln2_b", i), xn, M, E)
             self._calib("enc.ln2", i, xn)
             w, kw = self._wt(P, P8, "fc1_w", i)
@@ -889,13 +1034,17 @@ class PairModel:
             o.copy_rows(f, h0, 1, fb, fb, fb, G, models, fb, 0, 0, 2 * models * fb, 2 * fb,
                         side * fb)
         x = self._buf("dec_x", (Z, S, D), F32)
-        fold = self.lnfold and not self.fp8 and self.serial and D % 128 == 0
+        f8f = self._f8fold()
+        fold = self.lnfold and (not self.fp8 or f8f) and self.serial and D % 128 == 0
+        lns = None
         if fold:
-            xb = self._buf("dec_xb", (Z, S, D), BF16)
+            # fp8: the residual stream's shifted e4m3 copy (_fp8_fold_params) instead of bf16
+            xb = self._buf("dec_xq" if f8f else "dec_xb", (Z, S, D), U8 if f8f else BF16)
             st = self._buf("dec_stats", (Z, S, D // 128, 2), F32)
+            F0 = W.fp8_fold_dec[0]
+            lns = (xb, st, F0["s1"], F0["qs1"]) if f8f else (xb, st)
         o.gemm(h0, W.dec_embed_w, x, S, D, E, Z, sA=S * E, sB=D * E, sC=S * D,
-               bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32, wmod=wm,
-               ln_stats=(xb, st) if fold else None)
+               bias=W.dec_embed_b, sBias=D, flags=_lib.EPI_OUT_F32, wmod=wm, ln_stats=lns)
         if on_hook is not None:
             on_hook("h0", {"h0": h0})
         if fold and self.dec_split and models == 2 and G == 1 and on_hook is None:
@@ -984,6 +1133,7 @@ class PairModel:
             # norm1(x) and norm_y(other side's x) share the row statistics: one pass; then
             # y_'s k/v projection
             w, kw = wt("kv_w", 2 * D)
+            self._calib_raw("dec.x1", i, x, Z)
             o.ln_dual(x, P["ln1_g"], pb("ln1_b"), xn, P["lny_g"], pb("lny_b"), yn, S, D, Z,
                       S * D, S * D, D, pmod=wm)
             self._calib("dec.lny", i, yn, Z)
@@ -1001,6 +1151,7 @@ class PairModel:
             o.gemm(att, w, x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D, bias=pb("proj_b"),
                    sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
             # cross-attention: q from norm2(x), k/v from y_
+            self._calib_raw("dec.x2", i, x, Z)
             o.ln(x, P["ln2_g"], pb("ln2_b"), xn, S, D, Z, S * D, S * D, D, pmod=wm)
             self._calib("dec.ln2", i, xn, Z)
             w, kw = wt("q_w", D)
@@ -1013,6 +1164,7 @@ class PairModel:
             o.gemm(att, w, x, S, D, D, Z, sA=S * D, sB=D * D, sC=S * D,
                    bias=pb("cproj_b"), sBias=D, R=x, sR=S * D, flags=R32, wmod=wm, **kw)
             # MLP
+            self._calib_raw("dec.x3", i, x, Z)
             o.ln(x, P["ln3_g"], pb("ln3_b"), xn, S, D, Z, S * D, S * D, D, pmod=wm)
             self._calib("dec.ln3", i, xn, Z)
             w, kw = wt("fc1_w", Dm)
@@ -1031,6 +1183,63 @@ class PairModel:
             yield i
         return hooks
 
+    def _decode_f8fold_layer(self, i, x, xq, st, qkv, q, att, hid, hooks, hook_bufs, S, D, rt,
+                             wm, sl, on_hook):
+        """(Generator, one step.)  Decoder block i of _decode_folded_gen on e4m3 operands:
+        the gamma-folded qkvkv / q / fc1 projections read the shifted e4m3 copy xq of x that
+        the previous residual GEMM wrote (ln_stats with the calibrated shift / scale of the
+        LayerNorm it feeds), attention and GELU emit e4m3, proj / cproj / fc2 run on the
+        e4m3 weights with the calibrated bias shifts (_fp8_shifted_params); the hook layers'
+        bf16 copies come from x directly."""
+        o, a, W = self.ops, self.a, self.w
+        Z = x.shape[0]
+        F5, Dm = 5 * D, a.mlp_ratio * D
+        P, P8, Q, F = W.dec[i], W.dec8[i], W.fp8_shift_dec[i], W.fp8_fold_dec[i]
+        if sl is not None:
+            P = {k: v[sl] for k, v in P.items()}
+            P8 = {k: (v[0][sl], v[1][sl]) for k, v in P8.items()}
+            Q = {k: v[sl] for k, v in Q.items()}
+            F = {k: v[sl] for k, v in F.items()}
+        last = i + 1 == a.dec_depth
+        Fn = None if last else W.fp8_fold_dec[i + 1]
+        if Fn is not None and sl is not None:
+            Fn = {k: Fn[k][sl] for k in ("s1", "qs1")}
+        R32 = dict(R=x, sR=S * D, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32)
+        zs = dict(sA=S * D, sC=S * D, wmod=wm)
+        tl = _tile_knob("M3S_DEC_TILE", ("qkv", "proj", "q", "cproj", "fc1", "fc2"),
+                        self.dec_tiles if sl is None else self.dec_tiles_split).get
+        o.gemm(xq, P8["qkvkv_wf"][0], qkv, S, F5, D, Z, sA=S * D, sB=F5 * D, sC=S * F5,
+               bias=F["qkvkv_c2"], sBias=F5, rope=(rt, 3 * D, S), wmod=wm,
+               ln_fold=(st, P["qkvkv_c1"], 0, F["qkvkv_c3"]), fp8=(F["qkvkv_cs"], F5),
+               tile=tl("qkv"))
+        o.attn(qkv, F5, S * F5, qkv[:, :, D:], qkv[:, :, 3 * D:], F5, S * F5, att,
+               D, S * D, Z, a.dec_heads, S, S)
+        o.gemm(att, P8["proj_w"][0], x, S, D, D, Z, sB=D * D, bias=Q["proj_b"], sBias=D,
+               fp8=(P8["proj_w"][1], D), ln_stats=(xq, st, F["s2"], F["qs2"]), tile=tl("proj"),
+               **zs, **R32)
+        o.gemm(xq, P8["q_wf"][0], q, S, D, D, Z, sB=D * D, bias=F["q_c2"], sBias=D,
+               rope=(rt, D, S), ln_fold=(st, P["q_c1"], 0, F["q_c3"]), fp8=(F["q_cs"], D),
+               tile=tl("q"), **zs)
+        o.attn(q, D, S * D, qkv[:, :, 2 * D:], qkv[:, :, 4 * D:], F5, S * F5, att, D,
+               S * D, Z, a.dec_heads, S, S, kv_xor=1)
+        o.gemm(att, P8["cproj_w"][0], x, S, D, D, Z, sB=D * D, bias=Q["cproj_b"], sBias=D,
+               fp8=(P8["cproj_w"][1], D), ln_stats=(xq, st, F["s3"], F["qs3"]),
+               tile=tl("cproj"), **zs, **R32)
+        o.gemm(xq, P8["fc1_wf"][0], hid, S, Dm, D, Z, sA=S * D, sB=Dm * D, sC=S * Dm,
+               bias=F["fc1_c2"], sBias=Dm, flags=_lib.EPI_GELU, out_fp8=True, wmod=wm,
+               ln_fold=(st, P["fc1_c1"], 0, F["fc1_c3"]), fp8=(F["fc1_cs"], Dm),
+               tile=tl("fc1"))
+        o.gemm(hid, P8["fc2_w"][0], x, S, D, Dm, Z, sA=S * Dm, sB=Dm * D, sC=S * D,
+               bias=Q["fc2_b"], sBias=D, wmod=wm, fp8=(P8["fc2_w"][1], D), tile=tl("fc2"),
+               ln_stats=None if last else (xq, st, Fn["s1"], Fn["qs1"]), **R32)
+        if (i + 1) in hook_bufs:
+            hook_bufs[i + 1].copy_(x)
+            hooks[f"h{i + 1}"] = self._buf(f"h{i + 1}", (2 * wm if sl is not None else Z,
+                                                         S, D), BF16)
+            if on_hook is not None:
+                on_hook(f"h{i + 1}", hooks)
+        yield i
+
     def _decode_folded(self, *args, **kw):
         return _drain(self._decode_folded_gen(*args, **kw))
 
@@ -1044,11 +1253,13 @@ class PairModel:
         rows (PackedWeights "qkvkv"); the cross-attention reads them with kv_xor = 1.
         The hook layers' bf16 copies are written straight into the hook buffers."""
         o, a, W = self.ops, self.a, self.w
+        f8f = self._f8fold()                     # e4m3 operands (xb: shifted e4m3 copy)
+        adt = U8 if f8f else BF16
         F5 = 5 * D                               # fused [q | k | k' | v | v'] columns
         qkv = self._buf("dec_qkvkv", (Z, S, F5), BF16)
         q = self._buf("dec_q", (Z, S, D), BF16)
-        att = self._buf("dec_att", (Z, S, D), BF16)
-        hid = self._buf("dec_hid", (Z, S, a.mlp_ratio * D), BF16)
+        att = self._buf("dec_att_f8" if f8f else "dec_att", (Z, S, D), adt)
+        hid = self._buf("dec_hid_f8" if f8f else "dec_hid", (Z, S, a.mlp_ratio * D), adt)
         hooks = {"h0": h0}
         hook_bufs = {k: self._buf(f"h{k}", (Z, S, D), BF16) for k in a.hooks[1:3]}
         sl = None
@@ -1074,6 +1285,10 @@ class PairModel:
                 P = {k: v[sl] for k, v in P.items()}
             R32S = dict(R=x, sR=S * D, flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32,
                         ln_stats=(xb, st))
+            if f8f:
+                yield from self._decode_f8fold_layer(i, x, xb, st, qkv, q, att, hid, hooks,
+                                                     hook_bufs, S, D, rt, wm, sl, on_hook)
+                continue
             # norm1 → qkv of problem z and norm_y → cross k/v of problem z ^ 1, one GEMM over
             # x of the layer's start (the reference's y_ = norm_y(y) before x changes)
             o.gemm(xc, P["qkvkv_wf"], qkv, S, F5, D, Z, sA=S * D, sB=F5 * D, sC=S * F5,

@@ -598,19 +598,22 @@ def test_attention_fp8_out(ops, dev, monkeypatch, splits):
     assert _rel(out, ref) < 0.05
 
 
-@pytest.mark.parametrize("convs", [False, True])
-def test_fp8_model_vs_fp32_restatement_512(dev, parity_log, convs):
+@pytest.mark.parametrize("convs,fold", [(False, True), (True, True), (False, False)])
+def test_fp8_model_vs_fp32_restatement_512(dev, parity_log, convs, fold):
     """the fp8 transformer path (e4m3 activations + per-row weight scales on
     the scaled MFMA, calibrated per-channel shifts / bias correction; heads in bf16) at
     512x512 against the fp32 restatement.  Stated fp8 tolerances (looser than the bf16
     path's in _compare_pair): pointmap median relative error < 6 %, conf median < 8 %,
     descriptor median cosine > 0.97 and minimum > 0.98.  Measured round 5: X 2.85 %, D cos
     min 0.9958 (5.86 % / 0.962 before the calibration).  convs: the opt-in
-    fp8 head.0 / head.2 convs, X < 8 % (measured 5.41 %)."""
+    fp8 head.0 / head.2 convs, X < 8 % (measured 5.41 %).  fold: the LayerNorms folded
+    into the e4m3 projections (round 6 default, PairModel._f8fold) or separate e4m3
+    LayerNorm launches (M3S_FP8_FOLD=0) — same bars."""
     from monst3r_slam_amd import model as Mdl
     from oracle import vit_ref as V
     m, (sdm, am, sdM, aM) = Mdl.build(dev)
     m.set_fp8(True, convs=convs)
+    m.fp8_fold = fold
     gen = torch.Generator(device=dev).manual_seed(3)
     img_i = torch.rand(1, 3, 512, 512, device=dev, generator=gen) * 2 - 1
     img_j = torch.rand(1, 3, 512, 512, device=dev, generator=gen) * 2 - 1
@@ -626,7 +629,7 @@ def test_fp8_model_vs_fp32_restatement_512(dev, parity_log, convs):
     stats = dict(X_med=float(rel_X.median()), X_p99=float(rel_X.quantile(0.99)),
                  C_med=float(rel_C.median()), D_cos_med=float(cos_D.median()),
                  D_cos_min=float(cos_D.min()), Q_med=float(rel_Q.median()))
-    tag = "fp8-512-vs-fp32" + ("-convs" if convs else "")
+    tag = "fp8-512-vs-fp32" + ("-convs" if convs else "") + ("" if fold else "-unfolded")
     print(tag, stats)
     parity_log(tag, **stats)
     assert stats["X_med"] < (0.08 if convs else 0.06) and stats["C_med"] < 0.08, stats
@@ -878,6 +881,123 @@ def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi,
     assert _rel(out, ref) < 1e-2
 
 
+@pytest.mark.parametrize("fp8_in", [False, True])
+@pytest.mark.parametrize("tile", ["0", "12", "13", "15"])
+def test_gemm_ln_stats_fp8_copy(ops, dev, monkeypatch, fp8_in, tile):
+    """LN_STATS with ln_shift (ABI 0.5, the fp8 LayerNorm fold's producer): the copy C2 is
+    e4m3((x − shift[n])·qscale[g]) of the stored f32 x, shift / scale of weight batch
+    g % weight_mod; x and the statistics as without it.  Producers on bf16 operands (the
+    embeddings) and on e4m3 operands (proj / fc2 of the fp8 path); the ping-pong tile
+    (15) only takes bf16 operands (the fp8 dispatch maps it to the 128² tile)."""
+    from monst3r_slam_amd import _lib
+    if tile != "0":
+        monkeypatch.setenv("M3S_GEMM_TILE", tile)
+    M, N, K, batch = 768, 768, 1024, 4
+    g = torch.Generator(device=dev).manual_seed(31)
+    W = torch.randn(2, N, K, device=dev, generator=g) / K ** 0.5
+    kw = dict(sA=M * K, sB=N * K, sC=M * N, sBias=N, wmod=2)
+    if fp8_in:
+        A = _fp8(torch.randn(batch, M, K, device=dev, generator=g))
+        sw = W.abs().amax(-1) / 448.0
+        B = _fp8(W / sw[..., None])
+        prod = torch.stack([A[z].float() @ B[z % 2].float().t() * sw[z % 2] for z in range(batch)])
+        A, B = A.view(torch.uint8), B.view(torch.uint8)
+        kw["fp8"] = (sw.contiguous(), N)
+    else:
+        A = torch.randn(batch, M, K, device=dev, generator=g).bfloat16()
+        B = W.bfloat16()
+        prod = torch.stack([A[z].float() @ B[z % 2].float().t() for z in range(batch)])
+    bias = torch.randn(2, N, device=dev, generator=g)
+    x = torch.randn(batch, M, N, device=dev, generator=g) * 2.0 + 1.5
+    ref = x + prod + bias[torch.arange(batch, device=dev) % 2][:, None]
+    shift = (torch.randn(2, N, device=dev, generator=g) + 1.5).contiguous()
+    qs = torch.tensor([20.0, 35.0], device=dev)
+    xq = torch.empty(batch, M, N, device=dev, dtype=torch.uint8)
+    st = torch.full((batch, M, N // 128, 2), float("nan"), device=dev)
+    ops.gemm(A, B, x, M, N, K, batch, bias=bias, R=x, sR=M * N,
+             flags=_lib.EPI_OUT_F32 | _lib.EPI_RES_F32, ln_stats=(xq, st, shift, qs), **kw)
+    assert _rel(x, ref) < 1e-3
+    zi = torch.arange(batch, device=dev) % 2
+    _e4m3_close(xq, (x - shift[zi][:, None]) * qs[zi][:, None, None])
+    # the copy is RNE of the kernel's own x: exact but for the f32 (x − s)·q rounding
+    sr = _ln_stats_ref(x)
+    assert float((st[..., 0] - sr[..., 0]).abs().max()) < 1e-5 * float(x.abs().max())
+    assert float(((st[..., 1] - sr[..., 1]).abs() / sr[..., 1]).max()) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K,batch,axor,epi", [(768, 2304, 768, 4, 0, "rope"),
+                                                  (768, 3072, 768, 4, 0, "gelu8"),
+                                                  (1024, 4096, 1024, 1, 0, "gelu8"),
+                                                  (768, 1536, 768, 4, 1, "rope")])
+@pytest.mark.parametrize("tile", ["0", "2", "7", "12", "13"])
+def test_gemm_ln_fold_consumer_fp8(ops, dev, monkeypatch, M, N, K, batch, axor, epi, tile):
+    """LN_FOLD on e4m3 operands (ABI 0.5): A = e4m3((x − s)·q) (the producer's shifted copy),
+    B = the gamma-folded weight in e4m3 per row (scale sw), col_scale = sw / q and
+    c3 = W' s; the epilogue forms rstd (acc·cs + c3 − mean c1) + c2.  Against the same
+    e4m3 values in fp32 (products exact, f32 sums: 1e-3 bf16 out; e4m3 out within one
+    step), and — the point of the shift / c3 algebra — against torch fp32
+    LayerNorm → Linear of x itself within the fp8 quantisation error (5 % of the output
+    scale; 8 % for e4m3 outputs, whose own rounding is ±3 %)."""
+    from monst3r_slam_amd import _lib
+    from monst3r_slam_amd.model import ln_fold, LN_EPS, quant_e4m3
+    from oracle import vit_ref as V
+    if tile != "0":
+        monkeypatch.setenv("M3S_GEMM_TILE", tile)
+    g = torch.Generator(device=dev).manual_seed(13)
+    x = torch.randn(batch, M, K, device=dev, generator=g) * 1.5 + 0.7
+    x = x + 3.0 * torch.randn(batch, 1, K, device=dev, generator=g)     # per-channel offsets
+    gam = 1.0 + 0.3 * torch.randn(batch, K, device=dev, generator=g)
+    bet = 0.2 * torch.randn(batch, K, device=dev, generator=g)
+    Wt = torch.randn(batch, N, K, device=dev, generator=g) / K ** 0.5
+    b = torch.randn(batch, N, device=dev, generator=g)
+    wf, c1, c2 = ln_fold(Wt, b, gam, bet, dev)
+    q8, sw = quant_e4m3(wf)
+    zsrc = torch.arange(batch, device=dev) ^ axor        # output problem g reads A of g ^ axor
+    s = x.mean(1)                                        # [batch, K] per-problem channel means
+    qs = 448.0 / (2.0 * (x - s[:, None]).abs().amax((1, 2)))
+    xq = _fp8((x - s[:, None]) * qs[:, None, None])
+    cs = (sw / qs[zsrc][:, None]).contiguous()
+    c3 = torch.einsum("bnk,bk->bn", wf.double(), s[zsrc].double()).float().contiguous()
+    st = _ln_stats_ref(x).contiguous()
+    flags, kw, S = 0, {}, M
+    if epi == "rope":
+        kw["rope"] = (ops.rope_table(V.positions(1, 24, 32, dev)[0].contiguous(), 100.0),
+                      N // 2 if axor else 2 * N // 3, S)
+        out = torch.empty(batch, M, N, device=dev, dtype=torch.bfloat16)
+    else:
+        flags = _lib.EPI_GELU
+        kw["out_fp8"] = True
+        out = torch.empty(batch, M, N, device=dev, dtype=torch.uint8)
+    ops.gemm(xq.view(torch.uint8), q8, out, M, N, K, batch, sA=M * K, sB=N * K, sC=M * N,
+             bias=c2, sBias=N, flags=flags, fp8=(cs, N), ln_fold=(st, c1, axor, c3), **kw)
+    # the kernel's arithmetic on the same e4m3 values
+    mean = st[..., 0].mean(-1)
+    m2 = st[..., 1].sum(-1) + 128.0 * ((st[..., 0] - mean[..., None]) ** 2).sum(-1)
+    rstd = 1.0 / torch.sqrt(m2 / K + LN_EPS)
+    acc = torch.bmm(xq[zsrc].float(), q8.view(torch.float8_e4m3fn).float().transpose(1, 2))
+    y = rstd[zsrc][..., None] * (acc * cs[:, None] + c3[:, None] - mean[zsrc][..., None] * c1[:, None]) \
+        + c2[:, None]
+    # problem g normalises the rows of g ^ axor with ITS OWN gamma / beta (folded into W[g])
+    ln = F.layer_norm(x[zsrc], (K,), eps=LN_EPS) * gam[:, None] + bet[:, None]
+    true = torch.bmm(ln, Wt.transpose(1, 2)) + b[:, None]
+
+    def post(t):
+        if epi != "rope":
+            return F.gelu(t)
+        rc = kw["rope"][1]
+        r = t[..., :rc].reshape(batch, S, rc // 64, 64)
+        r = V.rope2d(r.transpose(1, 2), V.positions(batch, 24, 32, dev), 100.0).transpose(1, 2)
+        return torch.cat([r.reshape(batch, S, rc), t[..., rc:]], -1)
+    y, true = post(y), post(true)
+    if epi == "rope":
+        assert _rel(out, y) < 1e-2
+        got = out.float()
+    else:
+        _e4m3_close(out, y, extra=1e-3 * float(y.abs().max()))
+        got = out.view(torch.float8_e4m3fn).float()
+    assert _rel(got, true) < (0.05 if epi == "rope" else 0.08), _rel(got, true)
+
+
 @pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 @pytest.mark.parametrize("epi", ["gelu", "res", "tail"])
 def test_gemm_every_tile_config(ops, dev, monkeypatch, tile, epi):
@@ -1040,15 +1160,17 @@ def test_concurrent_encoder_tiles_match_table(dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("fp8", [False, "fold", "plain"])
 def test_decoder_split_by_model_matches_batched(dev, fp8):
     """dec_split (the two models' decoders as two batch-2 chains on two streams) against the
     batch-4 decoder: the same math on per-shape tiles that may split K differently, so
-    equal up to f32 summation order.  fp8: the unfolded (calibrated e4m3) decoder's split."""
+    equal up to f32 summation order.  fp8: the calibrated e4m3 decoder's split, with the
+    LayerNorms folded into the e4m3 projections (round 6 default) or as separate launches."""
     from monst3r_slam_amd import model as Mdl
     m, _ = Mdl.build(dev)
     if fp8:
         m.set_fp8(True)
+        m.fp8_fold = fp8 == "fold"
     g = torch.Generator(device=dev).manual_seed(9)
     img = torch.rand(1, 3, 384, 512, device=dev, generator=g) * 2 - 1
     feat_k = m.encode(torch.rand(1, 3, 384, 512, device=dev, generator=g) * 2 - 1)[0].clone()
