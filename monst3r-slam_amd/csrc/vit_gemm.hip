@@ -310,7 +310,9 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
   // needs the fused path (the reduce kernel has no fold)
   int fused = ln_fold ? 1 : (tuned ? tuned->fused : 0);
   if (const char* e = getenv("M3S_GEMM_FUSED")) fused = atoi(e) != 0 || ln_fold;  // tuning
-  const bool can_split = split_cfg && !f8 && !(d->flags & (M3S_EPI_CONVT | M3S_EPI_DPT_OUT)) &&
+  // (fp8: GEMM mode; the e4m3 tile set T64 / T128O2 / T128W8 / T256W8 / T128 all split)
+  const bool can_split = split_cfg && !(f8 && conv) &&
+                         !(d->flags & (M3S_EPI_CONVT | M3S_EPI_DPT_OUT)) &&
                          d->workspace &&
                          (!fused || (d->tile_counters && tiles_cfg <= (int64_t)d->tile_counters_len)) &&
                          (int64_t)splits * d->batch * d->M * d->N * 4 <= d->workspace_bytes;

@@ -1133,7 +1133,8 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_kernel(Args a) {
     const float* cs_g = a.cscale + gw * a.sCscale;
     // LN_FOLD consumer of a shifted e4m3 copy: + c3[n] = Σ_k shift[k] B[n][k] restores
     // Σ_k x[k] B[n][k] before the epilogue's rstd (acc − mean c1) + c2
-    const float* c3_g = a.ln_c3 ? a.ln_c3 + gw * a.sBias : nullptr;
+    // (split-K: the first split's partial carries it, so the sum adds it once)
+    const float* c3_g = (a.ln_c3 && split == 0) ? a.ln_c3 + gw * a.sBias : nullptr;
 #pragma unroll
     for (int j = 0; j < TN; j++) {
       const int n = n0 + wn * (BN / WN) + j * 32 + fr;
@@ -1614,9 +1615,27 @@ bool try_epi_b(Args& a, dim3 grid, hipStream_t s, int key) {
 // Implicit conv (MODE 1, C5's full-resolution DPT head convs, round 5): bf16 out (head.0)
 // and ReLU + the fused DPT tail (head.2).  The A operand is e4m3 NHWC and Cin arrives in
 // 2-byte units like K, so the tap / channel addressing is the bf16 kernel's unchanged.
-template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE>
+// SP: split-K (round 6: the residual GEMMs of the fp8 frame — N = 768 / 1024 at 1,024
+// tokens fill a quarter to half of the chip; partials are dequantised before the sum)
+template <int BM, int BN, int BK, int WM, int WN, int STAGES, int OCC, int MODE, bool SP = false>
 void launch_main_f8(Args& a, dim3 grid, hipStream_t s) {
   const int key = a.flags & ~(M3S_IN_FP8 | (a.bias ? 0 : M3S_EPI_BIAS));
+  if constexpr (SP) {
+    static_assert(MODE == 0, "fp8 split-K: GEMM mode");
+    constexpr int LS = M3S_EPI_LN_STATS | M3S_EPI_BIAS;
+    if (a.vec && try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_RES_F32 | M3S_EPI_OUT_F32,
+                         true, true>(a, grid, s, key))
+      return;
+    if (a.vec && key == (LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32)) {
+      hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true,
+                                      LS | M3S_EPI_RES_F32 | M3S_EPI_OUT_F32, true>),
+                         grid, dim3(WM * WN * 64), 0, s, a);
+      return;
+    }
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WM, WN, STAGES, OCC, 0, true, -1, true>), grid,
+                       dim3(WM * WN * 64), 0, s, a);
+    return;
+  }
   if (a.vec) {
     if constexpr (MODE == 0) {
       if (try_epi<BM, BN, BK, WM, WN, STAGES, OCC, 0, M3S_EPI_ROPE, true>(a, grid, s, key))
@@ -1723,10 +1742,13 @@ int launch(Args& a, int batch, hipStream_t s) {
   set_order(a, BM, BN, groups);
   if (split) {
     // split-K (fused last-split epilogue): 128^2 GEMM tiles, 64x128 GEMM / conv tiles
-    constexpr bool CAN = !F8 && ((BM == 128 && BN == 128 && BK == 64) ||
-                                 (BM == 64 && BN == 128 && BK == 64) ||
-                                 (BM == 256 && BN == 128 && BK == 64));
-    if constexpr (CAN) {
+    constexpr bool CAN = (BM == 128 && BN == 128 && BK == 64) ||
+                         (BM == 64 && BN == 128 && BK == 64) ||
+                         (BM == 256 && BN == 128 && BK == 64);
+    if constexpr (CAN && F8) {
+      if (a.mode != 0) return M3S_ERR_INVALID_ARG;
+      launch_main_f8<BM, BN, BK, WM, WN, STAGES, OCC, 0, true>(a, grid, s);
+    } else if constexpr (CAN) {
       if (a.mode == 0)
         launch_main<BM, BN, BK, WM, WN, STAGES, OCC, 0, true>(a, grid, s);
       else if (a.flags & M3S_PRO_RELU)

@@ -416,16 +416,21 @@ def _fp8(t):
                                               (200, 384, 256, 2, "plain"), (768, 1024, 4096, 1, "res"),
                                               (768, 2304, 768, 4, "rope")])
 @pytest.mark.parametrize("tile", ["0", "12", "13"])
-def test_gemm_fp8(ops, dev, monkeypatch, M, N, K, batch, mode, tile):
+@pytest.mark.parametrize("split", ["0", "3"])
+def test_gemm_fp8(ops, dev, monkeypatch, M, N, K, batch, mode, tile, split):
     """OCP e4m3 operands on the scaled 32x32x64 MFMA, per-column dequant scale, the ViT
     epilogue sets (GELU → fp8 out, f32 residual incl. split-K, RoPE), weight_mod batches.
     Reference: the same e4m3 values in fp32 (products exact, f32 sums: tolerance 1e-3;
     fp8 outputs compared after the same e4m3 rounding of the reference: 1 ulp ≈ 2^-3).
-    tile: the table / heuristic (0), or the 8-wave 128x128 / 256x128 configurations."""
+    tile: the table / heuristic (0), or the 8-wave 128x128 / 256x128 configurations.
+    split "3": K over 3 workgroups per tile (round 6), partials dequantised, summed in
+    split order by the last split (fused) or the reduce kernel (per the table)."""
     from monst3r_slam_amd import _lib
     from oracle import vit_ref as V
     if tile != "0":
         monkeypatch.setenv("M3S_GEMM_TILE", tile)
+    if split != "0":
+        monkeypatch.setenv("M3S_GEMM_SPLITS", split)
     g = torch.Generator(device=dev).manual_seed(21)
     A = _fp8(torch.randn(batch, M, K, device=dev, generator=g))
     W = torch.randn(2, N, K, device=dev, generator=g) / K ** 0.5
@@ -883,15 +888,20 @@ def test_gemm_ln_fold_consumer(ops, dev, monkeypatch, M, N, K, batch, axor, epi,
 
 @pytest.mark.parametrize("fp8_in", [False, True])
 @pytest.mark.parametrize("tile", ["0", "12", "13", "15"])
-def test_gemm_ln_stats_fp8_copy(ops, dev, monkeypatch, fp8_in, tile):
+@pytest.mark.parametrize("split", ["0", "2f", "3"])
+def test_gemm_ln_stats_fp8_copy(ops, dev, monkeypatch, fp8_in, tile, split):
     """LN_STATS with ln_shift (ABI 0.5, the fp8 LayerNorm fold's producer): the copy C2 is
     e4m3((x − shift[n])·qscale[g]) of the stored f32 x, shift / scale of weight batch
     g % weight_mod; x and the statistics as without it.  Producers on bf16 operands (the
     embeddings) and on e4m3 operands (proj / fc2 of the fp8 path); the ping-pong tile
-    (15) only takes bf16 operands (the fp8 dispatch maps it to the 128² tile)."""
+    (15) only takes bf16 operands (the fp8 dispatch maps it to the 128² tile).  split: K
+    over 2 (fused last-split epilogue, "2f") or 3 (reduce kernel) workgroups per tile."""
     from monst3r_slam_amd import _lib
     if tile != "0":
         monkeypatch.setenv("M3S_GEMM_TILE", tile)
+    if split != "0":
+        monkeypatch.setenv("M3S_GEMM_SPLITS", split[0])
+        monkeypatch.setenv("M3S_GEMM_FUSED", "1" if split.endswith("f") else "0")
     M, N, K, batch = 768, 768, 1024, 4
     g = torch.Generator(device=dev).manual_seed(31)
     W = torch.randn(2, N, K, device=dev, generator=g) / K ** 0.5
@@ -930,19 +940,23 @@ def test_gemm_ln_stats_fp8_copy(ops, dev, monkeypatch, fp8_in, tile):
                                                   (1024, 4096, 1024, 1, 0, "gelu8"),
                                                   (768, 1536, 768, 4, 1, "rope")])
 @pytest.mark.parametrize("tile", ["0", "2", "7", "12", "13"])
-def test_gemm_ln_fold_consumer_fp8(ops, dev, monkeypatch, M, N, K, batch, axor, epi, tile):
+@pytest.mark.parametrize("split", ["0", "3"])
+def test_gemm_ln_fold_consumer_fp8(ops, dev, monkeypatch, M, N, K, batch, axor, epi, tile, split):
     """LN_FOLD on e4m3 operands (ABI 0.5): A = e4m3((x − s)·q) (the producer's shifted copy),
     B = the gamma-folded weight in e4m3 per row (scale sw), col_scale = sw / q and
     c3 = W' s; the epilogue forms rstd (acc·cs + c3 − mean c1) + c2.  Against the same
     e4m3 values in fp32 (products exact, f32 sums: 1e-3 bf16 out; e4m3 out within one
     step), and — the point of the shift / c3 algebra — against torch fp32
     LayerNorm → Linear of x itself within the fp8 quantisation error (5 % of the output
-    scale; 8 % for e4m3 outputs, whose own rounding is ±3 %)."""
+    scale; 8 % for e4m3 outputs, whose own rounding is ±3 %).  split "3": K over 3
+    workgroups, c3 carried by the first split's partial, the fold by the last split."""
     from monst3r_slam_amd import _lib
     from monst3r_slam_amd.model import ln_fold, LN_EPS, quant_e4m3
     from oracle import vit_ref as V
     if tile != "0":
         monkeypatch.setenv("M3S_GEMM_TILE", tile)
+    if split != "0":
+        monkeypatch.setenv("M3S_GEMM_SPLITS", split)
     g = torch.Generator(device=dev).manual_seed(13)
     x = torch.randn(batch, M, K, device=dev, generator=g) * 1.5 + 0.7
     x = x + 3.0 * torch.randn(batch, 1, K, device=dev, generator=g)     # per-channel offsets
