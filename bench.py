@@ -292,13 +292,21 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
     blog = torch.zeros((nlog, 8), dtype=torch.int64, device=dev)
     bcnt = torch.zeros(2, dtype=torch.int32, device=dev)
 
+    ops = loop.tr.model.ops
+    epi_bytes = []       # per captured step: algorithmic bytes incl. the epilogue operands
+
     def cap_tl(k):
         from monst3r_slam_amd.capture import capture_graph, check_topology
         # warm / allocate outside the timeline's slot range, with the step's fork / join
         # structure and width checked before the capture (TopologyError, not a crash)
         check_topology(lambda: loop.step(k), dev)
         n0 = int(lib.m3s_timeline_count())
-        g = capture_graph(lambda: loop.step(k), dev, warmup=False)
+        ops.record = []          # the captured step's own GEMM descriptors (flags included)
+        try:
+            g = capture_graph(lambda: loop.step(k), dev, warmup=False)
+        finally:
+            rec, ops.record = ops.record, None
+        epi_bytes.append((len(rec), sum(_epilogue_bytes(d) for d, _, _ in rec)))
         return g, n0, int(lib.m3s_timeline_count())
 
     _lib.check(lib.m3s_timeline_set(P(buf), cap), "timeline_set")   # zeroes the headers
@@ -375,6 +383,8 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
 
     res = {"replays": len(rows), "step_ms": med(lambda r: r["step_ms"]),
            "cu_occupancy": occ,
+           "gemm_algorithmic_bytes_with_epilogue": float(np.median([b for _, b in epi_bytes])),
+           "gemm_recorded_launches": float(np.median([n for n, _ in epi_bytes])),
            "span_ms": med(lambda r: r["span_ms"]),
            "gemm_or_attn_union_ms": med(lambda r: r["busy_union_ms"])}
     for name in ("gemm", "attn"):
@@ -398,6 +408,35 @@ def step_timeline(loop, dev, rounds=3, pairs=4, out_path=None):
             json.dump(js, fh)
     del graphs
     return res
+
+
+def _epilogue_bytes(d):
+    """Algorithmic bytes of one GEMM descriptor with its epilogue operands at their stored
+    types: A (an implicit 3x3 conv's input image once: M·K/9 elements) and B once, bf16 (e4m3:
+    1 B); C once at its stored type (f32 4, bf16 2, e4m3 1; the fused DPT tail writes 16 B
+    of points + confidence per row instead); a residual read (f32 4 / bf16 2 B); LN_STATS:
+    the copy for the LayerNorm-fold consumer (bf16 2 / e4m3 1 B) + 8 B of statistics per
+    128 columns; LN_FOLD: the producer's statistics read (8 B per 128 K-columns).  What the
+    reference's own fp32 residual stream and LayerNorm read / write are counted; split-K
+    partials and re-reads are not (they are what the measured traffic adds on top)."""
+    from monst3r_slam_amd import _lib
+    M, N, K, b, f = d.M, d.N, d.K, d.batch, d.flags
+    ab = 1 if f & _lib.IN_FP8 else 2
+    ka = K / 9.0 if d.mode == 1 else K
+    byt = (M * ka + N * K) * ab
+    if f & _lib.EPI_DPT_OUT:
+        byt += M * 16
+    else:
+        byt += M * N * (4 if f & _lib.EPI_OUT_F32 else 1 if f & _lib.EPI_OUT_FP8 else 2)
+    if f & _lib.EPI_RES_F32:
+        byt += M * N * 4
+    elif f & _lib.EPI_RES_BF16:
+        byt += M * N * 2
+    if f & _lib.EPI_LN_STATS:
+        byt += M * N * (1 if d.ln_shift else 2) + M * (N // 128) * 8
+    if f & _lib.EPI_LN_FOLD:
+        byt += M * (K // 128) * 8
+    return float(byt * b)
 
 
 def gemm_replay(model, run, dev, reps=20):
@@ -493,6 +532,14 @@ def roofline_entry(tl, roof, pmc, mfma, step_ms):
                                    "((M·K + N·K + M·N)·batch·2 B per launch, step_timeline dims; "
                                    "an implicit 3x3 conv reads its input image once: M·K/9 "
                                    "for A)")
+    if tl.get("gemm_algorithmic_bytes_with_epilogue"):
+        e["algorithmic_bytes_with_epilogue_per_step"] = tl["gemm_algorithmic_bytes_with_epilogue"]
+        e["algorithmic_bytes_with_epilogue_rule"] = (
+            "the floor with each launch's epilogue operands at their stored types: f32 "
+            "residual read + f32 / bf16 / e4m3 C, the LayerNorm-fold copy + statistics, the "
+            "DPT tail's points / confidence (bench._epilogue_bytes over the step's own "
+            "recorded descriptors, " + str(int(tl.get("gemm_recorded_launches") or 0)) +
+            " launches)")
     if mfma:
         # the PMC pass ran on the box that committed it (its own untraced step time), this
         # line may run on another: both step times, and the utilisation at each
@@ -511,6 +558,9 @@ def roofline_entry(tl, roof, pmc, mfma, step_ms):
                                  + mfma.get("source", "") + ")")
             e["traffic_per_step_bytes"] = hb["bytes"]
             e["traffic_vs_algorithmic"] = hb["bytes"] / g["algorithmic_bytes"]
+            if e.get("algorithmic_bytes_with_epilogue_per_step"):
+                e["traffic_vs_algorithmic_with_epilogue"] = (
+                    hb["bytes"] / e["algorithmic_bytes_with_epilogue_per_step"])
             e.pop("traffic_per_pair_bytes", None)
             e.pop("l2_hit_rate", None)
     return e
