@@ -258,6 +258,13 @@ extern "C" int m3s_vit_gemm(const m3s_gemm_desc* d, void* stream) {
     // the short-K latency regime comes sooner; 64x128 tiles at 2/CU win below ~1.5 waves
     // of 128^2 tiles, 2 x 128^2 per CU above (1.96 PFLOP/s on 4096^3)
     cfg = tiles128 >= 400 ? T128O2 : T64;
+  } else if (cfg == 0 && !conv && eK >= 512 &&
+             (int64_t)((d->M + 255) / 256) * ((d->N + 255) / 256) * d->batch >= 256 &&
+             !(d->flags & (M3S_EPI_DPT_OUT | M3S_EPI_CONVT | M3S_EPI_OUT_FP8))) {
+    // a GEMM with at least a full wave of 256^2 tiles and K >= 512 that the table does not
+    // name: the ping-pong tile (tools/gemm_pp_bench.py, r06_pp_orders.txt: 4096^3 1083 ->
+    // 1431 TF/s, 8192^3 892 -> 1511 TF/s; every model shape of that size is in the table)
+    cfg = T256PP;
   } else if (cfg == 0) {
     // measured on the pair shapes (tools/gemm_tune.py): 2 x 128^2 blocks per CU win for
     // wide convs with several waves of tiles, for one-to-two waves of short-K GEMM tiles,
