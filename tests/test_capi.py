@@ -59,3 +59,29 @@ def test_dropin_module_surface():
     x = torch.zeros(1, 4, 4, 9)[..., ::1].transpose(1, 2)
     with pytest.raises(RuntimeError, match="must be contiguous"):
         mb.iter_proj(x, torch.zeros(1, 16, 3), torch.zeros(1, 16, 2), 10, 1e-8, 1e-6)
+
+
+def test_gemm_desc_layout_matches_header(tmp_path):
+    """The ctypes mirror of m3s_gemm_desc (_lib.GemmDesc) has the C header's size and field
+    offsets (gcc on include/monst3r_slam_amd.h): a drifted mirror would hand the library
+    garbage in the fields past the first mismatch (ABI 0.5 appended ln_c3 / ln_shift /
+    ln_qscale)."""
+    import shutil
+    import subprocess
+    from monst3r_slam_amd import _lib
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    names = [f[0] for f in _lib.GemmDesc._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "monst3r_slam_amd.h"\n'
+                   "int main(void) {\n"
+                   '  printf("%zu\\n", sizeof(m3s_gemm_desc));\n' +
+                   "".join(f'  printf("%zu\\n", offsetof(m3s_gemm_desc, {n}));\n' for n in names) +
+                   "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True,
+                                          text=True).stdout.split()]
+    assert out[0] == ctypes.sizeof(_lib.GemmDesc)
+    assert out[1:] == [getattr(_lib.GemmDesc, n).offset for n in names]
