@@ -164,7 +164,8 @@ __device__ __forceinline__ void store_bf16x8(bf16_t* p, const float* x) {
 // the per-channel calibrated shift centring each channel before the 3-bit mantissa.
 // ln_c2_operands loads a thread's 8 shifts + the scale once, ahead of the epilogue's
 // stores: a load issued between them would wait for every store before it (vmcnt counts
-// both), one memory round trip per row vector (enc fc2 15.7 → 22.8 us measured so)
+// both), one memory round trip per row vector.  (Measured cost of the whole LN_STATS
+// epilogue on the 1,024-token residual GEMMs: 0.6-2.4 us per launch, tools/ls_cost_probe.py)
 __device__ __forceinline__ void ln_c2_operands(const Args& a, int64_t g, int n, float* sh,
                                                float& q) {
   const int64_t gw = a.wmod > 0 ? g % a.wmod : g;
